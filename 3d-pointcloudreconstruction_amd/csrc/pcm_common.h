@@ -1,0 +1,56 @@
+// pcm_common.h -- shared device helpers for the gfx950 point-set metric kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "pcm.h"
+
+#define PCM_INF __builtin_huge_valf()
+
+typedef float pcm_f2 __attribute__((ext_vector_type(2)));
+typedef float pcm_f4 __attribute__((ext_vector_type(4)));
+
+// Squared distance in the pinned evaluation order shared with the oracle
+// (oracle/pcm_oracle.c: sqd_pinned) -- NVCC's contraction of the reference
+// expression x2*x2+y2*y2+z2*z2 (chamfer3D.cu:35).  Explicit fmas, so the
+// result does not depend on -ffp-contract.
+__device__ __forceinline__ float pcm_sqd(float dx, float dy, float dz) {
+    return __builtin_fmaf(dz, dz, __builtin_fmaf(dy, dy, dx * dx));
+}
+
+__device__ __forceinline__ pcm_f2 pcm_sqd2(pcm_f2 dx, pcm_f2 dy, pcm_f2 dz) {
+    return __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
+}
+
+__device__ __forceinline__ bool pcm_finite(float v) {
+    return __builtin_isfinite(v);
+}
+
+// Reference-exact single-query scan (NmDistanceKernel, chamfer3D.cu:12-134):
+// 512-point tiles, best = d(first) per tile, strict '<' inside, strict '>'
+// across tiles.  Used only when non-finite coordinates are present, where the
+// tile boundaries decide which NaN wins.  `t` = target cloud [m,3] in global.
+__device__ inline void pcm_ref_nn_scan(float x1, float y1, float z1, const float *__restrict__ t,
+                                       int m, float &out_d, int &out_i) {
+    float res = 0.f;
+    int res_i = 0;
+    for (int k2 = 0; k2 < m; k2 += 512) {
+        const int end_k = min(m, k2 + 512) - k2;
+        float best = 0.f;
+        int best_i = 0;
+        for (int k = 0; k < end_k; ++k) {
+            const float *q = t + 3 * (size_t)(k2 + k);
+            const float d = pcm_sqd(q[0] - x1, q[1] - y1, q[2] - z1);
+            if (k == 0 || d < best) { best = d; best_i = k + k2; }
+        }
+        if (k2 == 0 || res > best) { res = best; res_i = best_i; }
+    }
+    out_d = res;
+    out_i = res_i;
+}
+
+static inline int pcm_launch_status() {
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? PCM_OK : PCM_ERR_LAUNCH;
+}

@@ -1,0 +1,73 @@
+"""Chamfer3D autograd wrapper -- drop-in for metric/chamfer3D/dist_chamfer_3D.py.
+
+Same module name, classes and signatures as the reference
+(dist_chamfer_3D.py:29-81): ``chamfer_3DFunction.forward(ctx, xyz1, xyz2) ->
+(dist1, dist2, idx1, idx2)``, ``.backward(ctx, graddist1, graddist2, gradidx1,
+gradidx2) -> (gradxyz1, gradxyz2)`` and ``chamfer_3DDist()(input1, input2)``.
+Outputs keep the reference dtypes: float32 distances, int32 indices.
+
+Differences, all on the "stricter" side:
+  * outputs are allocated directly on the device (the reference built them on
+    the CPU and copied, dist_chamfer_3D.py:40-49, 63-67);
+  * kernels run on PyTorch's current stream under a device guard instead of
+    the legacy default stream + a global ``torch.cuda.set_device`` (:50);
+  * a non-zero library status raises instead of being ignored (:52, :68).
+Compute always goes through libpcm_hip.so; CPU tensors raise (the reference
+was GPU-only too: "GPU tensors only", :27).
+"""
+import os
+import sys
+
+import torch
+from torch import nn
+from torch.autograd import Function
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import pcm_hip  # noqa: E402
+
+
+class chamfer_3DFunction(Function):
+    @staticmethod
+    def forward(ctx, xyz1, xyz2):
+        batchsize, n, dim = xyz1.size()
+        assert dim == 3, "Wrong last dimension for the chamfer distance 's input! Check with .size()"
+        _, m, dim = xyz2.size()
+        assert dim == 3, "Wrong last dimension for the chamfer distance 's input! Check with .size()"
+        assert xyz2.size(0) == batchsize, "batch sizes of the two clouds differ"
+        if xyz1.dtype != torch.float32 or xyz2.dtype != torch.float32:
+            # the reference read Tensor::data<float>() and threw otherwise
+            raise TypeError("chamfer_3DFunction expects float32 clouds")
+        xyz1 = xyz1.contiguous()
+        xyz2 = xyz2.contiguous()
+        device = xyz1.device
+        dist1 = torch.zeros(batchsize, n, device=device)
+        dist2 = torch.zeros(batchsize, m, device=device)
+        idx1 = torch.zeros(batchsize, n, dtype=torch.int32, device=device)
+        idx2 = torch.zeros(batchsize, m, dtype=torch.int32, device=device)
+        pcm_hip.chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2)
+        ctx.save_for_backward(xyz1, xyz2, idx1, idx2)
+        ctx.mark_non_differentiable(idx1, idx2)
+        return dist1, dist2, idx1, idx2
+
+    @staticmethod
+    def backward(ctx, graddist1, graddist2, gradidx1, gradidx2):
+        xyz1, xyz2, idx1, idx2 = ctx.saved_tensors
+        # autograd hands None for an unused output
+        graddist1 = (torch.zeros_like(idx1, dtype=torch.float32) if graddist1 is None
+                     else graddist1.contiguous().float())
+        graddist2 = (torch.zeros_like(idx2, dtype=torch.float32) if graddist2 is None
+                     else graddist2.contiguous().float())
+        gradxyz1 = torch.empty_like(xyz1)
+        gradxyz2 = torch.empty_like(xyz2)
+        pcm_hip.chamfer_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
+        return gradxyz1, gradxyz2
+
+
+class chamfer_3DDist(nn.Module):
+    def __init__(self):
+        super(chamfer_3DDist, self).__init__()
+
+    def forward(self, input1, input2):
+        input1 = input1.contiguous()
+        input2 = input2.contiguous()
+        return chamfer_3DFunction.apply(input1, input2)

@@ -1,0 +1,137 @@
+"""ctypes binding of libpcm_hip.so (the gfx950 HIP kernels behind include/pcm.h).
+
+This is the product path's only route to compute: there is no CPU fallback.
+If the library is missing, or a tensor is not on a HIP device, every entry
+point raises.  Kernels are enqueued on PyTorch's *current* stream of the
+tensors' device (the reference launched on the legacy default stream,
+chamfer3D.cu:142-143 -- SURVEY.md appendix A.5).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get(
+    "PCM_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libpcm_hip.so"))
+
+_lib = None
+
+# every symbol include/pcm.h declares (checked by tests/test_capi.py)
+EXPORTED = (
+    "pcm_version", "pcm_strerror",
+    "pcm_chamfer_forward", "pcm_chamfer_backward",
+    "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward",
+)
+
+
+class PcmError(RuntimeError):
+    """A libpcm_hip call returned a non-zero pcm_status."""
+
+
+def load_library():
+    """Load libpcm_hip.so (raises OSError with the path if it is missing)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise OSError(
+            f"libpcm_hip.so not found at {LIB_PATH}; build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C "
+            "3d-pointcloudreconstruction_amd/csrc`")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, ci, cf, cs = ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+    L.pcm_version.restype = ci
+    L.pcm_version.argtypes = []
+    L.pcm_strerror.restype = ctypes.c_char_p
+    L.pcm_strerror.argtypes = [ci]
+    L.pcm_chamfer_forward.restype = ci
+    L.pcm_chamfer_forward.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
+    L.pcm_chamfer_backward.restype = ci
+    L.pcm_chamfer_backward.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
+    L.pcm_emd_workspace_bytes.restype = cs
+    L.pcm_emd_workspace_bytes.argtypes = [ci, ci]
+    L.pcm_emd_forward.restype = ci
+    L.pcm_emd_forward.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, vp, cs, vp]
+    L.pcm_emd_backward.restype = ci
+    L.pcm_emd_backward.argtypes = [vp, vp, ci, ci, vp, vp, vp, vp]
+    _lib = L
+    return L
+
+
+def strerror(status: int) -> str:
+    return load_library().pcm_strerror(int(status)).decode()
+
+
+def _check(status: int, what: str) -> None:
+    if status != 0:
+        raise PcmError(f"{what} failed: {strerror(status)} (status {status})")
+
+
+def _require_device(*tensors: torch.Tensor) -> torch.device:
+    dev = tensors[0].device
+    for t in tensors:
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                "pcm_hip kernels need HIP device tensors (got a tensor on "
+                f"{t.device}); there is no CPU path")
+        if t.device != dev:
+            raise RuntimeError(f"tensors on different devices: {dev} vs {t.device}")
+    return dev
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _stream(dev: torch.device):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:
+    """pcm_chamfer_forward on contiguous [B,N,3]/[B,M,3] float32 device tensors."""
+    dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_chamfer_forward(
+            _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
+            _stream(dev)), "pcm_chamfer_forward")
+
+
+def chamfer_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2) -> None:
+    dev = _require_device(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_chamfer_backward(
+            _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(graddist1), _ptr(graddist2), _ptr(idx1),
+            _ptr(idx2), _ptr(gradxyz1), _ptr(gradxyz2), _stream(dev)), "pcm_chamfer_backward")
+
+
+def emd_workspace_bytes(b: int, n: int) -> int:
+    return int(load_library().pcm_emd_workspace_bytes(b, n))
+
+
+def emd_forward(xyz1, xyz2, eps: float, iters: int, dist, assignment, price=None,
+                workspace=None) -> None:
+    dev = _require_device(xyz1, xyz2, dist, assignment)
+    b, n, _ = xyz1.shape
+    ws_bytes = emd_workspace_bytes(b, n)
+    if ws_bytes and (workspace is None or workspace.numel() * workspace.element_size() < ws_bytes):
+        workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_emd_forward(
+            _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
+            _ptr(price), _ptr(workspace), ws_bytes, _stream(dev)), "pcm_emd_forward")
+
+
+def emd_backward(xyz1, xyz2, graddist, assignment, gradxyz1) -> None:
+    dev = _require_device(xyz1, xyz2, graddist, assignment, gradxyz1)
+    b, n, _ = xyz1.shape
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_emd_backward(
+            _ptr(xyz1), _ptr(xyz2), b, n, _ptr(graddist), _ptr(assignment), _ptr(gradxyz1),
+            _stream(dev)), "pcm_emd_backward")

@@ -1,0 +1,49 @@
+"""Host-side behaviour of the reference-compatible Python API (no GPU).
+
+The product path has no CPU fallback: CPU tensors must raise, not compute.
+Shape/contract checks mirror the reference's asserts
+(dist_chamfer_3D.py:33-35, emd_module.py:36-39)."""
+import pytest
+import torch
+
+
+def test_chamfer_rejects_cpu_tensors():
+    import dist_chamfer_3D
+    with pytest.raises(RuntimeError, match="HIP device"):
+        dist_chamfer_3D.chamfer_3DDist()(torch.rand(2, 8, 3), torch.rand(2, 9, 3))
+
+
+def test_chamfer_rejects_wrong_last_dim():
+    import dist_chamfer_3D
+    with pytest.raises(AssertionError):
+        dist_chamfer_3D.chamfer_3DDist()(torch.rand(2, 8, 2), torch.rand(2, 9, 3))
+    with pytest.raises(AssertionError):
+        dist_chamfer_3D.chamfer_3DDist()(torch.rand(2, 8, 3), torch.rand(2, 9, 4))
+
+
+def test_chamfer_rejects_non_float32():
+    import dist_chamfer_3D
+    with pytest.raises(TypeError):
+        dist_chamfer_3D.chamfer_3DFunction.apply(torch.rand(2, 8, 3).double(), torch.rand(2, 9, 3))
+
+
+def test_emd_contract_asserts():
+    import emd_module
+    m = emd_module.emdModule()
+    with pytest.raises(AssertionError):
+        m(torch.rand(2, 1000, 3), torch.rand(2, 1000, 3), 0.005, 50)      # N % 1024
+    with pytest.raises(AssertionError):
+        m(torch.rand(2, 1024, 3), torch.rand(3, 1024, 3), 0.005, 50)      # batch mismatch
+    with pytest.raises(AssertionError):
+        m(torch.rand(513, 1024, 3), torch.rand(513, 1024, 3), 0.005, 50)  # B <= 512
+    with pytest.raises(RuntimeError, match="HIP device"):
+        m(torch.rand(2, 1024, 3), torch.rand(2, 1024, 3), 0.005, 50)
+
+
+def test_modules_have_reference_names():
+    import dist_chamfer_3D
+    import emd_module
+    for name in ("chamfer_3DFunction", "chamfer_3DDist"):
+        assert hasattr(dist_chamfer_3D, name)
+    for name in ("emdFunction", "emdModule"):
+        assert hasattr(emd_module, name)

@@ -1,47 +1,64 @@
 // chamfer.hip -- Chamfer3D forward/backward for MI355X (gfx950, CDNA4).
 //
 // Replaces the reference's NmDistanceKernel / NmDistanceGradKernel
-// (metric/chamfer3D/chamfer3D.cu:12-195).  Design:
+// (metric/chamfer3D/chamfer3D.cu:12-195).  DESIGN.md section 3 has the full
+// rationale and the roofline; in short:
 //
 // Forward: ONE launch computes both directions.  A workgroup owns 64*QPT query
 // points of one (direction, batch) and W waves; the opposing cloud is staged
-// through LDS in SoA tiles (X[], Y[], Z[] so one ds_read_b128 broadcast yields
+// through LDS in SoA tiles (X[], Y[], Z[]: one ds_read_b128 broadcast yields
 // four candidates' x), and each wave scans an interleaved 1/W share of the
 // tile's chunks of C candidates.  Distances are evaluated two candidates at a
-// time in packed-fp32 (v_pk_add/mul/fma_f32) in the pinned order
-// fma(dz,dz,fma(dy,dy,dx*dx)); a chunk's minimum is folded with v_min3_f32
-// and only the chunk id of the running minimum is tracked (strict '<', so the
-// lowest chunk wins).  After the waves' (min, chunk) pairs are merged
-// lexicographically, the single winning chunk is re-scanned to recover the
-// lowest index attaining the minimum -- bit-identical to the reference's
-// lowest-index first-min scan, at ~1/C of the compare/select cost.
-// Non-finite coordinates (where the reference's 512-point tile boundaries
-// decide NaN outcomes) divert the whole workgroup to a reference-exact scan.
+// time in packed fp32 (v_pk_add/mul/fma_f32 -- measured 2x the scalar rate on
+// MI355X) in the pinned order fma(dz,dz,fma(dy,dy,dx*dx)); a chunk's minimum
+// is folded with v_min3_f32 and only the chunk id of the running minimum is
+// tracked (strict '<': the lowest chunk wins).  After the waves' (min, chunk)
+// pairs are merged lexicographically, the single winning chunk is re-scanned
+// (from LDS, all threads, branch-free) for the lowest index attaining the
+// minimum -- bit-identical to the reference's lowest-index first-min scan at
+// ~1/C of its compare/select cost.  Non-finite coordinates (where the
+// reference's 512-point tile boundaries decide NaN outcomes) divert the
+// workgroup to a reference-exact scan.  Optionally (kLoss) the epilogue also
+// produces mean(dist1), mean(dist2) (loss/loss.py:36) deterministically:
+// per-workgroup partial sums + an arrival ticket, the last workgroup sums the
+// partials in a fixed order.
 //
-// Backward: deterministic.  A workgroup owns up to 1024 points of one cloud;
-// it gathers the direct term and sums the reverse-direction scatter terms in
-// ascending source index, using an LDS counting sort of the other
-// direction's argmin indices (no float atomics).
+// Backward: deterministic.  A workgroup owns kBwdT points of one cloud; it
+// gathers the direct term and sums the reverse-direction scatter terms in
+// ascending source index (LDS counting sort of the other direction's argmins,
+// no float atomics), in the reference's kernel order (chamfer3D.cu:184-185).
 #include "pcm_common.h"
+#include "pcm_internal.h"
 
 namespace {
 
-constexpr int kFwdW = 4;      // waves per workgroup (split the candidate chunks)
-constexpr int kFwdQPT = 2;    // query points per lane
-constexpr int kFwdC = 32;     // candidates per chunk
-constexpr int kFwdTile = 2048;  // candidates per LDS tile (3 x 8 KiB)
+constexpr int kTile = 2048;  // candidates per LDS tile (3 x 8 KiB SoA)
+constexpr int kChunk = 32;   // candidates per chunk (rescan granularity)
 
-template <int W, int QPT, int C, int TILE>
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+template <int W, int QPT, int C, int TILE, bool kLoss>
 __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1,
-    int32_t *__restrict__ idx2, int nblk1, int nblk2) {
+    int32_t *__restrict__ idx2, int nblk1, int nblk2, float *__restrict__ partials,
+    unsigned *__restrict__ ticket, float *__restrict__ mean_out) {
     static_assert(TILE % C == 0 && C % 4 == 0, "tile must hold whole chunks");
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
+    constexpr int PARTS = (NT / QW) > 0 ? (NT / QW) : 1;  // rescan splits per query
+    constexpr int CP = C / PARTS;
+    static_assert(C % PARTS == 0, "chunk must split evenly");
     __shared__ __attribute__((aligned(16))) float sXYZ[3][TILE];
     __shared__ float sBest[W][QW];
     __shared__ int sChunk[W][QW];
+    __shared__ int sHit[PARTS][QW];
+    __shared__ float sRed[2][W];
+    __shared__ int sLast;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -101,18 +118,26 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
     for (int t0 = 0; t0 < nt; t0 += TILE) {
         const int cnt = min(TILE, nt - t0);
         const int padded = (cnt + C - 1) / C * C;
-        __syncthreads();  // previous tile fully consumed
-        // coalesced flat read of the AoS tile, scattered to SoA; pad = +inf
+        if (t0 > 0) __syncthreads();  // previous tile fully consumed
+        // coalesced flat read of the AoS tile, scattered to SoA; pad = +inf.
+        // All of a thread's loads are issued before any LDS write, so the
+        // tile costs one memory latency, not one per element.
         const float *src = T + 3 * (size_t)t0;
-        for (int f = tid; f < 3 * padded; f += NT) {
-            const int p = f / 3;
-            const int comp = f - 3 * p;
-            float v = PCM_INF;
-            if (p < cnt) {
-                v = src[f];
-                nonfinite |= !pcm_finite(v);
+        constexpr int kFill = (3 * TILE + NT - 1) / NT;
+        float v[kFill];
+#pragma unroll
+        for (int r = 0; r < kFill; ++r) {
+            const int f = tid + r * NT;
+            v[r] = (f < 3 * cnt) ? src[f] : PCM_INF;
+        }
+#pragma unroll
+        for (int r = 0; r < kFill; ++r) {
+            const int f = tid + r * NT;
+            if (f < 3 * padded) {
+                const int p = f / 3;
+                nonfinite |= (f < 3 * cnt) && !pcm_finite(v[r]);
+                sXYZ[f - 3 * p][p] = v[r];
             }
-            sXYZ[comp][p] = v;
         }
         __syncthreads();
 
@@ -137,8 +162,9 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
                 for (int qq = 0; qq < QPT; ++qq) {
                     const pcm_f2 da = pcm_sqd2(xa - px[qq], ya - py[qq], za - pz[qq]);
                     const pcm_f2 db = pcm_sqd2(xb - px[qq], yb - py[qq], zb - pz[qq]);
-                    mn[qq] = __builtin_fminf(mn[qq], __builtin_fminf(da.x, da.y));
-                    mn[qq] = __builtin_fminf(mn[qq], __builtin_fminf(db.x, db.y));
+                    // written so that hipcc forms two v_min3_f32 per 4 candidates
+                    mn[qq] = __builtin_fminf(__builtin_fminf(mn[qq], da.x), da.y);
+                    mn[qq] = __builtin_fminf(__builtin_fminf(mn[qq], db.x), db.y);
                 }
             }
 #pragma unroll
@@ -151,56 +177,468 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
         }
     }
 
-    // ---- merge the W waves' (min, chunk) per query; recover the lowest index
+    // ---- merge the W waves' (min, chunk) per query
 #pragma unroll
     for (int qq = 0; qq < QPT; ++qq) {
         sBest[wave][qq * 64 + lane] = best[qq];
         sChunk[wave][qq * 64 + lane] = bchunk[qq];
     }
     const int any_nonfinite = __syncthreads_or(nonfinite ? 1 : 0);
-    if (nt == 0) return;  // reference leaves outputs untouched when m == 0
 
-    for (int s = tid; s < QW; s += NT) {
-        const int qi = qbase + s;
-        if (qi >= nq) continue;
-        const float x = Q[3 * (size_t)qi + 0];
-        const float y = Q[3 * (size_t)qi + 1];
-        const float z = Q[3 * (size_t)qi + 2];
-        float d;
-        int idx;
-        if (any_nonfinite) {
-            pcm_ref_nn_scan(x, y, z, T, nt, d, idx);
-        } else {
+    float my_d = 0.f;  // dist of the query this thread finalises (kLoss sum)
+    if (!any_nonfinite) {
+        // ---- rescan the winning chunk for the lowest index attaining the min.
+        // Every thread takes one (query, part) pair; candidates come from the
+        // LDS tile when the whole target cloud was one tile, else from global.
+        const bool resident = nt <= TILE;
+        for (int item = tid; item < QW * PARTS; item += NT) {
+            const int s = item % QW;
+            const int part = item / QW;
+            const int qi = qbase + s;
+            int hit = 0x7fffffff;
+            if (qi < nq) {
+                float fb = sBest[0][s];
+                int fc = sChunk[0][s];
+#pragma unroll
+                for (int w = 1; w < W; ++w) {
+                    const float v = sBest[w][s];
+                    const int c = sChunk[w][s];
+                    if (v < fb || (v == fb && c < fc)) { fb = v; fc = c; }
+                }
+                // item % 64 == lane, so query s is this lane's register copy
+                // number (item / 64) % QPT -- wave-uniform, no reload
+                const int qsel = (item >> 6) % QPT;
+                float x = px[0].x, y = py[0].x, z = pz[0].x;
+#pragma unroll
+                for (int qq = 1; qq < QPT; ++qq)
+                    if (qsel == qq) { x = px[qq].x; y = py[qq].x; z = pz[qq].x; }
+                const int k0 = fc * C + part * CP;
+                if (resident) {
+#pragma unroll
+                    for (int k = 0; k < CP; ++k) {
+                        const int kk = k0 + k;
+                        const float d = pcm_sqd(sXYZ[0][kk] - x, sXYZ[1][kk] - y, sXYZ[2][kk] - z);
+                        hit = (d == fb && hit == 0x7fffffff && kk < nt) ? kk : hit;
+                    }
+                } else {
+                    for (int k = 0; k < CP; ++k) {
+                        const int kk = k0 + k;
+                        if (kk >= nt) break;
+                        const float *q = T + 3 * (size_t)kk;
+                        const float d = pcm_sqd(q[0] - x, q[1] - y, q[2] - z);
+                        if (d == fb) { hit = kk; break; }
+                    }
+                }
+            }
+            sHit[part][s] = hit;
+        }
+        __syncthreads();
+        for (int s = tid; s < QW; s += NT) {
+            const int qi = qbase + s;
+            if (qi >= nq) continue;
             float fb = sBest[0][s];
-            int fc = sChunk[0][s];
+#pragma unroll
+            for (int w = 1; w < W; ++w) fb = __builtin_fminf(fb, sBest[w][s]);
+            int idx = sHit[0][s];
+#pragma unroll
+            for (int p = 1; p < PARTS; ++p) idx = min(idx, sHit[p][s]);
+            my_d = fb;
+            D[qi] = my_d;
+            I[qi] = idx;
+        }
+    } else {
+        for (int s = tid; s < QW; s += NT) {
+            const int qi = qbase + s;
+            if (qi >= nq) continue;
+            float d;
+            int idx;
+            pcm_ref_nn_scan(Q[3 * (size_t)qi + 0], Q[3 * (size_t)qi + 1], Q[3 * (size_t)qi + 2], T, nt,
+                            d, idx);
+            my_d = d;
+            D[qi] = d;
+            I[qi] = idx;
+        }
+    }
+
+    if constexpr (kLoss) {
+        // deterministic workgroup sum -> partials[block]; last block reduces
+        const float ws = wave_sum(my_d);
+        if (lane == 0) sRed[0][wave] = ws;
+        __syncthreads();
+        if (tid == 0) {
+            float s = 0.f;
+#pragma unroll
+            for (int w = 0; w < W; ++w) s += sRed[0][w];
+            // hand-off without fences (MI355X_MICROARCH.md, visibility table
+            // row 1): write-through (sc1) partial, drain, agent atomic ticket;
+            // the last arriver reads every partial with sc1 loads.
+            __hip_atomic_store(&partials[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sLast = (t == gridDim.x - 1);
+        }
+        __syncthreads();
+        if (sLast) {
+            const int nb1 = b * nblk1;
+            const int nbt = (int)gridDim.x;
+            float s1 = 0.f, s2 = 0.f;
+            for (int i = tid; i < nbt; i += NT) {
+                const float v = __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (i < nb1) s1 += v; else s2 += v;
+            }
+            s1 = wave_sum(s1);
+            s2 = wave_sum(s2);
+            if (lane == 0) { sRed[0][wave] = s1; sRed[1][wave] = s2; }
+            __syncthreads();
+            if (tid == 0) {
+                float a1 = 0.f, a2 = 0.f;
+#pragma unroll
+                for (int w = 0; w < W; ++w) { a1 += sRed[0][w]; a2 += sRed[1][w]; }
+                mean_out[0] = a1 / ((float)b * (float)n);
+                mean_out[1] = a2 / ((float)b * (float)m);
+                __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Forward, SGPR-stream form.  Same algorithm and results as above, but the
+// candidates are not staged through LDS for the scan: a wave's chunk index is
+// wave-uniform, so hipcc reads the AoS candidates with s_load (scalar cache)
+// and feeds them to v_pk_add_f32 as an SGPR operand broadcast with op_sel --
+// packing runs over two QUERIES per lane instead of two candidates.  No LDS
+// reads or barriers in the main loop.  (Any memory-writing intrinsic or
+// volatile asm placed before the scan -- e.g. an LDS-DMA prefetch -- makes
+// hipcc fall back to per-lane vector loads of the candidates: measured 35%
+// slower, so the epilogue reads global memory instead.)  With kLoss the
+// workgroup's partial sum is published right after the merge and the arrival
+// ticket's round trip overlaps the rescan.
+// ---------------------------------------------------------------------------
+
+// Arrival tickets are sharded two-level: one arrival counter per 128-byte line
+// for each of kShards shards (block id mod kShards), and a top counter that
+// only each shard's last arriver increments.  512 arrivals on ONE counter
+// serialise at ~12 ns each (MI355X_MICROARCH.md price list, row "fanin");
+// sharded, the tail sees ~16 + 32 arrivals.
+constexpr int kShards = 32;
+constexpr int kShardStride = 32;  // unsigned words = 128 B per counter line
+constexpr size_t kTicketBytes = (size_t)(kShards + 1) * kShardStride * 4;  // then the partials
+
+// Returns 1 in thread 0 of the overall last-arriving workgroup, else 0.  The
+// caller tests it only after its remaining work, so the atomics' round trips
+// overlap that work instead of stalling the workgroup at the next barrier.
+__device__ __forceinline__ unsigned publish_partial(float v, float *partials, unsigned *ticket,
+                                                    float (*sRed)[16]) {
+    // deterministic workgroup sum, then (tid 0) write-through store, drain,
+    // agent atomic ticket (MI355X_MICROARCH.md visibility table, row 1)
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const float ws = wave_sum(v);
+    if (lane == 0) sRed[0][wave] = ws;
+    __syncthreads();
+    unsigned last = 0;
+    if (threadIdx.x == 0) {
+        float s = 0.f;
+        const int nw = blockDim.x >> 6;
+        for (int w = 0; w < nw; ++w) s += sRed[0][w];
+        __hip_atomic_store(&partials[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned nb = gridDim.x;
+        const unsigned sh = blockIdx.x % kShards;
+        const unsigned in_shard = (nb - sh + kShards - 1) / kShards;
+        const unsigned active = nb < kShards ? nb : kShards;
+        const unsigned t = __hip_atomic_fetch_add(ticket + kShardStride * (1 + sh), 1u, __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT);
+        if (t == in_shard - 1) {
+            const unsigned u = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            last = (u == active - 1);
+        }
+    }
+    return last;
+}
+
+__device__ __forceinline__ void finish_loss(int nb1, int b, int n, int m, const float *partials,
+                                            unsigned *ticket, float *mean_out, float (*sRed)[16]) {
+    // the last-arriving workgroup: fixed-order reduction of every partial
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nbt = (int)gridDim.x;
+    float s1 = 0.f, s2 = 0.f;
+    for (int i = threadIdx.x; i < nbt; i += blockDim.x) {
+        const float v = __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (i < nb1) s1 += v; else s2 += v;
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) { sRed[0][wave] = s1; sRed[1][wave] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float a1 = 0.f, a2 = 0.f;
+        const int nw = blockDim.x >> 6;
+        for (int w = 0; w < nw; ++w) { a1 += sRed[0][w]; a2 += sRed[1][w]; }
+        mean_out[0] = a1 / ((float)b * (float)n);
+        mean_out[1] = a2 / ((float)b * (float)m);
+        // every arrival is in: re-arm the counters for the next stream-ordered call
+        for (int s = 0; s <= kShards; ++s)
+            __hip_atomic_store(ticket + kShardStride * s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <int W, int QPT, int C, bool kLoss>
+__global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
+    float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1,
+    int32_t *__restrict__ idx2, int nblk1, int nblk2, float *__restrict__ partials,
+    unsigned *__restrict__ ticket, float *__restrict__ mean_out) {
+    static_assert(QPT % 2 == 0, "queries are packed in pairs");
+    static_assert(C % 2 == 0, "candidates are consumed in pairs");
+    static_assert(W <= 16, "sRed holds 16 waves");
+    constexpr int QW = 64 * QPT;
+    constexpr int NT = 64 * W;
+    static_assert(NT >= QW, "one thread per query slot in the merge");
+    constexpr int QP = QPT / 2;        // packed query pairs per lane
+    constexpr int PARTS = NT / QW;     // rescan splits per query
+    constexpr int CP = C / PARTS;
+    static_assert(C % PARTS == 0, "chunk must split evenly");
+    __shared__ float sBest[W][QW];
+    __shared__ int sChunk[W][QW];
+    __shared__ float sFb[QW];
+    __shared__ int sFc[QW];
+    __shared__ int sHit[PARTS][QW];
+    __shared__ float sRed[2][16];
+    __shared__ int sLast[4];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    int bid = blockIdx.x;
+    const float *Q, *T;
+    float *D;
+    int32_t *I;
+    int nq, nt, blk;
+    if (bid < b * nblk1) {
+        const int batch = bid / nblk1;
+        blk = bid - batch * nblk1;
+        Q = xyz1 + (size_t)batch * n * 3;
+        T = xyz2 + (size_t)batch * m * 3;
+        D = dist1 + (size_t)batch * n;
+        I = idx1 + (size_t)batch * n;
+        nq = n;
+        nt = m;
+    } else {
+        bid -= b * nblk1;
+        const int batch = bid / nblk2;
+        blk = bid - batch * nblk2;
+        Q = xyz2 + (size_t)batch * m * 3;
+        T = xyz1 + (size_t)batch * n * 3;
+        D = dist2 + (size_t)batch * m;
+        I = idx2 + (size_t)batch * m;
+        nq = m;
+        nt = n;
+    }
+    const int qbase = blk * QW;
+
+    // ---- queries: pair pp holds the lane's queries (2pp)*64+lane, (2pp+1)*64+lane
+    pcm_f2 px[QP], py[QP], pz[QP];
+    bool nonfinite = false;
+#pragma unroll
+    for (int pp = 0; pp < QP; ++pp) {
+        float c3[2][3];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int qi = qbase + (2 * pp + h) * 64 + lane;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) c3[h][d] = 0.f;
+            if (qi < nq) {
+#pragma unroll
+                for (int d = 0; d < 3; ++d) c3[h][d] = Q[3 * (size_t)qi + d];
+                nonfinite |= !(pcm_finite(c3[h][0]) && pcm_finite(c3[h][1]) && pcm_finite(c3[h][2]));
+            }
+        }
+        px[pp] = pcm_f2{c3[0][0], c3[1][0]};
+        py[pp] = pcm_f2{c3[0][1], c3[1][1]};
+        pz[pp] = pcm_f2{c3[0][2], c3[1][2]};
+    }
+    // finiteness of the target cloud: issue the loads now, test after the scan
+    // (kChk per thread covers 3*nt <= kChk*NT; larger clouds loop at the end)
+    constexpr int kChk = 8;
+    float chk[kChk];
+    const bool chk_all = 3 * nt <= kChk * NT;
+#pragma unroll
+    for (int r = 0; r < kChk; ++r) {
+        const int f = tid + r * NT;
+        chk[r] = (chk_all && f < 3 * nt) ? T[f] : 0.f;
+    }
+
+    float best[QPT];
+    int bchunk[QPT];
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) { best[q] = PCM_INF; bchunk[q] = 0; }
+
+    // ---- main scan: chunks c = wave, wave+W, ... ; candidates via SGPRs
+    const int nfull = nt / C;
+    for (int c = wave; c < nfull; c += W) {
+        float mn[QPT];
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) mn[q] = PCM_INF;
+        const float *tk = T + 3 * (size_t)c * C;
+#pragma unroll
+        for (int k = 0; k < C; k += 2) {
+            const float ax = tk[3 * k + 0], ay = tk[3 * k + 1], az = tk[3 * k + 2];
+            const float bx = tk[3 * k + 3], by = tk[3 * k + 4], bz = tk[3 * k + 5];
+#pragma unroll
+            for (int pp = 0; pp < QP; ++pp) {
+                const pcm_f2 da = pcm_sqd2(pcm_f2{ax, ax} - px[pp], pcm_f2{ay, ay} - py[pp],
+                                           pcm_f2{az, az} - pz[pp]);
+                const pcm_f2 db = pcm_sqd2(pcm_f2{bx, bx} - px[pp], pcm_f2{by, by} - py[pp],
+                                           pcm_f2{bz, bz} - pz[pp]);
+                mn[2 * pp] = __builtin_fminf(__builtin_fminf(mn[2 * pp], da.x), db.x);
+                mn[2 * pp + 1] = __builtin_fminf(__builtin_fminf(mn[2 * pp + 1], da.y), db.y);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) {
+            if (mn[q] < best[q]) { best[q] = mn[q]; bchunk[q] = c; }
+        }
+    }
+    // tail chunk (nt % C candidates), owned by the wave that owns chunk nfull
+    if (nfull * C < nt && (nfull % W) == wave) {
+        float mn[QPT];
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) mn[q] = PCM_INF;
+        for (int k = nfull * C; k < nt; ++k) {
+            const float ax = T[3 * (size_t)k], ay = T[3 * (size_t)k + 1], az = T[3 * (size_t)k + 2];
+#pragma unroll
+            for (int pp = 0; pp < QP; ++pp) {
+                const pcm_f2 da = pcm_sqd2(pcm_f2{ax, ax} - px[pp], pcm_f2{ay, ay} - py[pp],
+                                           pcm_f2{az, az} - pz[pp]);
+                mn[2 * pp] = __builtin_fminf(mn[2 * pp], da.x);
+                mn[2 * pp + 1] = __builtin_fminf(mn[2 * pp + 1], da.y);
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < QPT; ++q) {
+            if (mn[q] < best[q]) { best[q] = mn[q]; bchunk[q] = nfull; }
+        }
+    }
+
+    // ---- per-wave results to LDS; finish the finiteness check
+#pragma unroll
+    for (int q = 0; q < QPT; ++q) {
+        sBest[wave][q * 64 + lane] = best[q];
+        sChunk[wave][q * 64 + lane] = bchunk[q];
+    }
+    if (chk_all) {
+#pragma unroll
+        for (int r = 0; r < kChk; ++r) nonfinite |= !pcm_finite(chk[r]);
+    } else {
+        // large clouds: 8 independent loads in flight per step
+        for (int f0 = tid; f0 < 3 * nt; f0 += kChk * NT) {
+            float v[kChk];
+#pragma unroll
+            for (int r = 0; r < kChk; ++r) {
+                const int f = f0 + r * NT;
+                v[r] = f < 3 * nt ? T[f] : 0.f;
+            }
+#pragma unroll
+            for (int r = 0; r < kChk; ++r) nonfinite |= !pcm_finite(v[r]);
+        }
+    }
+    const int any_nonfinite = __syncthreads_or(nonfinite ? 1 : 0);
+    unsigned tk = 0;  // arrival ticket (thread 0, kLoss)
+
+    if (!any_nonfinite) {
+        // ---- merge: thread s < QW owns query slot s
+        float fbv = 0.f;
+        if (tid < QW) {
+            float fb = sBest[0][tid];
+            int fc = sChunk[0][tid];
 #pragma unroll
             for (int w = 1; w < W; ++w) {
-                const float v = sBest[w][s];
-                const int c = sChunk[w][s];
+                const float v = sBest[w][tid];
+                const int c = sChunk[w][tid];
                 if (v < fb || (v == fb && c < fc)) { fb = v; fc = c; }
             }
-            const int k0 = fc * C;
-            const int k1 = min(k0 + C, nt);
-            idx = k0;
-            for (int k = k0; k < k1; ++k) {
-                const float *q = T + 3 * (size_t)k;
-                if (pcm_sqd(q[0] - x, q[1] - y, q[2] - z) == fb) { idx = k; break; }
-            }
-            d = fb;
+            sFb[tid] = fb;
+            sFc[tid] = fc;
+            if (qbase + tid < nq) fbv = fb;
         }
-        D[qi] = d;
-        I[qi] = idx;
+        if constexpr (kLoss) tk = publish_partial(fbv, partials, ticket, sRed);  // has a barrier
+        else __syncthreads();
+        // ---- rescan the winning chunk: item -> (query s, part)
+#pragma unroll
+        for (int r = 0; r < (QW * PARTS + NT - 1) / NT; ++r) {
+            const int item = tid + r * NT;
+            if (item >= QW * PARTS) break;
+            const int s = item % QW;
+            const int part = item / QW;
+            int hit = 0x7fffffff;
+            if (qbase + s < nq) {
+                const float fb = sFb[s];
+                const int fc = sFc[s];
+                // query s is this lane's register copy q = (item/64) % QPT
+                const int qsel = (item >> 6) % QPT;
+                float x = px[0].x, y = py[0].x, z = pz[0].x;
+#pragma unroll
+                for (int q = 1; q < QPT; ++q) {
+                    if (qsel == q) {
+                        x = (q & 1) ? px[q / 2].y : px[q / 2].x;
+                        y = (q & 1) ? py[q / 2].y : py[q / 2].x;
+                        z = (q & 1) ? pz[q / 2].y : pz[q / 2].x;
+                    }
+                }
+                const int k0 = fc * C + part * CP;
+#pragma unroll
+                for (int k = 0; k < CP; ++k) {
+                    const int kk = k0 + k;
+                    if (kk < nt) {
+                        const float *t = T + 3 * (size_t)kk;
+                        const float d = pcm_sqd(t[0] - x, t[1] - y, t[2] - z);
+                        hit = (d == fb && hit == 0x7fffffff) ? kk : hit;
+                    }
+                }
+            }
+            sHit[part][s] = hit;
+        }
+        __syncthreads();
+        if (tid < QW && qbase + tid < nq) {
+            int idx = sHit[0][tid];
+#pragma unroll
+            for (int p = 1; p < PARTS; ++p) idx = min(idx, sHit[p][tid]);
+            D[qbase + tid] = sFb[tid];
+            I[qbase + tid] = idx;
+        }
+    } else {
+        float myd = 0.f;
+        for (int s = tid; s < QW; s += NT) {
+            const int qi = qbase + s;
+            if (qi >= nq) continue;
+            float d;
+            int idx;
+            pcm_ref_nn_scan(Q[3 * (size_t)qi + 0], Q[3 * (size_t)qi + 1], Q[3 * (size_t)qi + 2], T, nt,
+                            d, idx);
+            myd = d;
+            D[qi] = d;
+            I[qi] = idx;
+        }
+        if constexpr (kLoss) tk = publish_partial(myd, partials, ticket, sRed);
+    }
+    if constexpr (kLoss) {
+        if (tid == 0) sLast[0] = tk;
+        __syncthreads();
+        if (sLast[0]) finish_loss(b * nblk1, b, n, m, partials, ticket, mean_out, sRed);
     }
 }
 
 // ---------------------------------------------------------------------------
 // Backward
 // ---------------------------------------------------------------------------
-constexpr int kBwdThreads = 1024;   // targets per workgroup = threads
-constexpr int kBwdCap = 8192;       // scatter entries sortable in LDS per workgroup
+constexpr int kBwdT = 256;     // targets per workgroup = threads
+constexpr int kBwdCap = 4096;  // scatter entries sortable in LDS per workgroup
 
-// exclusive scan of one value per thread over a 1024-thread workgroup
-__device__ inline int block_exclusive_scan_1024(int v, int *wave_tot) {
+template <int NT>
+__device__ inline int block_exclusive_scan(int v, int *wave_tot) {
+    constexpr int NW = NT / 64;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     int x = v;
@@ -211,30 +649,22 @@ __device__ inline int block_exclusive_scan_1024(int v, int *wave_tot) {
     }
     if (lane == 63) wave_tot[wave] = x;
     __syncthreads();
-    if (wave == 0) {
-        int t = lane < (kBwdThreads / 64) ? wave_tot[lane] : 0;
+    int before = 0;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(t, o, 64);
-            if (lane >= o) t += y;
-        }
-        if (lane < (kBwdThreads / 64)) wave_tot[lane] = t;  // inclusive wave prefix
-    }
-    __syncthreads();
-    const int before = wave == 0 ? 0 : wave_tot[wave - 1];
+    for (int w = 0; w < NW; ++w) before += (w < wave) ? wave_tot[w] : 0;
     return before + x - v;
 }
 
-__global__ __launch_bounds__(kBwdThreads) void chamfer_bwd_kernel(
+__global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
     const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
     const int32_t *__restrict__ idx2, float *__restrict__ grad1, float *__restrict__ grad2,
     int nblk1, int nblk2) {
-    __shared__ int sCnt[kBwdThreads];
-    __shared__ int sOff[kBwdThreads + 1];
+    __shared__ int sCnt[kBwdT];
+    __shared__ int sOff[kBwdT + 1];
     __shared__ int sTmp[kBwdCap];
     __shared__ int sSrt[kBwdCap];
-    __shared__ int sWave[kBwdThreads / 64];
+    __shared__ int sWave[kBwdT / 64];
 
     const int tid = threadIdx.x;
     int bid = blockIdx.x;
@@ -273,30 +703,45 @@ __global__ __launch_bounds__(kBwdThreads) void chamfer_bwd_kernel(
         no = n;
         direct_first = false;
     }
-    const int t0 = blk * kBwdThreads;
-    const int T = min(kBwdThreads, ns - t0);
+    const int t0 = blk * kBwdT;
+    const int T = min(kBwdT, ns - t0);
+
+    // direct term first: its loads overlap the histogram pass
+    const int i = t0 + tid;
+    const bool own = tid < T;
+    float sx = 0.f, sy = 0.f, sz = 0.f, dir0 = 0.f, dir1 = 0.f, dir2 = 0.f;
+    if (own) {
+        sx = self[3 * (size_t)i + 0];
+        sy = self[3 * (size_t)i + 1];
+        sz = self[3 * (size_t)i + 2];
+        const int k = ids[i];
+        const float g = __fmul_rn(gds[i], 2.f);
+        dir0 = __fmul_rn(g, __fsub_rn(sx, other[3 * (size_t)k + 0]));
+        dir1 = __fmul_rn(g, __fsub_rn(sy, other[3 * (size_t)k + 1]));
+        dir2 = __fmul_rn(g, __fsub_rn(sz, other[3 * (size_t)k + 2]));
+    }
 
     // 1. histogram of the other direction's argmins that land in [t0, t0+T)
     sCnt[tid] = 0;
     __syncthreads();
-    for (int j = tid; j < no; j += kBwdThreads) {
+    for (int j = tid; j < no; j += kBwdT) {
         const unsigned k = (unsigned)(ido[j] - t0);
         if (k < (unsigned)T) atomicAdd(&sCnt[k], 1);
     }
     __syncthreads();
     // 2. bucket offsets
     const int c = sCnt[tid];
-    const int off = block_exclusive_scan_1024(c, sWave);
+    const int off = block_exclusive_scan<kBwdT>(c, sWave);
     sOff[tid] = off;
-    if (tid == kBwdThreads - 1) sOff[kBwdThreads] = off + c;
+    if (tid == kBwdT - 1) sOff[kBwdT] = off + c;
     sCnt[tid] = 0;
     __syncthreads();
-    const int total = sOff[kBwdThreads];
+    const int total = sOff[kBwdT];
     const bool fits = total <= kBwdCap;  // uniform
 
-    if (fits) {
+    if (fits && total > 0) {
         // 3. fill buckets (arbitrary order inside a bucket) ...
-        for (int j = tid; j < no; j += kBwdThreads) {
+        for (int j = tid; j < no; j += kBwdT) {
             const unsigned k = (unsigned)(ido[j] - t0);
             if (k < (unsigned)T) {
                 const int s = atomicAdd(&sCnt[k], 1);
@@ -305,7 +750,7 @@ __global__ __launch_bounds__(kBwdThreads) void chamfer_bwd_kernel(
         }
         __syncthreads();
         // 4. ... then rank each entry by source index inside its bucket
-        for (int p = tid; p < total; p += kBwdThreads) {
+        for (int p = tid; p < total; p += kBwdT) {
             const int j = sTmp[p];
             const int k = ido[j] - t0;
             const int lo = sOff[k], hi = sOff[k + 1];
@@ -316,24 +761,12 @@ __global__ __launch_bounds__(kBwdThreads) void chamfer_bwd_kernel(
         __syncthreads();
     }
 
-    if (tid >= T) return;
-    const int i = t0 + tid;
-    const float sx = self[3 * (size_t)i + 0];
-    const float sy = self[3 * (size_t)i + 1];
-    const float sz = self[3 * (size_t)i + 2];
-    float dir[3];
-    {
-        const int k = ids[i];
-        const float g = __fmul_rn(gds[i], 2.f);
-        dir[0] = __fmul_rn(g, __fsub_rn(sx, other[3 * (size_t)k + 0]));
-        dir[1] = __fmul_rn(g, __fsub_rn(sy, other[3 * (size_t)k + 1]));
-        dir[2] = __fmul_rn(g, __fsub_rn(sz, other[3 * (size_t)k + 2]));
-    }
+    if (!own) return;
     float ax = 0.f, ay = 0.f, az = 0.f;
     if (direct_first) {
-        ax = __fadd_rn(ax, dir[0]);
-        ay = __fadd_rn(ay, dir[1]);
-        az = __fadd_rn(az, dir[2]);
+        ax = __fadd_rn(ax, dir0);
+        ay = __fadd_rn(ay, dir1);
+        az = __fadd_rn(az, dir2);
     }
     auto scatter = [&](int j) {
         const float g = __fmul_rn(gdo[j], 2.f);
@@ -351,9 +784,295 @@ __global__ __launch_bounds__(kBwdThreads) void chamfer_bwd_kernel(
             if (ido[j] == i) scatter(j);
     }
     if (!direct_first) {
-        ax = __fadd_rn(ax, dir[0]);
-        ay = __fadd_rn(ay, dir[1]);
-        az = __fadd_rn(az, dir[2]);
+        ax = __fadd_rn(ax, dir0);
+        ay = __fadd_rn(ay, dir1);
+        az = __fadd_rn(az, dir2);
+    }
+    grad[3 * (size_t)i + 0] = ax;
+    grad[3 * (size_t)i + 1] = ay;
+    grad[3 * (size_t)i + 2] = az;
+}
+
+// ---------------------------------------------------------------------------
+// Backward, LDS-resident: one workgroup per batch element computes BOTH
+// clouds' gradients with the whole batch (points, graddists, argmins, the two
+// inverse-index counting sorts) in LDS: one coalesced load phase, LDS-only
+// work, one store phase.  Used when 36*(n+m) bytes fit (n = m <= 2048).
+// ---------------------------------------------------------------------------
+constexpr int kBwdLdsT = 1024;
+
+__host__ __device__ inline size_t bwd_lds_bytes(int n, int m) { return (size_t)36 * (n + m) + 64; }
+constexpr size_t kBwdLdsMax = 150 * 1024;
+
+// copy `count` 4-byte words global -> LDS, loads batched ahead of the stores
+template <int NT, typename Tp>
+__device__ inline void lds_copy(Tp *__restrict__ dst, const Tp *__restrict__ src, int count) {
+    constexpr int U = 4;
+    for (int base = 0; base < count; base += U * NT) {
+        Tp v[U];
+#pragma unroll
+        for (int r = 0; r < U; ++r) {
+            const int i = base + r * NT + (int)threadIdx.x;
+            if (i < count) v[r] = src[i];
+        }
+#pragma unroll
+        for (int r = 0; r < U; ++r) {
+            const int i = base + r * NT + (int)threadIdx.x;
+            if (i < count) dst[i] = v[r];
+        }
+    }
+}
+
+// exclusive scan of cnt[0..len) into off[0..len] (off[len] = total), NT threads
+template <int NT>
+__device__ inline void block_scan_array(const int *cnt, int *off, int len, int *wave_tot) {
+    const int per = (len + NT - 1) / NT;
+    const int lo = min(len, (int)threadIdx.x * per), hi = min(len, lo + per);
+    int local = 0;
+    for (int i = lo; i < hi; ++i) local += cnt[i];
+    const int before = block_exclusive_scan<NT>(local, wave_tot);
+    int run = before;
+    for (int i = lo; i < hi; ++i) { off[i] = run; run += cnt[i]; }
+    if (threadIdx.x == NT - 1) off[len] = run;
+}
+
+// counting sort of sources j (0..ns) by key[j] in [0, nk): off[0..nk], srt[]
+// ascending j inside every bucket.  cnt is scratch [nk]; tmp scratch [ns].
+template <int NT>
+__device__ inline void inverse_index(const int *key, int ns, int nk, int *cnt, int *off, int *tmp,
+                                     int *srt, int *wave_tot) {
+    for (int i = threadIdx.x; i < nk; i += NT) cnt[i] = 0;
+    __syncthreads();
+    for (int j = threadIdx.x; j < ns; j += NT) atomicAdd(&cnt[key[j]], 1);
+    __syncthreads();
+    block_scan_array<NT>(cnt, off, nk, wave_tot);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nk; i += NT) cnt[i] = 0;
+    __syncthreads();
+    for (int j = threadIdx.x; j < ns; j += NT) {
+        const int k = key[j];
+        tmp[off[k] + atomicAdd(&cnt[k], 1)] = j;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < ns; p += NT) {
+        const int j = tmp[p];
+        const int k = key[j];
+        const int lo = off[k], hi = off[k + 1];
+        int r = 0;
+        for (int q = lo; q < hi; ++q) r += (tmp[q] < j);
+        srt[lo + r] = j;
+    }
+}
+
+__global__ __launch_bounds__(kBwdLdsT) void chamfer_bwd_lds_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, int m,
+    const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
+    const int32_t *__restrict__ idx2, float *__restrict__ grad1, float *__restrict__ grad2) {
+    extern __shared__ __attribute__((aligned(16))) float lds[];
+    __shared__ int sWave[kBwdLdsT / 64];
+    const int batch = blockIdx.x;
+    float *P1 = lds;                 // [3n] AoS
+    float *P2 = P1 + 3 * n;          // [3m]
+    float *G1 = P2 + 3 * m;          // [n]
+    float *G2 = G1 + n;              // [m]
+    int *I1 = (int *)(G2 + m);       // [n] argmin in cloud 2
+    int *I2 = I1 + n;                // [m] argmin in cloud 1
+    int *cnt = I2 + m;               // [max(n,m)] scratch
+    int *off1 = cnt + max(n, m);     // [n+1] buckets of cloud-2 sources per cloud-1 point
+    int *off2 = off1 + n + 1;        // [m+1]
+    int *tmp = off2 + m + 1;         // [max(n,m)] scratch
+    int *srt1 = tmp + max(n, m);     // [m]
+    int *srt2 = srt1 + m;            // [n]
+
+    lds_copy<kBwdLdsT>(P1, xyz1 + (size_t)batch * n * 3, 3 * n);
+    lds_copy<kBwdLdsT>(P2, xyz2 + (size_t)batch * m * 3, 3 * m);
+    lds_copy<kBwdLdsT>(G1, gd1 + (size_t)batch * n, n);
+    lds_copy<kBwdLdsT>(G2, gd2 + (size_t)batch * m, m);
+    lds_copy<kBwdLdsT>(I1, idx1 + (size_t)batch * n, n);
+    lds_copy<kBwdLdsT>(I2, idx2 + (size_t)batch * m, m);
+    __syncthreads();
+    // cloud-1 points receive scatter terms from cloud-2 sources (key idx2)
+    inverse_index<kBwdLdsT>(I2, m, n, cnt, off1, tmp, srt1, sWave);
+    __syncthreads();
+    inverse_index<kBwdLdsT>(I1, n, m, cnt, off2, tmp, srt2, sWave);
+    __syncthreads();
+
+    // cloud 1: direct term first (chamfer3D.cu:184), then cloud-2 scatters
+    float *g1o = grad1 + (size_t)batch * n * 3;
+    for (int i = threadIdx.x; i < n; i += kBwdLdsT) {
+        const float sx = P1[3 * i], sy = P1[3 * i + 1], sz = P1[3 * i + 2];
+        const int k = I1[i];
+        const float g = __fmul_rn(G1[i], 2.f);
+        float ax = __fadd_rn(0.f, __fmul_rn(g, __fsub_rn(sx, P2[3 * k])));
+        float ay = __fadd_rn(0.f, __fmul_rn(g, __fsub_rn(sy, P2[3 * k + 1])));
+        float az = __fadd_rn(0.f, __fmul_rn(g, __fsub_rn(sz, P2[3 * k + 2])));
+        for (int p = off1[i]; p < off1[i + 1]; ++p) {
+            const int j = srt1[p];
+            const float h = __fmul_rn(G2[j], 2.f);
+            ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(P2[3 * j], sx)));
+            ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(P2[3 * j + 1], sy)));
+            az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(P2[3 * j + 2], sz)));
+        }
+        g1o[3 * i] = ax;
+        g1o[3 * i + 1] = ay;
+        g1o[3 * i + 2] = az;
+    }
+    // cloud 2: cloud-1 scatters first (kernel 1 ran before kernel 2), then direct
+    float *g2o = grad2 + (size_t)batch * m * 3;
+    for (int i = threadIdx.x; i < m; i += kBwdLdsT) {
+        const float sx = P2[3 * i], sy = P2[3 * i + 1], sz = P2[3 * i + 2];
+        float ax = 0.f, ay = 0.f, az = 0.f;
+        for (int p = off2[i]; p < off2[i + 1]; ++p) {
+            const int j = srt2[p];
+            const float h = __fmul_rn(G1[j], 2.f);
+            ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(P1[3 * j], sx)));
+            ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(P1[3 * j + 1], sy)));
+            az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(P1[3 * j + 2], sz)));
+        }
+        const int k = I2[i];
+        const float g = __fmul_rn(G2[i], 2.f);
+        ax = __fadd_rn(ax, __fmul_rn(g, __fsub_rn(sx, P1[3 * k])));
+        ay = __fadd_rn(ay, __fmul_rn(g, __fsub_rn(sy, P1[3 * k + 1])));
+        az = __fadd_rn(az, __fmul_rn(g, __fsub_rn(sz, P1[3 * k + 2])));
+        g2o[3 * i] = ax;
+        g2o[3 * i + 1] = ay;
+        g2o[3 * i + 2] = az;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Backward, staged: the 256-target workgroup layout of chamfer_bwd_kernel, but
+// the other cloud's argmins, points and graddists (everything the histogram,
+// fill, rank and scatter phases touch) arrive by one asynchronous LDS-DMA, so
+// the phases run on LDS instead of re-reading global memory.  The own
+// targets' direct terms load meanwhile.  Used when 20*no bytes fit.
+// ---------------------------------------------------------------------------
+constexpr int kBwdStageMax = 2048;  // sources staged (20 B each + sort scratch)
+
+__global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
+    const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
+    const int32_t *__restrict__ idx2, float *__restrict__ grad1, float *__restrict__ grad2,
+    int nblk1, int nblk2) {
+    __shared__ __attribute__((aligned(16))) float sO[3 * kBwdStageMax];   // other cloud, AoS
+    __shared__ __attribute__((aligned(16))) float sG[kBwdStageMax];       // other graddist
+    __shared__ __attribute__((aligned(16))) int sK[kBwdStageMax];         // other argmins
+    __shared__ int sCnt[kBwdT];
+    __shared__ int sOff[kBwdT + 4];
+    __shared__ int sTmp[kBwdStageMax];
+    __shared__ int sSrt[kBwdStageMax];
+    __shared__ int sWave[kBwdT / 64];
+
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    int bid = blockIdx.x;
+    const float *self, *other, *gds, *gdo;
+    const int32_t *ids, *ido;
+    float *grad;
+    int ns, no, blk;
+    bool direct_first;
+    if (bid < b * nblk1) {
+        const int batch = bid / nblk1;
+        blk = bid - batch * nblk1;
+        self = xyz1 + (size_t)batch * n * 3;
+        other = xyz2 + (size_t)batch * m * 3;
+        gds = gd1 + (size_t)batch * n;
+        gdo = gd2 + (size_t)batch * m;
+        ids = idx1 + (size_t)batch * n;
+        ido = idx2 + (size_t)batch * m;
+        grad = grad1 + (size_t)batch * n * 3;
+        ns = n;
+        no = m;
+        direct_first = true;
+    } else {
+        bid -= b * nblk1;
+        const int batch = bid / nblk2;
+        blk = bid - batch * nblk2;
+        self = xyz2 + (size_t)batch * m * 3;
+        other = xyz1 + (size_t)batch * n * 3;
+        gds = gd2 + (size_t)batch * m;
+        gdo = gd1 + (size_t)batch * n;
+        ids = idx2 + (size_t)batch * m;
+        ido = idx1 + (size_t)batch * n;
+        grad = grad2 + (size_t)batch * m * 3;
+        ns = m;
+        no = n;
+        direct_first = false;
+    }
+    const int t0 = blk * kBwdT;
+    const int T = min(kBwdT, ns - t0);
+
+    pcm_dma_to_lds(sK, ido, 4 * no, wave, kBwdT / 64);
+    pcm_dma_to_lds(sO, other, 12 * no, wave, kBwdT / 64);
+    pcm_dma_to_lds(sG, gdo, 4 * no, wave, kBwdT / 64);
+
+    const int i = t0 + tid;
+    const bool own = tid < T;
+    float sx = 0.f, sy = 0.f, sz = 0.f, gself = 0.f;
+    int kself = 0;
+    if (own) {
+        sx = self[3 * (size_t)i + 0];
+        sy = self[3 * (size_t)i + 1];
+        sz = self[3 * (size_t)i + 2];
+        kself = ids[i];
+        gself = gds[i];
+    }
+    sCnt[tid] = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    // 1. histogram of the other direction's argmins landing in [t0, t0+T)
+    for (int j = tid; j < no; j += kBwdT) {
+        const unsigned k = (unsigned)(sK[j] - t0);
+        if (k < (unsigned)T) atomicAdd(&sCnt[k], 1);
+    }
+    __syncthreads();
+    const int c = sCnt[tid];
+    const int off = block_exclusive_scan<kBwdT>(c, sWave);
+    sOff[tid] = off;
+    if (tid == kBwdT - 1) sOff[kBwdT] = off + c;
+    sCnt[tid] = 0;
+    __syncthreads();
+    const int total = sOff[kBwdT];
+    // 2. fill buckets, 3. rank by source index inside each bucket
+    for (int j = tid; j < no; j += kBwdT) {
+        const unsigned k = (unsigned)(sK[j] - t0);
+        if (k < (unsigned)T) sTmp[sOff[k] + atomicAdd(&sCnt[k], 1)] = j;
+    }
+    __syncthreads();
+    for (int p = tid; p < total; p += kBwdT) {
+        const int j = sTmp[p];
+        const int k = sK[j] - t0;
+        const int lo = sOff[k], hi = sOff[k + 1];
+        int r = 0;
+        for (int q = lo; q < hi; ++q) r += (sTmp[q] < j);
+        sSrt[lo + r] = j;
+    }
+    __syncthreads();
+    if (!own) return;
+
+    // 4. accumulate in the reference's kernel order
+    const float g = __fmul_rn(gself, 2.f);
+    const float d0 = __fmul_rn(g, __fsub_rn(sx, sO[3 * kself + 0]));
+    const float d1 = __fmul_rn(g, __fsub_rn(sy, sO[3 * kself + 1]));
+    const float d2 = __fmul_rn(g, __fsub_rn(sz, sO[3 * kself + 2]));
+    float ax = 0.f, ay = 0.f, az = 0.f;
+    if (direct_first) {
+        ax = __fadd_rn(ax, d0);
+        ay = __fadd_rn(ay, d1);
+        az = __fadd_rn(az, d2);
+    }
+    for (int p = sOff[tid]; p < sOff[tid + 1]; ++p) {
+        const int j = sSrt[p];
+        const float h = __fmul_rn(sG[j], 2.f);
+        ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(sO[3 * j + 0], sx)));
+        ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(sO[3 * j + 1], sy)));
+        az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(sO[3 * j + 2], sz)));
+    }
+    if (!direct_first) {
+        ax = __fadd_rn(ax, d0);
+        ay = __fadd_rn(ay, d1);
+        az = __fadd_rn(az, d2);
     }
     grad[3 * (size_t)i + 0] = ax;
     grad[3 * (size_t)i + 1] = ay;
@@ -362,32 +1081,122 @@ __global__ __launch_bounds__(kBwdThreads) void chamfer_bwd_kernel(
 
 inline bool bad_dims(int b, int n, int m) { return b < 0 || n < 0 || m < 0; }
 
+// ---- forward variant table (tuning: tools/tune_chamfer.py) -----------------
+typedef void (*fwd_kernel_t)(const float *, const float *, int, int, int, float *, float *,
+                             int32_t *, int32_t *, int, int, float *, unsigned *, float *);
+struct FwdVariant {
+    fwd_kernel_t plain, loss;
+    int waves, qpt;
+    bool sgpr;  // SGPR-stream form (else LDS-tile form)
+};
+#define PCM_FWD_LDS(W, Q)                                                              \
+    FwdVariant{chamfer_fwd_kernel<W, Q, kChunk, kTile, false>,                         \
+               chamfer_fwd_kernel<W, Q, kChunk, kTile, true>, W, Q, false}
+#define PCM_FWD_SGPR(W, Q, C)                                                          \
+    FwdVariant{chamfer_fwd_sgpr_kernel<W, Q, C, false>,                                \
+               chamfer_fwd_sgpr_kernel<W, Q, C, true>, W, Q, false}
+const FwdVariant kFwdVariants[] = {
+    PCM_FWD_LDS(8, 2),       // 0: LDS-tile form
+    PCM_FWD_LDS(8, 4),       // 1
+    PCM_FWD_SGPR(8, 2, 32),  // 2: SGPR-stream form
+    PCM_FWD_SGPR(8, 4, 32),  // 3
+    PCM_FWD_SGPR(4, 2, 32),  // 4
+    PCM_FWD_SGPR(16, 2, 32), // 5
+    PCM_FWD_SGPR(4, 4, 32),  // 6
+    PCM_FWD_SGPR(16, 4, 32), // 7
+    PCM_FWD_SGPR(8, 2, 16),  // 8
+    PCM_FWD_SGPR(16, 2, 16), // 9
+};
+constexpr int kNumFwdVariants = sizeof(kFwdVariants) / sizeof(kFwdVariants[0]);
+// Default policy from tools/tune_chamfer.py on MI355X (profiles/r01): the
+// SGPR-stream form wins everywhere; 2 queries per lane and 16-candidate chunks
+// for ShapeNet-size clouds (B=32, N=M=1024: 12.7 us vs 13.5 us LDS-tile), 4
+// queries per lane once a batch has >= 4M pairs (B=8, N=M=16384: 453 us).
+inline int default_fwd_variant(int n, int m) {
+    return (long long)n * m >= (1LL << 22) ? 3 : 8;
+}
+
+int fwd_grid(const FwdVariant &v, int b, int n, int m, int &nblk1, int &nblk2, long long &blocks) {
+    const int QW = 64 * v.qpt;
+    // a direction with no targets leaves its outputs untouched: give it no blocks
+    nblk1 = (m > 0) ? (n + QW - 1) / QW : 0;
+    nblk2 = (n > 0) ? (m + QW - 1) / QW : 0;
+    blocks = (long long)b * (nblk1 + nblk2);
+    return blocks > 0x7fffffffLL ? PCM_ERR_UNSUPPORTED : PCM_OK;
+}
+
+int launch_fwd(int variant, const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
+               float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out, void *ws, size_t ws_bytes,
+               void *stream) {
+    if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
+    if (variant < 0 || variant >= kNumFwdVariants) return PCM_ERR_INVALID_ARG;
+    const FwdVariant &v = kFwdVariants[variant];
+    const bool loss = mean_out != nullptr;
+    if (loss && (b == 0 || n == 0 || m == 0)) return PCM_ERR_INVALID_ARG;
+    if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
+    if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2)))
+        return PCM_ERR_INVALID_ARG;
+    int nblk1, nblk2;
+    long long blocks;
+    if (fwd_grid(v, b, n, m, nblk1, nblk2, blocks) != PCM_OK) return PCM_ERR_UNSUPPORTED;
+    if (blocks == 0) return PCM_OK;
+    float *partials = nullptr;
+    unsigned *ticket = nullptr;
+    if (loss) {
+        const size_t need = pcm_chamfer_workspace_bytes(b, n, m);
+        if (!ws || ws_bytes < need) return PCM_ERR_WORKSPACE;
+        ticket = (unsigned *)ws;
+        partials = (float *)((char *)ws + kTicketBytes);
+    }
+    hipLaunchKernelGGL(loss ? v.loss : v.plain, dim3((unsigned)blocks), dim3(64 * v.waves), 0,
+                       (hipStream_t)stream, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nblk1,
+                       nblk2, partials, ticket, mean_out);
+    return pcm_launch_status();
+}
+
 }  // namespace
+
+extern "C" size_t pcm_chamfer_workspace_bytes(int b, int n, int m) {
+    if (b <= 0 || n < 0 || m < 0) return kTicketBytes;
+    long long most = 0;
+    for (int i = 0; i < kNumFwdVariants; ++i) {
+        int n1, n2;
+        long long blocks;
+        fwd_grid(kFwdVariants[i], b, n, m, n1, n2, blocks);
+        most = blocks > most ? blocks : most;
+    }
+    return kTicketBytes + (size_t)most * sizeof(float);
+}
 
 extern "C" int pcm_chamfer_forward(const float *xyz1, const float *xyz2, int b, int n, int m,
                                    float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                    void *stream) {
-    if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
-    if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
-    if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2)))
-        return PCM_ERR_INVALID_ARG;
-    constexpr int QW = 64 * kFwdQPT;
-    // a direction with no targets leaves its outputs untouched: give it no blocks
-    const int nblk1 = (m > 0) ? (n + QW - 1) / QW : 0;
-    const int nblk2 = (n > 0) ? (m + QW - 1) / QW : 0;
-    const long long blocks = (long long)b * (nblk1 + nblk2);
-    if (blocks == 0) return PCM_OK;
-    if (blocks > 0x7fffffffLL) return PCM_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL((chamfer_fwd_kernel<kFwdW, kFwdQPT, kFwdC, kFwdTile>), dim3((unsigned)blocks),
-                       dim3(64 * kFwdW), 0, (hipStream_t)stream, xyz1, xyz2, b, n, m, dist1, dist2,
-                       idx1, idx2, nblk1, nblk2);
-    return pcm_launch_status();
+    return launch_fwd(default_fwd_variant(n, m), xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nullptr,
+                      nullptr, 0, stream);
 }
 
-extern "C" int pcm_chamfer_backward(const float *xyz1, const float *xyz2, int b, int n, int m,
-                                    const float *graddist1, const float *graddist2,
-                                    const int32_t *idx1, const int32_t *idx2, float *gradxyz1,
-                                    float *gradxyz2, void *stream) {
+extern "C" int pcm_chamfer_forward_loss(const float *xyz1, const float *xyz2, int b, int n, int m,
+                                        float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                                        float *mean_out, void *workspace, size_t workspace_bytes,
+                                        void *stream) {
+    if (!mean_out) return PCM_ERR_INVALID_ARG;
+    return launch_fwd(default_fwd_variant(n, m), xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, mean_out,
+                      workspace, workspace_bytes, stream);
+}
+
+extern "C" int pcm_tune_chamfer_forward(int variant, const float *xyz1, const float *xyz2, int b, int n,
+                                        int m, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                                        void *stream) {
+    return launch_fwd(variant, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nullptr, nullptr, 0,
+                      stream);
+}
+
+extern "C" int pcm_tune_num_chamfer_variants(void) { return kNumFwdVariants; }
+
+namespace {
+int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
+               const float *graddist1, const float *graddist2, const int32_t *idx1,
+               const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     // Without targets a direction has no argmins; the reference would read
@@ -395,12 +1204,47 @@ extern "C" int pcm_chamfer_backward(const float *xyz1, const float *xyz2, int b,
     if (n == 0 || m == 0) return PCM_ERR_INVALID_ARG;
     if (!xyz1 || !xyz2 || !graddist1 || !graddist2 || !idx1 || !idx2 || !gradxyz1 || !gradxyz2)
         return PCM_ERR_INVALID_ARG;
-    const int nblk1 = (n + kBwdThreads - 1) / kBwdThreads;
-    const int nblk2 = (m + kBwdThreads - 1) / kBwdThreads;
+    const int nblk1 = (n + kBwdT - 1) / kBwdT;
+    const int nblk2 = (m + kBwdT - 1) / kBwdT;
     const long long blocks = (long long)b * (nblk1 + nblk2);
     if (blocks > 0x7fffffffLL) return PCM_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(chamfer_bwd_kernel, dim3((unsigned)blocks), dim3(kBwdThreads), 0,
+    if (variant == 0 && n <= kBwdStageMax && m <= kBwdStageMax) {
+        hipLaunchKernelGGL(chamfer_bwd_staged_kernel, dim3((unsigned)blocks), dim3(kBwdT), 0,
+                           (hipStream_t)stream, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1,
+                           idx2, gradxyz1, gradxyz2, nblk1, nblk2);
+        return pcm_launch_status();
+    }
+    const size_t lds = bwd_lds_bytes(n, m);
+    if (variant == 2 && lds <= kBwdLdsMax) {
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute((const void *)chamfer_bwd_lds_kernel,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return PCM_ERR_LAUNCH;
+        hipLaunchKernelGGL(chamfer_bwd_lds_kernel, dim3((unsigned)b), dim3(kBwdLdsT), lds,
+                           (hipStream_t)stream, xyz1, xyz2, n, m, graddist1, graddist2, idx1, idx2,
+                           gradxyz1, gradxyz2);
+        return pcm_launch_status();
+    }
+    hipLaunchKernelGGL(chamfer_bwd_kernel, dim3((unsigned)blocks), dim3(kBwdT), 0,
                        (hipStream_t)stream, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2,
                        gradxyz1, gradxyz2, nblk1, nblk2);
     return pcm_launch_status();
+}
+}  // namespace
+
+extern "C" int pcm_chamfer_backward(const float *xyz1, const float *xyz2, int b, int n, int m,
+                                    const float *graddist1, const float *graddist2,
+                                    const int32_t *idx1, const int32_t *idx2, float *gradxyz1,
+                                    float *gradxyz2, void *stream) {
+    return launch_bwd(0, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2,
+                      stream);
+}
+
+extern "C" int pcm_tune_chamfer_backward(int variant, const float *xyz1, const float *xyz2, int b,
+                                         int n, int m, const float *graddist1,
+                                         const float *graddist2, const int32_t *idx1,
+                                         const int32_t *idx2, float *gradxyz1, float *gradxyz2,
+                                         void *stream) {
+    return launch_bwd(variant, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1,
+                      gradxyz2, stream);
 }

@@ -50,6 +50,35 @@ __device__ inline void pcm_ref_nn_scan(float x1, float y1, float z1, const float
     out_i = res_i;
 }
 
+typedef __attribute__((address_space(3))) void pcm_lds_void;
+
+// Asynchronous global -> LDS copy of `nbytes` (multiple of 4) by the W waves of
+// a workgroup using LDS-DMA (global_load_lds_*): no VGPRs, no LDS-write
+// instructions; the caller waits with `s_waitcnt vmcnt(0)` + a barrier before
+// reading.  16 B per lane (1 KiB per wave-instruction) when both ends are
+// 16-byte aligned and nbytes % 16 == 0, else 4 B per lane.
+__device__ __forceinline__ void pcm_dma_to_lds(void *lds_dst, const void *src, int nbytes, int wave,
+                                               int nwaves) {
+    const int lane = threadIdx.x & 63;
+    const char *g = (const char *)src;
+    char *l = (char *)lds_dst;
+    if (((((uintptr_t)g) | ((uintptr_t)l) | (uintptr_t)nbytes) & 15) == 0) {
+        for (int k = wave; k * 1024 < nbytes; k += nwaves) {
+            const int off = k * 1024 + lane * 16;
+            if (off < nbytes)
+                __builtin_amdgcn_global_load_lds((const void *)(g + off), (pcm_lds_void *)(l + k * 1024), 16,
+                                                 0, 0);
+        }
+    } else {
+        for (int k = wave; k * 256 < nbytes; k += nwaves) {
+            const int off = k * 256 + lane * 4;
+            if (off < nbytes)
+                __builtin_amdgcn_global_load_lds((const void *)(g + off), (pcm_lds_void *)(l + k * 256), 4, 0,
+                                                 0);
+        }
+    }
+}
+
 static inline int pcm_launch_status() {
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? PCM_OK : PCM_ERR_LAUNCH;

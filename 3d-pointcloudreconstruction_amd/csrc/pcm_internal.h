@@ -1,0 +1,18 @@
+// pcm_internal.h -- tuning entry points exported by libpcm_hip.so but not part
+// of the public C ABI (include/pcm.h).  Used by tools/tune_chamfer.py to A/B
+// kernel variants inside one process (cdna_hip_programming.md section 5.4
+// rule 24).
+#pragma once
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+int pcm_tune_num_chamfer_variants(void);
+int pcm_tune_chamfer_forward(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
+                             float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, void *stream);
+int pcm_tune_chamfer_backward(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
+                              const float *graddist1, const float *graddist2, const int32_t *idx1,
+                              const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream);
+#ifdef __cplusplus
+}
+#endif

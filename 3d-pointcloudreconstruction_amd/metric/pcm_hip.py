@@ -23,6 +23,7 @@ _lib = None
 EXPORTED = (
     "pcm_version", "pcm_strerror",
     "pcm_chamfer_forward", "pcm_chamfer_backward",
+    "pcm_chamfer_workspace_bytes", "pcm_chamfer_forward_loss",
     "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward",
 )
 
@@ -51,6 +52,16 @@ def load_library():
     L.pcm_chamfer_forward.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
     L.pcm_chamfer_backward.restype = ci
     L.pcm_chamfer_backward.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
+    L.pcm_chamfer_workspace_bytes.restype = cs
+    L.pcm_chamfer_workspace_bytes.argtypes = [ci, ci, ci]
+    L.pcm_chamfer_forward_loss.restype = ci
+    L.pcm_chamfer_forward_loss.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, cs, vp]
+    L.pcm_tune_num_chamfer_variants.restype = ci
+    L.pcm_tune_num_chamfer_variants.argtypes = []
+    L.pcm_tune_chamfer_forward.restype = ci
+    L.pcm_tune_chamfer_forward.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
+    L.pcm_tune_chamfer_backward.restype = ci
+    L.pcm_tune_chamfer_backward.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
     L.pcm_emd_workspace_bytes.restype = cs
     L.pcm_emd_workspace_bytes.argtypes = [ci, ci]
     L.pcm_emd_forward.restype = ci
@@ -99,6 +110,63 @@ def chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:
         _check(load_library().pcm_chamfer_forward(
             _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
             _stream(dev)), "pcm_chamfer_forward")
+
+
+_ws_cache = {}
+
+
+def chamfer_workspace(dev: torch.device, b: int, n: int, m: int) -> torch.Tensor:
+    """Zero-filled, cached per (device, size) workspace for the fused-loss forward
+    (the kernel leaves it zeroed after every stream-ordered call)."""
+    need = int(load_library().pcm_chamfer_workspace_bytes(b, n, m))
+    key = (dev, need)
+    ws = _ws_cache.get(key)
+    if ws is None:
+        ws = torch.zeros(need, dtype=torch.uint8, device=dev)
+        _ws_cache[key] = ws
+    return ws
+
+
+def chamfer_forward_loss(xyz1, xyz2, dist1, dist2, idx1, idx2, mean_out, workspace=None) -> None:
+    """pcm_chamfer_forward_loss: forward + mean_out[0:2] = (mean(dist1), mean(dist2))."""
+    dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2, mean_out)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    if workspace is None:
+        workspace = chamfer_workspace(dev, b, n, m)
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_chamfer_forward_loss(
+            _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
+            _ptr(mean_out), _ptr(workspace), workspace.numel(), _stream(dev)),
+            "pcm_chamfer_forward_loss")
+
+
+def tune_chamfer_forward(variant, xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:
+    """Internal: launch forward kernel variant `variant` (tools/tune_chamfer.py)."""
+    dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_tune_chamfer_forward(
+            int(variant), _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1),
+            _ptr(idx2), _stream(dev)), "pcm_tune_chamfer_forward")
+
+
+def tune_chamfer_backward(variant, xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1,
+                          gradxyz2) -> None:
+    """Internal: backward path `variant` (0 = automatic: staged, 1 = global-memory kernel, 2 = per-batch LDS kernel)."""
+    dev = _require_device(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_tune_chamfer_backward(
+            int(variant), _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(graddist1), _ptr(graddist2),
+            _ptr(idx1), _ptr(idx2), _ptr(gradxyz1), _ptr(gradxyz2), _stream(dev)),
+            "pcm_tune_chamfer_backward")
+
+
+def tune_num_chamfer_variants() -> int:
+    return int(load_library().pcm_tune_num_chamfer_variants())
 
 
 def chamfer_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2) -> None:

@@ -77,14 +77,15 @@ class ChamferStep:
         self.gx1 = torch.empty(B, N, 3, device=dev)
         self.gx2 = torch.empty(B, M, 3, device=dev)
         self.loss = torch.zeros(2, device=dev)
+        self.ws = pcm_hip.chamfer_workspace(dev, B, N, M)
         self.world = world
 
     def __call__(self):
-        pcm_hip.chamfer_forward(self.xyz1, self.xyz2, self.d1, self.d2, self.i1, self.i2)
-        self.loss[0] = self.d1.sum()
-        self.loss[1] = self.d2.sum()
+        # forward + deterministic in-kernel mean(dist1), mean(dist2)
+        pcm_hip.chamfer_forward_loss(self.xyz1, self.xyz2, self.d1, self.d2, self.i1, self.i2,
+                                     self.loss, self.ws)
         if self.world > 1:
-            dist.all_reduce(self.loss)
+            dist.all_reduce(self.loss)  # sum of per-rank means; /world = global mean
         pcm_hip.chamfer_backward(self.xyz1, self.xyz2, self.g1, self.g2, self.i1, self.i2,
                                  self.gx1, self.gx2)
 

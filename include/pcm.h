@@ -70,6 +70,22 @@ int pcm_chamfer_forward(const float *xyz1, const float *xyz2, int b, int n, int 
                         void *stream);
 
 /*
+ * Fused forward + loss (extension; replaces the torch reductions that
+ * loss/loss.py:34-36 and utils/metrics.py:56-60 run on the forward's outputs):
+ * everything pcm_chamfer_forward does, plus
+ *   mean_out[0] = mean(dist1), mean_out[1] = mean(dist2)   (device float[2])
+ * summed in a fixed order (deterministic run to run).  Needs b, n, m > 0 and a
+ * device workspace of pcm_chamfer_workspace_bytes(b, n, m) bytes that is
+ * ZERO-FILLED when first allocated; each call leaves it zeroed again, so it
+ * can be reused by stream-ordered calls (not by concurrent ones).
+ */
+size_t pcm_chamfer_workspace_bytes(int b, int n, int m);
+int pcm_chamfer_forward_loss(const float *xyz1, const float *xyz2, int b, int n, int m,
+                             float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                             float *mean_out, void *workspace, size_t workspace_bytes,
+                             void *stream);
+
+/*
  * Chamfer backward (chamfer3D.cu:155-195).  With g = 2*graddist:
  *   gradxyz1[j] = g1[j](xyz1[j]-xyz2[idx1[j]]) - sum_{k: idx2[k]=j} g2[k](xyz2[k]-xyz1[j])
  *   gradxyz2[k] = g2[k](xyz2[k]-xyz1[idx2[k]]) - sum_{j: idx1[j]=k} g1[j](xyz1[j]-xyz2[k])

@@ -200,3 +200,66 @@ def test_nondefault_stream_and_repeatability(cuda):
     for o in outs:
         for x, y in zip(o, ref):
             assert torch.equal(x, y)
+
+
+def test_all_forward_variants_bit_identical(cuda, oracle):
+    import pcm_hip
+    a, c = _clouds(41, 4, 1500, 700, "normal")
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    x1, x2 = a.to(cuda), c.to(cuda)
+    for v in range(pcm_hip.tune_num_chamfer_variants()):
+        d1 = torch.empty(4, 1500, device=cuda)
+        d2 = torch.empty(4, 700, device=cuda)
+        i1 = torch.empty(4, 1500, dtype=torch.int32, device=cuda)
+        i2 = torch.empty(4, 700, dtype=torch.int32, device=cuda)
+        pcm_hip.tune_chamfer_forward(v, x1, x2, d1, d2, i1, i2)
+        torch.cuda.synchronize()
+        _assert_fwd_equal((d1.cpu().numpy(), d2.cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()), ref)
+
+
+def test_fused_loss_forward(cuda, oracle):
+    import pcm_hip
+    for (b, n, m, seed) in [(32, 1024, 1024, 51), (3, 1000, 2000, 52), (1, 5, 7, 53)]:
+        a, c = _clouds(seed, b, n, m)
+        x1, x2 = a.to(cuda), c.to(cuda)
+        d1 = torch.empty(b, n, device=cuda)
+        d2 = torch.empty(b, m, device=cuda)
+        i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+        i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+        means = []
+        for _ in range(3):
+            mo = torch.empty(2, device=cuda)
+            pcm_hip.chamfer_forward_loss(x1, x2, d1, d2, i1, i2, mo)
+            means.append(mo.cpu())
+        torch.cuda.synchronize()
+        assert all(torch.equal(means[0], x) for x in means)  # deterministic, ticket reset
+        ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+        _assert_fwd_equal((d1.cpu().numpy(), d2.cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()), ref)
+        r = np.array([ref[0].astype(np.float64).mean(), ref[1].astype(np.float64).mean()])
+        np.testing.assert_allclose(means[0].numpy(), r, rtol=2e-6)
+
+
+@pytest.mark.parametrize("b,n,m", [(32, 1024, 1024), (2, 2048, 2048), (3, 700, 1900), (2, 5000, 300)])
+def test_backward_paths_identical(cuda, oracle, b, n, m):
+    import pcm_hip
+    a, c = _clouds(61, b, n, m)
+    x1, x2 = a.to(cuda), c.to(cuda)
+    d1 = torch.empty(b, n, device=cuda)
+    d2 = torch.empty(b, m, device=cuda)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+    pcm_hip.chamfer_forward(x1, x2, d1, d2, i1, i2)
+    gen = torch.Generator().manual_seed(62)
+    g1 = torch.rand(b, n, generator=gen).to(cuda)
+    g2 = torch.rand(b, m, generator=gen).to(cuda)
+    outs = []
+    for v in (0, 1, 2):
+        gx1 = torch.full((b, n, 3), float("nan"), device=cuda)
+        gx2 = torch.full((b, m, 3), float("nan"), device=cuda)
+        pcm_hip.tune_chamfer_backward(v, x1, x2, g1, g2, i1, i2, gx1, gx2)
+        outs.append((gx1.cpu().numpy(), gx2.cpu().numpy()))
+    r1, r2 = oracle.chamfer_backward(a.numpy(), c.numpy(), g1.cpu().numpy(), g2.cpu().numpy(),
+                                     i1.cpu().numpy(), i2.cpu().numpy())
+    for o1, o2 in outs:
+        np.testing.assert_array_equal(o1.view(np.int32), r1.view(np.int32))
+        np.testing.assert_array_equal(o2.view(np.int32), r2.view(np.int32))

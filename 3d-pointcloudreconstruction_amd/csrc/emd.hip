@@ -2,30 +2,49 @@
 //
 // Replaces the reference's 7-launches-per-iteration host loop
 // (metric/emd/emd_cuda.cu:256-269: clear, calc_unass_cnt, calc_unass_cnt_sum,
-// calc_unass_idx, Bid, GetMax, Assign) with ONE persistent workgroup per batch
-// element that runs every auction iteration in-kernel, keeping the whole
-// auction state (assignment, owner, price, max increment, claim) in LDS and
-// separating the phases with workgroup barriers only -- no grid barrier, no
-// host round trip, 1 launch + 1 epilogue for any `iters`.
+// calc_unass_idx, Bid, GetMax, Assign) by two launches for any `iters`:
 //
-// Determinism: the reference's GetMax lets racing writers decide which of the
-// bidders within the 1e-6 window wins (emd_cuda.cu:188-190); here the window
-// is evaluated exactly as there (double compare) and the LOWEST point index
-// wins via an LDS atomicMin, so results do not depend on scheduling.  The max
-// increment uses an order-preserving int encoding + atomicMax (the reference
-// uses a CAS loop, emd_cuda.cu:10-20) -- same value.
+//  1. emd_seed_kernel (all CUs): iteration 0's bids.  With every price 0 the
+//     bid value v = (float)((3.0 - (double)sqrtf(d)) - 0.0) is a monotone
+//     non-increasing function of the squared distance d, so each point's
+//     nearest candidates by d (16 lanes per point, branch-free top-3 per lane,
+//     then a shuffle extraction of the L = 16 nearest) are exactly the top of
+//     its value list.  The exact bid (best, better, argbest) is read off the
+//     cached entries whenever the cache PROVES it: every uncached object has
+//     d >= D*, hence v <= T = v(D*), so if the cached second-best value > T
+//     nothing outside the cache can enter the top two.  Otherwise the point
+//     is flagged for a full scan.  The cache (16 object ids + T) is kept.
 //
-// Bid: each unassigned point is scanned by a group of G lanes (G = 1024/|U|
-// rounded to a power of two, <= 64), lanes strided over the objects; value
-// v = (float)((3.0 - (double)sqrtf(d)) - (double)price) as emd_cuda.cu:146
-// evaluates it; per-lane top-2 merged across the group with shuffles
-// (lowest index wins ties).
+//  2. emd_auction_kernel (one persistent workgroup per batch element): every
+//     auction iteration in-kernel with the whole auction state (assignment,
+//     owner, price, max increment, claim) in LDS and workgroup barriers only.
+//     An unassigned point re-bids from its cache (16 lanes evaluate the 16
+//     cached objects at CURRENT prices): prices only rise, so uncached values
+//     are still <= T and the same proof applies.  Points whose cache cannot
+//     prove the top two are re-scanned in full by one wave each, which also
+//     rebuilds their cache from the value-ordered candidates.
+//
+// The cache only skips evaluations that provably cannot change the bid, so
+// the results are identical to scanning every object every iteration (the
+// oracle does exactly that).  Tie rules: argbest = lowest index among equal
+// best values (the reference's strict '>' scan, emd_cuda.cu:147); `better` is
+// the second largest value of the multiset; GetMax's 1e-6 window is evaluated
+// in double exactly as emd_cuda.cu:188 and the LOWEST qualifying point index
+// wins (the reference lets a racing writer win); max increments use an
+// order-preserving int encoding + atomicMax (the reference's CAS loop,
+// emd_cuda.cu:10-20).  Non-finite inputs are outside the reference's
+// contract (coordinates in [0, 1], emd_module.py:9).
 #include "pcm_common.h"
+#include "pcm_internal.h"
 
 namespace {
 
-constexpr int kEmdThreads = 1024;
-constexpr int kEmdMaxN = 4096;  // LDS-resident state: 7 x 4 B x n
+constexpr int kL = 16;             // cached candidates per point
+constexpr int kSeedLanes = 16;     // lanes per point in the seed kernel
+constexpr int kSeedThreads = 256;  // 16 points per workgroup
+constexpr int kEmdThreads = 1024;  // auction workgroup (16 waves)
+constexpr int kEmdMaxN = 4096;     // LDS-resident auction state: 9 x 4 B x n
+constexpr int kEmdStageMaxN = 2048;  // + 12 B x n target-cloud copy up to here
 
 __device__ __forceinline__ int f2key(float f) {
     const int i = __float_as_int(f);
@@ -35,42 +54,262 @@ __device__ __forceinline__ float key2f(int k) {
     return __int_as_float(k ^ ((k >> 31) & 0x7fffffff));
 }
 
-__device__ __forceinline__ float bid_value(float x1, float y1, float z1, float qx, float qy,
-                                           float qz, float price) {
-    const float s = __builtin_sqrtf(pcm_sqd(qx - x1, qy - y1, qz - z1));
+// emd_cuda.cu:142-146: x2 = xyz2 - xyz1 ...; v = 3.0 - sqrtf(d) - price in double
+__device__ __forceinline__ float sqd_to(float x1, float y1, float z1, const float *q) {
+    return pcm_sqd(q[0] - x1, q[1] - y1, q[2] - z1);
+}
+__device__ __forceinline__ float value_of(float d, float price) {
+    const float s = __builtin_sqrtf(d);
     const double v = (3.0 - (double)s) - (double)price;
     return (float)v;
 }
 
-// (best, better, best_i) merge: top-2 of the union, lowest index on equal best
-__device__ __forceinline__ void top2_merge(float &b, float &c, int &bi, float b2, float c2, int bi2) {
-    if (b2 > b || (b2 == b && bi2 >= 0 && (bi < 0 || bi2 < bi))) {
-        c = fmaxf(b, c2);
-        b = b2;
-        bi = bi2;
+// (a better than b) in bid order: larger value, then lower index
+__device__ __forceinline__ bool vk_better(float va, int ka, float vb, int kb) {
+    return va > vb || (va == vb && ka < kb);
+}
+
+// top-2 triple merge (b1, k1, b2): b2 = second largest value of the union
+__device__ __forceinline__ void top2_merge(float &b1, int &k1, float &b2, float ob1, int ok1, float ob2) {
+    if (vk_better(ob1, ok1, b1, k1)) {
+        b2 = fmaxf(b1, ob2);
+        b1 = ob1;
+        k1 = ok1;
     } else {
-        c = fmaxf(c, b2);
+        b2 = fmaxf(b2, ob1);
     }
 }
 
-__global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
-    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps, int iters,
-    float *__restrict__ dist, int32_t *__restrict__ assignment_out, float *__restrict__ price_out) {
-    extern __shared__ __attribute__((aligned(16))) int smem[];
-    int *sAss = smem;                 // [n] assignment (point -> object)
-    int *sInv = sAss + n;             // [n] owner (object -> point)
-    float *sPrice = (float *)(sInv + n);  // [n]
-    int *sMax = (int *)(sPrice + n);  // [n] max increment (f2key)
-    int *sClaim = sMax + n;           // [n] lowest qualifying bidder
-    int *sBid = sClaim + n;           // [n] bid object per point
-    float *sInc = (float *)(sBid + n);  // [n] bid increment per point
-    int *sU = (int *)(sInc + n);      // [n] unassigned list
-    __shared__ int sNu;
+// ---- DPP cross-lane steps (VALU operand modifiers: no LDS crossbar round trip).
+// Lanes the DPP pattern does not feed keep their own value (old = self), so a
+// combine with it is a no-op for idempotent selections.  Hillis-Steele:
+// row_shr 1,2,4,8 leaves each 16-lane row's result in its lane 15; row_bcast
+// 15 and 31 then carry it across rows so lane 63 holds the wave's result.
+constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
+constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143;
 
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ int dpp_i(int x) {
+    return __builtin_amdgcn_update_dpp(x, x, CTRL, ROWMASK, 0xf, false);
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, ROWMASK,
+                                                      0xf, false));
+}
+
+// argbest under (v desc, k asc) -- combine of two candidates
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void dpp_argmax_step(float &v, int &k) {
+    const float ov = dpp_f<CTRL, ROWMASK>(v);
+    const int ok = dpp_i<CTRL, ROWMASK>(k);
+    if (vk_better(ov, ok, v, k)) { v = ov; k = ok; }
+}
+// argbest under (d asc, k asc)
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void dpp_argmin_step(float &d, int &k) {
+    const float od = dpp_f<CTRL, ROWMASK>(d);
+    const int ok = dpp_i<CTRL, ROWMASK>(k);
+    if (od < d || (od == d && ok < k)) { d = od; k = ok; }
+}
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void dpp_top2_step(float &b1, int &k1, float &b2) {
+    const float ob1 = dpp_f<CTRL, ROWMASK>(b1);
+    const int ok1 = dpp_i<CTRL, ROWMASK>(k1);
+    const float ob2 = dpp_f<CTRL, ROWMASK>(b2);
+    top2_merge(b1, k1, b2, ob1, ok1, ob2);
+}
+
+// 16-lane row reductions: result valid in lane 15 of each row
+__device__ __forceinline__ void row_argmin(float &d, int &k) {
+    dpp_argmin_step<kDppRowShr1, 0xf>(d, k);
+    dpp_argmin_step<kDppRowShr2, 0xf>(d, k);
+    dpp_argmin_step<kDppRowShr4, 0xf>(d, k);
+    dpp_argmin_step<kDppRowShr8, 0xf>(d, k);
+}
+__device__ __forceinline__ void row_top2(float &b1, int &k1, float &b2) {
+    dpp_top2_step<kDppRowShr1, 0xf>(b1, k1, b2);
+    dpp_top2_step<kDppRowShr2, 0xf>(b1, k1, b2);
+    dpp_top2_step<kDppRowShr4, 0xf>(b1, k1, b2);
+    dpp_top2_step<kDppRowShr8, 0xf>(b1, k1, b2);
+}
+__device__ __forceinline__ float row_min(float d) {
+    d = fminf(d, dpp_f<kDppRowShr1, 0xf>(d));
+    d = fminf(d, dpp_f<kDppRowShr2, 0xf>(d));
+    d = fminf(d, dpp_f<kDppRowShr4, 0xf>(d));
+    d = fminf(d, dpp_f<kDppRowShr8, 0xf>(d));
+    return d;
+}
+// full-wave reductions: result returned wave-uniform (read from lane 63)
+__device__ __forceinline__ void wave_argmax(float &v, int &k) {
+    dpp_argmax_step<kDppRowShr1, 0xf>(v, k);
+    dpp_argmax_step<kDppRowShr2, 0xf>(v, k);
+    dpp_argmax_step<kDppRowShr4, 0xf>(v, k);
+    dpp_argmax_step<kDppRowShr8, 0xf>(v, k);
+    dpp_argmax_step<kDppRowBcast15, 0xa>(v, k);
+    dpp_argmax_step<kDppRowBcast31, 0xc>(v, k);
+    v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+    k = __builtin_amdgcn_readlane(k, 63);
+}
+__device__ __forceinline__ float wave_max(float v) {
+    v = fmaxf(v, dpp_f<kDppRowShr1, 0xf>(v));
+    v = fmaxf(v, dpp_f<kDppRowShr2, 0xf>(v));
+    v = fmaxf(v, dpp_f<kDppRowShr4, 0xf>(v));
+    v = fmaxf(v, dpp_f<kDppRowShr8, 0xf>(v));
+    v = fmaxf(v, dpp_f<kDppRowBcast15, 0xa>(v));
+    v = fmaxf(v, dpp_f<kDppRowBcast31, 0xc>(v));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+// value of lane 15 of this lane's 16-lane row
+__device__ __forceinline__ float row_last_f(float x) { return __shfl(x, (threadIdx.x & 48) | 15, 64); }
+__device__ __forceinline__ int row_last_i(int x) { return __shfl(x, (threadIdx.x & 48) | 15, 64); }
+
+// ===========================================================================
+// 1. seed kernel: iteration-0 bids + caches, 16 lanes per point
+// ===========================================================================
+__global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps,
+    int32_t *__restrict__ cache_idx, float *__restrict__ cache_T, int32_t *__restrict__ bid0,
+    float *__restrict__ inc0) {
     const int tid = threadIdx.x;
-    const int batch = blockIdx.x;
+    const int gl = tid & (kSeedLanes - 1);  // lane within the point's group
+    const int pt = blockIdx.x * (kSeedThreads / kSeedLanes) + tid / kSeedLanes;  // global point id
+    const int batch = pt / n;
+    const int j = pt - batch * n;
     const float *P = xyz1 + (size_t)batch * n * 3;
     const float *Qc = xyz2 + (size_t)batch * n * 3;
+    const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
+
+    // lane-local 3 smallest d (objects k = gl, gl+16, ... ascending: strict '<'
+    // keeps the lower index on ties)
+    float d1 = PCM_INF, d2 = PCM_INF, d3 = PCM_INF;
+    int k1 = 0x7fffffff, k2 = 0x7fffffff;
+    for (int k = gl; k < n; k += kSeedLanes) {
+        const float d = sqd_to(x1, y1, z1, Qc + 3 * (size_t)k);
+        const bool c1 = d < d1, c2 = d < d2;
+        d3 = c2 ? d2 : fminf(d, d3);
+        k2 = c1 ? k1 : (c2 ? k : k2);
+        d2 = c1 ? d1 : fminf(d, d2);
+        k1 = c1 ? k : k1;
+        d1 = fminf(d, d1);
+    }
+    // every object outside the lanes' top-2 has d >= min over lanes of d3
+    // (the group is one 16-lane DPP row; row results land in its lane 15)
+    const float D3 = row_last_f(row_min(d3));
+
+    // extract the kL+1 smallest (d, k) among the group's 32 candidates; the
+    // group's lane r keeps the r-th extracted entry
+    float myd = PCM_INF;
+    int myk = 0x7fffffff;
+    float dL = PCM_INF;  // the (kL+1)-th candidate's d
+    for (int r = 0; r <= kL; ++r) {
+        float bd = d1;
+        int bk = k1;
+        row_argmin(bd, bk);
+        bd = row_last_f(bd);
+        bk = row_last_i(bk);
+        if (r < kL) {
+            if (gl == r) { myd = bd; myk = bk; }
+        } else {
+            dL = bd;
+        }
+        if (bk == k1) { d1 = d2; k1 = k2; d2 = PCM_INF; k2 = 0x7fffffff; }  // pop the winner
+    }
+    if ((unsigned)myk >= (unsigned)n) myk = 0;  // only with non-finite inputs: keep ids valid
+    const float Dstar = fminf(D3, dL);
+    // values of the cached entries at price 0; T bounds every uncached value
+    const float v = value_of(myd, 0.f);
+    const float T = value_of(Dstar, 0.f);
+    float b1 = v, b2 = -PCM_INF;
+    int kb = myk;
+    row_top2(b1, kb, b2);  // valid in the row's lane 15
+    cache_idx[(size_t)pt * kL + gl] = myk;
+    if (gl == kSeedLanes - 1) {
+        cache_T[pt] = T;
+        const bool proven = b2 > T && (unsigned)kb < (unsigned)n;
+        bid0[pt] = proven ? kb : -2;  // -2: needs a full scan in the auction kernel
+        inc0[pt] = b1 - b2 + eps;
+    }
+}
+
+// ===========================================================================
+// 2. auction kernel: one workgroup per batch element, all iterations
+// ===========================================================================
+
+// full scan of point j by ONE wave at current prices: exact (b1, kb, b2) and a
+// rebuilt cache (kL best by value, lowest index on ties; T bounds the rest)
+__device__ __forceinline__ void full_scan_wave(const float *__restrict__ P, const float *__restrict__ Qc,
+                                               int n, int j, const float *sPrice,
+                                               int32_t *__restrict__ cidx, float *__restrict__ cT,
+                                               float &out_b1, int &out_kb, float &out_b2) {
+    const int lane = threadIdx.x & 63;
+    const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
+    // lane-local top-2 by (v desc, k asc) and third-best value
+    float v1 = -PCM_INF, v2 = -PCM_INF, v3 = -PCM_INF;
+    int q1 = 0x7fffffff, q2 = 0x7fffffff;
+#pragma unroll 4
+    for (int k = lane; k < n; k += 64) {
+        const float v = value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), sPrice[k]);
+        const bool c1 = v > v1, c2 = v > v2;
+        v3 = c2 ? v2 : fmaxf(v, v3);
+        q2 = c1 ? q1 : (c2 ? k : q2);
+        v2 = c1 ? v1 : fmaxf(v, v2);
+        q1 = c1 ? k : q1;
+        v1 = fmaxf(v, v1);
+    }
+    const float V3 = wave_max(v3);
+    float vL = -PCM_INF, e1 = 0.f, e2 = 0.f;
+    int e1k = 0;
+    for (int r = 0; r <= kL; ++r) {
+        float bv = v1;
+        int bk = q1;
+        wave_argmax(bv, bk);  // wave-uniform result
+        if (r < kL) {
+            if (lane == r) cidx[r] = (unsigned)bk < (unsigned)n ? bk : 0;
+            if (r == 0) { e1 = bv; e1k = bk; }
+            if (r == 1) e2 = bv;
+        } else {
+            vL = bv;
+        }
+        if (bk == q1) { v1 = v2; q1 = q2; v2 = -PCM_INF; q2 = 0x7fffffff; }
+    }
+    if (lane == 0) *cT = fmaxf(V3, vL);
+    out_b1 = e1;
+    out_kb = e1k;
+    out_b2 = e2;
+}
+
+// kStage: the target cloud is copied into LDS (LDS-DMA at kernel start) so
+// the bid evaluations read it with LDS latency instead of L2 latency.
+template <bool kStage>
+__global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps, int iters,
+    int32_t *__restrict__ cache_idx, float *__restrict__ cache_T, const int32_t *__restrict__ bid0,
+    const float *__restrict__ inc0, float *__restrict__ dist, int32_t *__restrict__ assignment_out,
+    float *__restrict__ price_out, int32_t *__restrict__ stats) {
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    int *sAss = smem;                     // [n] assignment (point -> object)
+    int *sInv = sAss + n;                 // [n] owner (object -> point)
+    float *sPrice = (float *)(sInv + n);  // [n]
+    int *sMax = (int *)(sPrice + n);      // [n] max increment (f2key)
+    int *sClaim = sMax + n;               // [n] lowest qualifying bidder
+    int *sBid = sClaim + n;               // [n] bid object per point
+    float *sInc = (float *)(sBid + n);    // [n] bid increment per point
+    int *sU = (int *)(sInc + n);          // [n] unassigned list
+    int *sMiss = sU + n;                  // [n] points needing a full scan
+    float *sQ = (float *)(sMiss + n);     // [3n] target cloud copy (kStage)
+    __shared__ int sNu, sNm;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    const int batch = blockIdx.x;
+    const float *P = xyz1 + (size_t)batch * n * 3;
+    const float *Qg = xyz2 + (size_t)batch * n * 3;
+    if (kStage) pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kEmdThreads / 64);
+    const float *Qc = kStage ? (const float *)sQ : Qg;
+    int32_t *C = cache_idx + (size_t)batch * n * kL;
+    float *CT = cache_T + (size_t)batch * n;
 
     for (int j = tid; j < n; j += kEmdThreads) {
         sAss[j] = -1;
@@ -79,10 +318,18 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
         sMax[j] = f2key(0.f);  // emd_module.py:49 zero-inits max_increments
         sClaim[j] = 0x7fffffff;
     }
-    if (tid == 0) sNu = 0;
+    if (tid == 0) { sNu = 0; sNm = 0; }
+    if (kStage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA has landed
     __syncthreads();
 
-    const int lane = tid & 63;
+    // diagnostics only (stats != nullptr): per-phase wall time of batch 0
+    unsigned long long tprev = __builtin_amdgcn_s_memrealtime();
+#define PCM_EMD_PHASE(i)                                                               \
+    if (stats && tid == 0 && blockIdx.x == 0) {                                        \
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();               \
+        atomicAdd(&stats[2 * iters + (i)], (int)(tn - tprev));                         \
+        tprev = tn;                                                                    \
+    }
     for (int it = 0; it < iters; ++it) {
         const bool last = (it == iters - 1);
         // ---- A: compact the unassigned points (order irrelevant downstream)
@@ -90,53 +337,78 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
             const int j = j0 + tid;
             const bool un = (j < n) && sAss[j] == -1;
             const unsigned long long bal = __ballot(un);
-            const int below = __popcll(bal & ((1ull << lane) - 1ull));
             int base = 0;
             if (lane == 0 && bal) base = atomicAdd(&sNu, __popcll(bal));
             base = __shfl(base, 0, 64);
-            if (un) sU[base + below] = j;
+            if (un) sU[base + __popcll(bal & ((1ull << lane) - 1ull))] = j;
         }
         __syncthreads();
+        PCM_EMD_PHASE(0);
         const int nu = sNu;
         if (nu == 0) break;  // nothing left to bid: later iterations are no-ops
 
-        // ---- B: bids.  G lanes per unassigned point.
-        int G = 64;
-        while (G > 1 && G * nu > kEmdThreads) G >>= 1;
-        const int P_ = kEmdThreads / G;  // points in flight
-        const int g = tid / G;           // group id
-        const int gl = tid - g * G;      // lane in group
-        for (int u0 = 0; u0 < nu; u0 += P_) {
-            const int u = u0 + g;
-            const bool active = u < nu;
-            const int j = active ? sU[u] : 0;
-            const float x1 = P[3 * (size_t)j + 0];
-            const float y1 = P[3 * (size_t)j + 1];
-            const float z1 = P[3 * (size_t)j + 2];
-            float best = -1e9f, better = -1e9f;
-            int best_i = -1;
-            if (active) {
-                for (int k = gl; k < n; k += G) {
-                    const float d = bid_value(x1, y1, z1, Qc[3 * (size_t)k + 0], Qc[3 * (size_t)k + 1],
-                                              Qc[3 * (size_t)k + 2], sPrice[k]);
-                    if (d > best) { better = best; best = d; best_i = k; }
-                    else if (d > better) { better = d; }
+        // ---- B1: bids from the caches (16 lanes per point), misses listed
+        if (it == 0) {
+            for (int u = tid; u < nu; u += kEmdThreads) {
+                const int j = sU[u];
+                const int k = bid0[(size_t)batch * n + j];
+                if (k >= 0) {
+                    const float inc = inc0[(size_t)batch * n + j];
+                    sBid[j] = k;
+                    sInc[j] = inc;
+                    atomicMax(&sMax[k], f2key(inc));
+                } else {
+                    sMiss[atomicAdd(&sNm, 1)] = j;
                 }
             }
-            for (int o = 1; o < G; o <<= 1) {
-                const float b2 = __shfl_xor(best, o, 64);
-                const float c2 = __shfl_xor(better, o, 64);
-                const int i2 = __shfl_xor(best_i, o, 64);
-                top2_merge(best, better, best_i, b2, c2, i2);
-            }
-            if (active && gl == 0) {
-                const float inc = best - better + eps;
-                sBid[j] = best_i;
-                sInc[j] = inc;
-                if (best_i >= 0) atomicMax(&sMax[best_i], f2key(inc));
+        } else {
+            const int g = tid / kL, gl = tid % kL;
+            for (int u0 = 0; u0 < nu; u0 += kEmdThreads / kL) {
+                const int u = u0 + g;
+                const bool act = u < nu;
+                const int j = act ? sU[u] : 0;
+                const int k = C[(size_t)j * kL + gl];
+                const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
+                float b1 = value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), sPrice[k]);
+                float b2 = -PCM_INF;
+                int kb = k;
+                static_assert(kL == 16, "one cache = one 16-lane DPP row");
+                row_top2(b1, kb, b2);  // valid in the row's lane 15
+                if (act && gl == kL - 1) {
+                    if (b2 > CT[j]) {
+                        const float inc = b1 - b2 + eps;
+                        sBid[j] = kb;
+                        sInc[j] = inc;
+                        atomicMax(&sMax[kb], f2key(inc));
+                    } else {
+                        sMiss[atomicAdd(&sNm, 1)] = j;
+                    }
+                }
             }
         }
         __syncthreads();
+        PCM_EMD_PHASE(1);
+        // ---- B2: full scans (one wave per missed point), cache rebuilt
+        const int nm = sNm;
+        if (stats && tid == 0) {  // diagnostics: [iter] -> (unassigned, full scans), summed over batches
+            atomicAdd(&stats[2 * it], nu);
+            atomicAdd(&stats[2 * it + 1], nm);
+        }
+        for (int q = wave; q < nm; q += kEmdThreads / 64) {
+            const int j = sMiss[q];
+            float b1, b2;
+            int kb;
+            full_scan_wave(P, Qc, n, j, sPrice, C + (size_t)j * kL, CT + j, b1, kb, b2);
+            if (lane == 0) {
+                const float inc = b1 - b2 + eps;
+                const bool valid = (unsigned)kb < (unsigned)n;  // all-NaN values: no bid (oracle: best_i = -1)
+                sBid[j] = valid ? kb : -1;
+                sInc[j] = inc;
+                if (valid) atomicMax(&sMax[kb], f2key(inc));
+            }
+        }
+        __syncthreads();
+        PCM_EMD_PHASE(2);
 
         // ---- C: claim -- lowest bidder inside the reference's 1e-6 window
         for (int u = tid; u < nu; u += kEmdThreads) {
@@ -148,6 +420,7 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
             if (bi - 1e-6 <= mi && mi <= bi + 1e-6) atomicMin(&sClaim[k], j);
         }
         __syncthreads();
+        PCM_EMD_PHASE(3);
 
         // ---- D: assign (emd_cuda.cu:196-215).  On the last iteration every
         // bidder takes its object; prices/owners are then dead state and are
@@ -168,12 +441,14 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
             }
         }
         __syncthreads();
+        PCM_EMD_PHASE(4);
         for (int u = tid; u < nu; u += kEmdThreads) {
             const int k = sBid[sU[u]];
             if (k >= 0) sClaim[k] = 0x7fffffff;
         }
-        if (tid == 0) sNu = 0;
+        if (tid == 0) { sNu = 0; sNm = 0; }
         __syncthreads();
+        PCM_EMD_PHASE(5);
     }
 
     // ---- CalcDist (emd_cuda.cu:217-226): deltas xyz1 - xyz2
@@ -206,34 +481,70 @@ __global__ void emd_bwd_kernel(const float *__restrict__ xyz1, const float *__re
     }
 }
 
-size_t emd_lds_bytes(int n) { return (size_t)8 * 4 * n; }
+size_t emd_lds_bytes(int n) { return (size_t)9 * 4 * n; }
+
+// workspace layout: cache_idx [b*n*kL] i32 | cache_T [b*n] f32 | bid0 [b*n] i32 | inc0 [b*n] f32
+size_t ws_bytes(int b, int n) {
+    const size_t pts = (size_t)b * n;
+    return pts * kL * 4 + pts * 4 * 3;
+}
 
 }  // namespace
 
 extern "C" size_t pcm_emd_workspace_bytes(int b, int n) {
-    (void)b;
-    (void)n;
-    return 0;  // v1 keeps the whole auction state in LDS
+    if (b <= 0 || n <= 0) return 0;
+    return ws_bytes(b, n);
 }
 
-extern "C" int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int n, float eps,
-                               int iters, float *dist, int32_t *assignment, float *price,
-                               void *workspace, size_t workspace_bytes, void *stream) {
-    (void)workspace;
-    (void)workspace_bytes;
+namespace {
+int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters, float *dist,
+               int32_t *assignment, float *price, void *workspace, size_t workspace_bytes,
+               int32_t *stats, void *stream) {
     // emd_cuda.cu:236-249 (n == m is enforced by the single n here)
     if (b < 0 || n < 0 || b > 512 || n % 1024 != 0 || iters < 1) return PCM_ERR_INVALID_ARG;
     if (b == 0 || n == 0) return PCM_OK;
     if (!xyz1 || !xyz2 || !dist || !assignment) return PCM_ERR_INVALID_ARG;
     if (n > kEmdMaxN) return PCM_ERR_UNSUPPORTED;
-    const size_t lds = emd_lds_bytes(n);
+    if (!workspace || workspace_bytes < ws_bytes(b, n)) return PCM_ERR_WORKSPACE;
+    const size_t pts = (size_t)b * n;
+    int32_t *cache_idx = (int32_t *)workspace;
+    float *cache_T = (float *)(cache_idx + pts * kL);
+    int32_t *bid0 = (int32_t *)(cache_T + pts);
+    float *inc0 = (float *)(bid0 + pts);
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(emd_seed_kernel, dim3((unsigned)(pts / (kSeedThreads / kSeedLanes))),
+                       dim3(kSeedThreads), 0, s, xyz1, xyz2, n, eps, cache_idx, cache_T, bid0, inc0);
+    const bool stage = n <= kEmdStageMaxN;
+    const size_t lds = emd_lds_bytes(n) + (stage ? (size_t)12 * n : 0);
+    const void *kfn = stage ? (const void *)emd_auction_kernel<true> : (const void *)emd_auction_kernel<false>;
     if (lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void *)emd_auction_kernel,
-                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
         return PCM_ERR_LAUNCH;
-    hipLaunchKernelGGL(emd_auction_kernel, dim3(b), dim3(kEmdThreads), lds, (hipStream_t)stream, xyz1,
-                       xyz2, n, eps, iters, dist, assignment, price);
+    if (stage)
+        hipLaunchKernelGGL(emd_auction_kernel<true>, dim3(b), dim3(kEmdThreads), lds, s, xyz1, xyz2, n, eps,
+                           iters, cache_idx, cache_T, bid0, inc0, dist, assignment, price, stats);
+    else
+        hipLaunchKernelGGL(emd_auction_kernel<false>, dim3(b), dim3(kEmdThreads), lds, s, xyz1, xyz2, n,
+                           eps, iters, cache_idx, cache_T, bid0, inc0, dist, assignment, price, stats);
     return pcm_launch_status();
+}
+}  // namespace
+
+extern "C" int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int n, float eps,
+                               int iters, float *dist, int32_t *assignment, float *price,
+                               void *workspace, size_t workspace_bytes, void *stream) {
+    return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, price, workspace, workspace_bytes,
+                      nullptr, stream);
+}
+
+// diagnostics: stats[2*it] += unassigned points, stats[2*it+1] += full scans
+// (summed over the batch; caller zero-fills int32[2*iters])
+extern "C" int pcm_tune_emd_forward_stats(const float *xyz1, const float *xyz2, int b, int n, float eps,
+                                          int iters, float *dist, int32_t *assignment,
+                                          void *workspace, size_t workspace_bytes, int32_t *stats,
+                                          void *stream) {
+    return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, nullptr, workspace,
+                      workspace_bytes, stats, stream);
 }
 
 extern "C" int pcm_emd_backward(const float *xyz1, const float *xyz2, int b, int n,

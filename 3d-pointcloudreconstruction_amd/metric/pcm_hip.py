@@ -62,6 +62,8 @@ def load_library():
     L.pcm_tune_chamfer_forward.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
     L.pcm_tune_chamfer_backward.restype = ci
     L.pcm_tune_chamfer_backward.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
+    L.pcm_tune_emd_forward_stats.restype = ci
+    L.pcm_tune_emd_forward_stats.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, cs, vp, vp]
     L.pcm_emd_workspace_bytes.restype = cs
     L.pcm_emd_workspace_bytes.argtypes = [ci, ci]
     L.pcm_emd_forward.restype = ci
@@ -189,7 +191,11 @@ def emd_forward(xyz1, xyz2, eps: float, iters: int, dist, assignment, price=None
     b, n, _ = xyz1.shape
     ws_bytes = emd_workspace_bytes(b, n)
     if ws_bytes and (workspace is None or workspace.numel() * workspace.element_size() < ws_bytes):
-        workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        key = ("emd", dev, ws_bytes)
+        workspace = _ws_cache.get(key)
+        if workspace is None:  # content on entry is irrelevant to the kernels
+            workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+            _ws_cache[key] = workspace
     with torch.cuda.device(dev):
         _check(load_library().pcm_emd_forward(
             _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
@@ -203,3 +209,16 @@ def emd_backward(xyz1, xyz2, graddist, assignment, gradxyz1) -> None:
         _check(load_library().pcm_emd_backward(
             _ptr(xyz1), _ptr(xyz2), b, n, _ptr(graddist), _ptr(assignment), _ptr(gradxyz1),
             _stream(dev)), "pcm_emd_backward")
+
+
+def tune_emd_forward_stats(xyz1, xyz2, eps: float, iters: int, dist, assignment, stats) -> None:
+    """Internal: EMD forward that also accumulates per-iteration diagnostics into
+    stats (int32 [iters, 2], zero-filled): unassigned points and full scans."""
+    dev = _require_device(xyz1, xyz2, dist, assignment, stats)
+    b, n, _ = xyz1.shape
+    ws_bytes = emd_workspace_bytes(b, n)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_tune_emd_forward_stats(
+            _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
+            _ptr(ws), ws_bytes, _ptr(stats), _stream(dev)), "pcm_tune_emd_forward_stats")

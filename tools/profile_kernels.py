@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Fixed kernel sequence for rocprofv3 counter passes (BASELINE configs 2 and 3):
+20x Chamfer fused-loss forward, 20x Chamfer backward (B=32, N=M=1024), 3x EMD
+forward (B=16, N=1024, 50 iters, eps 0.005).  Inputs resident before the loop."""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric"))
+import pcm_hip  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    g = torch.Generator().manual_seed(0)
+    B, N = 32, 1024
+    x1 = torch.rand(B, N, 3, generator=g).to(dev)
+    x2 = torch.rand(B, N, 3, generator=g).to(dev)
+    d1, d2 = torch.empty(B, N, device=dev), torch.empty(B, N, device=dev)
+    i1 = torch.empty(B, N, dtype=torch.int32, device=dev)
+    i2 = torch.empty(B, N, dtype=torch.int32, device=dev)
+    g1 = torch.full((B, N), 1.0 / (B * N), device=dev)
+    g2 = torch.full((B, N), 1.0 / (B * N), device=dev)
+    gx1, gx2 = torch.empty(B, N, 3, device=dev), torch.empty(B, N, 3, device=dev)
+    mo = torch.empty(2, device=dev)
+    ws = pcm_hip.chamfer_workspace(dev, B, N, N)
+    e1 = torch.rand(16, 1024, 3, generator=g).to(dev)
+    e2 = torch.rand(16, 1024, 3, generator=g).to(dev)
+    ed = torch.empty(16, 1024, device=dev)
+    ea = torch.empty(16, 1024, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    for _ in range(20):
+        pcm_hip.chamfer_forward_loss(x1, x2, d1, d2, i1, i2, mo, ws)
+    for _ in range(20):
+        pcm_hip.chamfer_backward(x1, x2, g1, g2, i1, i2, gx1, gx2)
+    for _ in range(3):
+        pcm_hip.emd_forward(e1, e2, 0.005, 50, ed, ea)
+    torch.cuda.synchronize()
+    print("done")
+
+
+if __name__ == "__main__":
+    main()

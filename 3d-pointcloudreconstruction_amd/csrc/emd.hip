@@ -39,9 +39,8 @@
 
 namespace {
 
-constexpr int kL = 16;             // cached candidates per point
-constexpr int kSeedLanes = 16;     // lanes per point in the seed kernel
-constexpr int kSeedThreads = 256;  // 16 points per workgroup
+constexpr int kL = 32;             // cache slots per point (unused slots hold -1)
+constexpr int kSeedThreads = 256;  // one wave per point, 4 points per workgroup
 constexpr int kEmdThreads = 1024;  // auction workgroup (16 waves)
 constexpr int kEmdMaxN = 4096;     // LDS-resident auction state: 9 x 4 B x n
 constexpr int kEmdStageMaxN = 2048;  // + 12 B x n target-cloud copy up to here
@@ -58,10 +57,12 @@ __device__ __forceinline__ float key2f(int k) {
 __device__ __forceinline__ float sqd_to(float x1, float y1, float z1, const float *q) {
     return pcm_sqd(q[0] - x1, q[1] - y1, q[2] - z1);
 }
-__device__ __forceinline__ float value_of(float d, float price) {
-    const float s = __builtin_sqrtf(d);
+__device__ __forceinline__ float value_from_s(float s, float price) {
     const double v = (3.0 - (double)s) - (double)price;
     return (float)v;
+}
+__device__ __forceinline__ float value_of(float d, float price) {
+    return value_from_s(__builtin_sqrtf(d), price);  // correctly rounded sqrtf
 }
 
 // (a better than b) in bid order: larger value, then lower index
@@ -98,20 +99,6 @@ __device__ __forceinline__ float dpp_f(float x) {
                                                       0xf, false));
 }
 
-// argbest under (v desc, k asc) -- combine of two candidates
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ void dpp_argmax_step(float &v, int &k) {
-    const float ov = dpp_f<CTRL, ROWMASK>(v);
-    const int ok = dpp_i<CTRL, ROWMASK>(k);
-    if (vk_better(ov, ok, v, k)) { v = ov; k = ok; }
-}
-// argbest under (d asc, k asc)
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ void dpp_argmin_step(float &d, int &k) {
-    const float od = dpp_f<CTRL, ROWMASK>(d);
-    const int ok = dpp_i<CTRL, ROWMASK>(k);
-    if (od < d || (od == d && ok < k)) { d = od; k = ok; }
-}
 template <int CTRL, int ROWMASK>
 __device__ __forceinline__ void dpp_top2_step(float &b1, int &k1, float &b2) {
     const float ob1 = dpp_f<CTRL, ROWMASK>(b1);
@@ -121,36 +108,13 @@ __device__ __forceinline__ void dpp_top2_step(float &b1, int &k1, float &b2) {
 }
 
 // 16-lane row reductions: result valid in lane 15 of each row
-__device__ __forceinline__ void row_argmin(float &d, int &k) {
-    dpp_argmin_step<kDppRowShr1, 0xf>(d, k);
-    dpp_argmin_step<kDppRowShr2, 0xf>(d, k);
-    dpp_argmin_step<kDppRowShr4, 0xf>(d, k);
-    dpp_argmin_step<kDppRowShr8, 0xf>(d, k);
-}
 __device__ __forceinline__ void row_top2(float &b1, int &k1, float &b2) {
     dpp_top2_step<kDppRowShr1, 0xf>(b1, k1, b2);
     dpp_top2_step<kDppRowShr2, 0xf>(b1, k1, b2);
     dpp_top2_step<kDppRowShr4, 0xf>(b1, k1, b2);
     dpp_top2_step<kDppRowShr8, 0xf>(b1, k1, b2);
 }
-__device__ __forceinline__ float row_min(float d) {
-    d = fminf(d, dpp_f<kDppRowShr1, 0xf>(d));
-    d = fminf(d, dpp_f<kDppRowShr2, 0xf>(d));
-    d = fminf(d, dpp_f<kDppRowShr4, 0xf>(d));
-    d = fminf(d, dpp_f<kDppRowShr8, 0xf>(d));
-    return d;
-}
 // full-wave reductions: result returned wave-uniform (read from lane 63)
-__device__ __forceinline__ void wave_argmax(float &v, int &k) {
-    dpp_argmax_step<kDppRowShr1, 0xf>(v, k);
-    dpp_argmax_step<kDppRowShr2, 0xf>(v, k);
-    dpp_argmax_step<kDppRowShr4, 0xf>(v, k);
-    dpp_argmax_step<kDppRowShr8, 0xf>(v, k);
-    dpp_argmax_step<kDppRowBcast15, 0xa>(v, k);
-    dpp_argmax_step<kDppRowBcast31, 0xc>(v, k);
-    v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-    k = __builtin_amdgcn_readlane(k, 63);
-}
 __device__ __forceinline__ float wave_max(float v) {
     v = fmaxf(v, dpp_f<kDppRowShr1, 0xf>(v));
     v = fmaxf(v, dpp_f<kDppRowShr2, 0xf>(v));
@@ -160,71 +124,199 @@ __device__ __forceinline__ float wave_max(float v) {
     v = fmaxf(v, dpp_f<kDppRowBcast31, 0xc>(v));
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
-// value of lane 15 of this lane's 16-lane row
-__device__ __forceinline__ float row_last_f(float x) { return __shfl(x, (threadIdx.x & 48) | 15, 64); }
-__device__ __forceinline__ int row_last_i(int x) { return __shfl(x, (threadIdx.x & 48) | 15, 64); }
 
 // ===========================================================================
-// 1. seed kernel: iteration-0 bids + caches, 16 lanes per point
+// Candidate scan + cache selection by ONE wave (64 lanes) for one point.
+//
+// A cache entry is (object id, s = sqrtf(d)): s does not depend on prices, so
+// re-evaluating a cached object later costs the two double subtractions of
+// emd_cuda.cu:146 and nothing else.
+//
+// Selection (no sorting, no extraction rounds): with key = "larger is better,
+// lower object index on ties", each lane keeps its top-2 (key, k, d) and its
+// 3rd-best key.  Cache = every lane-top-2 entry strictly above K3 = max over
+// lanes of the 3rd-best keys (~30 on random clouds): every other object lies
+// at or below K3 -- it is either outside its lane's top-2 (<= that lane's 3rd
+// <= K3) or a top-2 entry not above K3.  If more than kL qualify, fall back
+// to the lane-top-1 entries strictly above K2 = max over lanes of the 2nd
+// keys (same argument).  Two ballots, popcounts, mbcnt.
+// ===========================================================================
+struct LaneTop {
+    float a1, a2, a3;  // keys
+    int q1, q2;        // object ids
+    float d1, d2;      // squared distances of the top-2
+};
+
+__device__ __forceinline__ void lane_top_init(LaneTop &t) {
+    t.a1 = t.a2 = t.a3 = -PCM_INF;
+    t.q1 = t.q2 = 0x7fffffff;
+    t.d1 = t.d2 = 0.f;
+}
+// strict '>' while k ascends keeps the lower index on ties
+__device__ __forceinline__ void lane_top_push(LaneTop &t, float key, int k, float d) {
+    const bool c1 = key > t.a1, c2 = key > t.a2;
+    t.a3 = c2 ? t.a2 : fmaxf(key, t.a3);
+    t.q2 = c1 ? t.q1 : (c2 ? k : t.q2);
+    t.d2 = c1 ? t.d1 : (c2 ? d : t.d2);
+    t.a2 = c1 ? t.a1 : fmaxf(key, t.a2);
+    t.q1 = c1 ? k : t.q1;
+    t.d1 = c1 ? d : t.d1;
+    t.a1 = fmaxf(key, t.a1);
+}
+
+// picks the cache entries; writes the ids and s = sqrtf(d) of the chosen
+// entries into cidx/cs (unused slots: id -1).  Returns K* (every uncached
+// key <= K*) or +inf when nothing could be cached.  s1/s2: this lane's
+// entries chosen.
+__device__ __forceinline__ float select_cache(const LaneTop &t, int32_t *__restrict__ cidx,
+                                              float *__restrict__ cs, bool &s1, bool &s2) {
+    const int lane = threadIdx.x & 63;
+    float Kstar = wave_max(t.a3);
+    s1 = t.a1 > Kstar;
+    s2 = t.a2 > Kstar;
+    unsigned long long m1 = __ballot(s1), m2 = __ballot(s2);
+    int cnt = __popcll(m1) + __popcll(m2);
+    if (cnt > kL) {  // wave-uniform
+        Kstar = wave_max(t.a2);
+        s1 = t.a1 > Kstar;
+        s2 = false;
+        m1 = __ballot(s1);
+        m2 = 0ull;
+        cnt = __popcll(m1);
+    }
+    if (cnt > kL) {
+        s1 = s2 = false;
+        m1 = m2 = 0ull;
+        cnt = 0;
+        Kstar = PCM_INF;
+    }
+    const unsigned long long below = (1ull << lane) - 1ull;
+    if (lane < kL && lane >= cnt) cidx[lane] = -1;  // unused slots
+    if (s1) {
+        const int p = __popcll(m1 & below);
+        cidx[p] = t.q1;
+        cs[p] = __builtin_sqrtf(t.d1);
+    }
+    if (s2) {
+        const int p = __popcll(m1) + __popcll(m2 & below);
+        cidx[p] = t.q2;
+        cs[p] = __builtin_sqrtf(t.d2);
+    }
+    return Kstar;
+}
+
+// exact (best, argbest, better) over the wave: each lane offers up to two
+// (value, id) entries; result wave-uniform
+__device__ __forceinline__ void wave_top2(float v1, int k1, float v2, int k2, float &b1, int &kb, float &b2) {
+    if (vk_better(v2, k2, v1, k1)) {
+        const float tv = v1; v1 = v2; v2 = tv;
+        const int tk = k1; k1 = k2; k2 = tk;
+    }
+    b1 = v1; kb = k1; b2 = v2;
+    dpp_top2_step<kDppRowShr1, 0xf>(b1, kb, b2);
+    dpp_top2_step<kDppRowShr2, 0xf>(b1, kb, b2);
+    dpp_top2_step<kDppRowShr4, 0xf>(b1, kb, b2);
+    dpp_top2_step<kDppRowShr8, 0xf>(b1, kb, b2);
+    dpp_top2_step<kDppRowBcast15, 0xa>(b1, kb, b2);
+    dpp_top2_step<kDppRowBcast31, 0xc>(b1, kb, b2);
+    b1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b1), 63));
+    kb = __builtin_amdgcn_readlane(kb, 63);
+    b2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b2), 63));
+}
+
+// ---- seed: key = -d (every price is 0: the bid value is monotone
+// non-increasing in d).  T = v(-K*) bounds every uncached value.  The bid is
+// exact whenever b2 > T (caller checks).
+__device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const float *Qc, int n,
+                                          int32_t *__restrict__ cidx, float *__restrict__ cs,
+                                          float &b1, int &kb, float &b2, float &T) {
+    const int lane = threadIdx.x & 63;
+    LaneTop t;
+    lane_top_init(t);
+#pragma unroll 4
+    for (int k = lane; k < n; k += 64) {
+        const float d = sqd_to(x1, y1, z1, Qc + 3 * (size_t)k);
+        lane_top_push(t, -d, k, d);
+    }
+    bool s1, s2;
+    const float Kstar = select_cache(t, cidx, cs, s1, s2);
+    T = Kstar == PCM_INF ? PCM_INF : value_of(-Kstar, 0.f);
+    wave_top2(s1 ? value_of(t.d1, 0.f) : -PCM_INF, s1 ? t.q1 : 0x7fffffff,
+              s2 ? value_of(t.d2, 0.f) : -PCM_INF, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
+}
+
+// ---- auction full scan, exact: key = the exact bid value.  Always exact
+// bid (the lanes' top-2 hold the global top-2); T = K*.
+__device__ __noinline__ void scan_exact(float x1, float y1, float z1, const float *Qc,
+                                        const float *sPrice, int n, int32_t *__restrict__ cidx,
+                                        float *__restrict__ cs, float &b1, int &kb, float &b2,
+                                        float &T) {
+    const int lane = threadIdx.x & 63;
+    LaneTop t;
+    lane_top_init(t);
+    for (int k = lane; k < n; k += 64) {
+        const float d = sqd_to(x1, y1, z1, Qc + 3 * (size_t)k);
+        lane_top_push(t, value_of(d, sPrice[k]), k, d);
+    }
+    bool s1, s2;
+    T = select_cache(t, cidx, cs, s1, s2);
+    wave_top2(t.a1, t.q1, t.a2, t.q2, b1, kb, b2);
+}
+
+// ---- auction full scan, fast: selection on an fp32 approximation
+//   v' = (3 - sqrt_approx(d)) - price    (v_sqrt_f32, <= 1 ulp)
+// |v' - v| <= 4u(s + price + 3) with u = 2^-23 (1.5 ulp of sqrt + 3 fp32
+// roundings + v's own rounding, with a 2x margin); with the wave maxima of s
+// and price that gives one delta for every object, so
+//   T = K*' + delta
+// bounds every uncached EXACT value.  Exact values are then computed for the
+// cached entries only; if their second best does not exceed T the exact scan
+// runs instead (rare).  Returns false when the fallback is needed.
+__device__ __forceinline__ bool scan_fast(float x1, float y1, float z1, const float *Qc,
+                                          const float *sPrice, int n, int32_t *__restrict__ cidx,
+                                          float *__restrict__ cs, float &b1, int &kb, float &b2,
+                                          float &T) {
+    const int lane = threadIdx.x & 63;
+    LaneTop t;
+    lane_top_init(t);
+    float smax = 0.f, pmax = 0.f;
+#pragma unroll 4
+    for (int k = lane; k < n; k += 64) {
+        const float d = sqd_to(x1, y1, z1, Qc + 3 * (size_t)k);
+        const float s = __builtin_amdgcn_sqrtf(d);
+        const float p = sPrice[k];
+        smax = fmaxf(smax, s);
+        pmax = fmaxf(pmax, p);
+        lane_top_push(t, (3.f - s) - p, k, d);
+    }
+    bool s1, s2;
+    const float Kp = select_cache(t, cidx, cs, s1, s2);
+    const float delta = 4.f * 1.1920929e-7f * (wave_max(smax) + wave_max(pmax) + 3.f);
+    T = Kp + delta;  // +inf stays +inf
+    // exact values of this lane's cached entries
+    const float v1 = s1 ? value_of(t.d1, sPrice[t.q1]) : -PCM_INF;
+    const float v2 = s2 ? value_of(t.d2, sPrice[t.q2]) : -PCM_INF;
+    wave_top2(v1, s1 ? t.q1 : 0x7fffffff, v2, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
+    return b2 > T;
+}
+
+// ===========================================================================
+// 1. seed kernel: iteration-0 bids + caches, one wave per point
 // ===========================================================================
 __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps,
-    int32_t *__restrict__ cache_idx, float *__restrict__ cache_T, int32_t *__restrict__ bid0,
-    float *__restrict__ inc0) {
-    const int tid = threadIdx.x;
-    const int gl = tid & (kSeedLanes - 1);  // lane within the point's group
-    const int pt = blockIdx.x * (kSeedThreads / kSeedLanes) + tid / kSeedLanes;  // global point id
+    int32_t *__restrict__ cache_idx, float *__restrict__ cache_s, float *__restrict__ cache_T,
+    int32_t *__restrict__ bid0, float *__restrict__ inc0) {
+    const int pt = blockIdx.x * (kSeedThreads / 64) + (threadIdx.x >> 6);  // global point id
     const int batch = pt / n;
     const int j = pt - batch * n;
     const float *P = xyz1 + (size_t)batch * n * 3;
     const float *Qc = xyz2 + (size_t)batch * n * 3;
-    const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
-
-    // lane-local 3 smallest d (objects k = gl, gl+16, ... ascending: strict '<'
-    // keeps the lower index on ties)
-    float d1 = PCM_INF, d2 = PCM_INF, d3 = PCM_INF;
-    int k1 = 0x7fffffff, k2 = 0x7fffffff;
-    for (int k = gl; k < n; k += kSeedLanes) {
-        const float d = sqd_to(x1, y1, z1, Qc + 3 * (size_t)k);
-        const bool c1 = d < d1, c2 = d < d2;
-        d3 = c2 ? d2 : fminf(d, d3);
-        k2 = c1 ? k1 : (c2 ? k : k2);
-        d2 = c1 ? d1 : fminf(d, d2);
-        k1 = c1 ? k : k1;
-        d1 = fminf(d, d1);
-    }
-    // every object outside the lanes' top-2 has d >= min over lanes of d3
-    // (the group is one 16-lane DPP row; row results land in its lane 15)
-    const float D3 = row_last_f(row_min(d3));
-
-    // extract the kL+1 smallest (d, k) among the group's 32 candidates; the
-    // group's lane r keeps the r-th extracted entry
-    float myd = PCM_INF;
-    int myk = 0x7fffffff;
-    float dL = PCM_INF;  // the (kL+1)-th candidate's d
-    for (int r = 0; r <= kL; ++r) {
-        float bd = d1;
-        int bk = k1;
-        row_argmin(bd, bk);
-        bd = row_last_f(bd);
-        bk = row_last_i(bk);
-        if (r < kL) {
-            if (gl == r) { myd = bd; myk = bk; }
-        } else {
-            dL = bd;
-        }
-        if (bk == k1) { d1 = d2; k1 = k2; d2 = PCM_INF; k2 = 0x7fffffff; }  // pop the winner
-    }
-    if ((unsigned)myk >= (unsigned)n) myk = 0;  // only with non-finite inputs: keep ids valid
-    const float Dstar = fminf(D3, dL);
-    // values of the cached entries at price 0; T bounds every uncached value
-    const float v = value_of(myd, 0.f);
-    const float T = value_of(Dstar, 0.f);
-    float b1 = v, b2 = -PCM_INF;
-    int kb = myk;
-    row_top2(b1, kb, b2);  // valid in the row's lane 15
-    cache_idx[(size_t)pt * kL + gl] = myk;
-    if (gl == kSeedLanes - 1) {
+    float b1, b2, T;
+    int kb;
+    scan_seed(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, n, cache_idx + (size_t)pt * kL,
+              cache_s + (size_t)pt * kL, b1, kb, b2, T);
+    if ((threadIdx.x & 63) == 0) {
         cache_T[pt] = T;
         const bool proven = b2 > T && (unsigned)kb < (unsigned)n;
         bid0[pt] = proven ? kb : -2;  // -2: needs a full scan in the auction kernel
@@ -236,55 +328,13 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(
 // 2. auction kernel: one workgroup per batch element, all iterations
 // ===========================================================================
 
-// full scan of point j by ONE wave at current prices: exact (b1, kb, b2) and a
-// rebuilt cache (kL best by value, lowest index on ties; T bounds the rest)
-__device__ __forceinline__ void full_scan_wave(const float *__restrict__ P, const float *__restrict__ Qc,
-                                               int n, int j, const float *sPrice,
-                                               int32_t *__restrict__ cidx, float *__restrict__ cT,
-                                               float &out_b1, int &out_kb, float &out_b2) {
-    const int lane = threadIdx.x & 63;
-    const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
-    // lane-local top-2 by (v desc, k asc) and third-best value
-    float v1 = -PCM_INF, v2 = -PCM_INF, v3 = -PCM_INF;
-    int q1 = 0x7fffffff, q2 = 0x7fffffff;
-#pragma unroll 4
-    for (int k = lane; k < n; k += 64) {
-        const float v = value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), sPrice[k]);
-        const bool c1 = v > v1, c2 = v > v2;
-        v3 = c2 ? v2 : fmaxf(v, v3);
-        q2 = c1 ? q1 : (c2 ? k : q2);
-        v2 = c1 ? v1 : fmaxf(v, v2);
-        q1 = c1 ? k : q1;
-        v1 = fmaxf(v, v1);
-    }
-    const float V3 = wave_max(v3);
-    float vL = -PCM_INF, e1 = 0.f, e2 = 0.f;
-    int e1k = 0;
-    for (int r = 0; r <= kL; ++r) {
-        float bv = v1;
-        int bk = q1;
-        wave_argmax(bv, bk);  // wave-uniform result
-        if (r < kL) {
-            if (lane == r) cidx[r] = (unsigned)bk < (unsigned)n ? bk : 0;
-            if (r == 0) { e1 = bv; e1k = bk; }
-            if (r == 1) e2 = bv;
-        } else {
-            vL = bv;
-        }
-        if (bk == q1) { v1 = v2; q1 = q2; v2 = -PCM_INF; q2 = 0x7fffffff; }
-    }
-    if (lane == 0) *cT = fmaxf(V3, vL);
-    out_b1 = e1;
-    out_kb = e1k;
-    out_b2 = e2;
-}
-
 // kStage: the target cloud is copied into LDS (LDS-DMA at kernel start) so
 // the bid evaluations read it with LDS latency instead of L2 latency.
 template <bool kStage>
 __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps, int iters,
-    int32_t *__restrict__ cache_idx, float *__restrict__ cache_T, const int32_t *__restrict__ bid0,
+    int32_t *__restrict__ cache_idx, float *__restrict__ cache_s, float *__restrict__ cache_T,
+    const int32_t *__restrict__ bid0,
     const float *__restrict__ inc0, float *__restrict__ dist, int32_t *__restrict__ assignment_out,
     float *__restrict__ price_out, int32_t *__restrict__ stats) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
@@ -309,6 +359,7 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
     if (kStage) pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kEmdThreads / 64);
     const float *Qc = kStage ? (const float *)sQ : Qg;
     int32_t *C = cache_idx + (size_t)batch * n * kL;
+    float *CS = cache_s + (size_t)batch * n * kL;
     float *CT = cache_T + (size_t)batch * n;
 
     for (int j = tid; j < n; j += kEmdThreads) {
@@ -362,19 +413,27 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
                 }
             }
         } else {
-            const int g = tid / kL, gl = tid % kL;
-            for (int u0 = 0; u0 < nu; u0 += kEmdThreads / kL) {
+            // one 16-lane DPP row per point, two cached (id, s) entries per lane
+            static_assert(kL == 32, "one cache = one 16-lane DPP row x 2 entries");
+            const int g = tid >> 4, gl = tid & 15;
+            for (int u0 = 0; u0 < nu; u0 += kEmdThreads / 16) {
                 const int u = u0 + g;
                 const bool act = u < nu;
                 const int j = act ? sU[u] : 0;
-                const int k = C[(size_t)j * kL + gl];
-                const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
-                float b1 = value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), sPrice[k]);
-                float b2 = -PCM_INF;
-                int kb = k;
-                static_assert(kL == 16, "one cache = one 16-lane DPP row");
-                row_top2(b1, kb, b2);  // valid in the row's lane 15
-                if (act && gl == kL - 1) {
+                const int ka = C[(size_t)j * kL + gl];  // -1: unused slot
+                const int kc = C[(size_t)j * kL + gl + 16];
+                const float sa = CS[(size_t)j * kL + gl];
+                const float sc = CS[(size_t)j * kL + gl + 16];
+                float b1 = ka >= 0 ? value_from_s(sa, sPrice[ka]) : -PCM_INF;
+                int kb = ka >= 0 ? ka : 0x7fffffff;
+                float b2 = kc >= 0 ? value_from_s(sc, sPrice[kc]) : -PCM_INF;
+                int k2 = kc >= 0 ? kc : 0x7fffffff;
+                if (vk_better(b2, k2, b1, kb)) {
+                    const float tv = b1; b1 = b2; b2 = tv;
+                    kb = k2;
+                }
+                row_top2(b1, kb, b2);  // row result in lane 15
+                if (act && gl == 15) {
                     if (b2 > CT[j]) {
                         const float inc = b1 - b2 + eps;
                         sBid[j] = kb;
@@ -396,10 +455,26 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
         }
         for (int q = wave; q < nm; q += kEmdThreads / 64) {
             const int j = sMiss[q];
-            float b1, b2;
+            float b1, b2, T;
             int kb;
-            full_scan_wave(P, Qc, n, j, sPrice, C + (size_t)j * kL, CT + j, b1, kb, b2);
+            const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
+            int32_t *cj = C + (size_t)j * kL;
+            float *sj = CS + (size_t)j * kL;
+            const unsigned long long ts0 = stats ? __builtin_amdgcn_s_memrealtime() : 0ull;
+            const bool fast_ok = scan_fast(x1, y1, z1, Qc, sPrice, n, cj, sj, b1, kb, b2, T);
+            const unsigned long long ts1 = stats ? __builtin_amdgcn_s_memrealtime() : 0ull;
+            if (!fast_ok) scan_exact(x1, y1, z1, Qc, sPrice, n, cj, sj, b1, kb, b2, T);
+            if (stats && lane == 0) {  // diagnostics: fallbacks; wave-0 scan times of batch 0
+                if (!fast_ok) atomicAdd(&stats[2 * iters + 6], 1);
+                if (blockIdx.x == 0 && wave == 0) {
+                    const unsigned long long ts2 = __builtin_amdgcn_s_memrealtime();
+                    atomicAdd(&stats[2 * iters + 7], 1);
+                    atomicAdd(&stats[2 * iters + 8], (int)(ts1 - ts0));
+                    atomicAdd(&stats[2 * iters + 9], (int)(ts2 - ts1));
+                }
+            }
             if (lane == 0) {
+                CT[j] = T;
                 const float inc = b1 - b2 + eps;
                 const bool valid = (unsigned)kb < (unsigned)n;  // all-NaN values: no bid (oracle: best_i = -1)
                 sBid[j] = valid ? kb : -1;
@@ -483,10 +558,11 @@ __global__ void emd_bwd_kernel(const float *__restrict__ xyz1, const float *__re
 
 size_t emd_lds_bytes(int n) { return (size_t)9 * 4 * n; }
 
-// workspace layout: cache_idx [b*n*kL] i32 | cache_T [b*n] f32 | bid0 [b*n] i32 | inc0 [b*n] f32
+// workspace layout: cache_idx [b*n*kL] i32 | cache_s [b*n*kL] f32 | cache_T [b*n] f32 |
+//                   bid0 [b*n] i32 | inc0 [b*n] f32
 size_t ws_bytes(int b, int n) {
     const size_t pts = (size_t)b * n;
-    return pts * kL * 4 + pts * 4 * 3;
+    return pts * kL * 8 + pts * 4 * 3;
 }
 
 }  // namespace
@@ -508,12 +584,13 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     if (!workspace || workspace_bytes < ws_bytes(b, n)) return PCM_ERR_WORKSPACE;
     const size_t pts = (size_t)b * n;
     int32_t *cache_idx = (int32_t *)workspace;
-    float *cache_T = (float *)(cache_idx + pts * kL);
+    float *cache_s = (float *)(cache_idx + pts * kL);
+    float *cache_T = cache_s + pts * kL;
     int32_t *bid0 = (int32_t *)(cache_T + pts);
     float *inc0 = (float *)(bid0 + pts);
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(emd_seed_kernel, dim3((unsigned)(pts / (kSeedThreads / kSeedLanes))),
-                       dim3(kSeedThreads), 0, s, xyz1, xyz2, n, eps, cache_idx, cache_T, bid0, inc0);
+    hipLaunchKernelGGL(emd_seed_kernel, dim3((unsigned)(pts / (kSeedThreads / 64))),
+                       dim3(kSeedThreads), 0, s, xyz1, xyz2, n, eps, cache_idx, cache_s, cache_T, bid0, inc0);
     const bool stage = n <= kEmdStageMaxN;
     const size_t lds = emd_lds_bytes(n) + (stage ? (size_t)12 * n : 0);
     const void *kfn = stage ? (const void *)emd_auction_kernel<true> : (const void *)emd_auction_kernel<false>;
@@ -522,10 +599,10 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
         return PCM_ERR_LAUNCH;
     if (stage)
         hipLaunchKernelGGL(emd_auction_kernel<true>, dim3(b), dim3(kEmdThreads), lds, s, xyz1, xyz2, n, eps,
-                           iters, cache_idx, cache_T, bid0, inc0, dist, assignment, price, stats);
+                           iters, cache_idx, cache_s, cache_T, bid0, inc0, dist, assignment, price, stats);
     else
         hipLaunchKernelGGL(emd_auction_kernel<false>, dim3(b), dim3(kEmdThreads), lds, s, xyz1, xyz2, n,
-                           eps, iters, cache_idx, cache_T, bid0, inc0, dist, assignment, price, stats);
+                           eps, iters, cache_idx, cache_s, cache_T, bid0, inc0, dist, assignment, price, stats);
     return pcm_launch_status();
 }
 }  // namespace

@@ -18,11 +18,14 @@ def main(b=16, n=1024, eps=0.005, iters=50):
     x2 = torch.rand(b, n, 3, generator=g).to(dev)
     d = torch.empty(b, n, device=dev)
     a = torch.empty(b, n, dtype=torch.int32, device=dev)
-    st = torch.zeros(2 * iters + 8, dtype=torch.int32, device=dev)
+    st = torch.zeros(2 * iters + 16, dtype=torch.int32, device=dev)
     pcm_hip.tune_emd_forward_stats(x1, x2, eps, iters, d, a, st)
     torch.cuda.synchronize()
     st = st.cpu()
     ph = st[2 * iters:2 * iters + 6].tolist()
+    fb, nw0, tf, te = st[2 * iters + 6:2 * iters + 10].tolist()
+    print(f"fast-scan fallbacks (all batches): {fb}; batch-0 wave-0 scans: {nw0}, "
+          f"fast {tf / 100.0 / max(nw0, 1):.2f} us/scan, exact-fallback {te / 100.0 / max(nw0, 1):.2f} us/scan")
     st = st[:2 * iters].view(iters, 2)
     names = ["compact", "bid-from-cache", "full-scans", "claim", "assign", "reset"]
     print("batch-0 phase wall time over all iterations (us):",

@@ -43,7 +43,7 @@ constexpr int kL = 32;             // cache slots per point (unused slots hold -
 constexpr int kSeedThreads = 256;  // one wave per point, 4 points per workgroup
 constexpr int kEmdThreads = 1024;  // auction workgroup (16 waves)
 constexpr int kEmdMaxN = 4096;     // LDS-resident auction state: 9 x 4 B x n
-constexpr int kEmdStageMaxN = 2048;  // + 12 B x n target-cloud copy up to here
+constexpr int kEmdStageMaxN = 2048;  // + 24 B x n copies of both clouds up to here
 
 __device__ __forceinline__ int f2key(float f) {
     const int i = __float_as_int(f);
@@ -142,33 +142,49 @@ __device__ __forceinline__ float wave_max(float v) {
 // keys (same argument).  Two ballots, popcounts, mbcnt.
 // ===========================================================================
 struct LaneTop {
-    float a1, a2, a3;  // keys
-    int q1, q2;        // object ids
-    float d1, d2;      // squared distances of the top-2
+    float a1, a2, a3;  // the lane's three largest keys (multiset order)
+    int q1, q2;        // object ids of the top-2
 };
 
 __device__ __forceinline__ void lane_top_init(LaneTop &t) {
     t.a1 = t.a2 = t.a3 = -PCM_INF;
     t.q1 = t.q2 = 0x7fffffff;
-    t.d1 = t.d2 = 0.f;
 }
-// strict '>' while k ascends keeps the lower index on ties
-__device__ __forceinline__ void lane_top_push(LaneTop &t, float key, int k, float d) {
-    const bool c1 = key > t.a1, c2 = key > t.a2;
-    t.a3 = c2 ? t.a2 : fmaxf(key, t.a3);
-    t.q2 = c1 ? t.q1 : (c2 ? k : t.q2);
-    t.d2 = c1 ? t.d1 : (c2 ? d : t.d2);
-    t.a2 = c1 ? t.a1 : fmaxf(key, t.a2);
-    t.q1 = c1 ? k : t.q1;
-    t.d1 = c1 ? d : t.d1;
-    t.a1 = fmaxf(key, t.a1);
+// Insertion into a sorted triple with v_med3: a1' = max(a1, key),
+// a2' = med3(a1, a2, key), a3' = med3(a2, a3, key).  Ids follow with strict
+// '>' while k ascends, so equal keys keep the lower index.  (fmed3 takes its
+// operands as they are: no NaN-canonicalising v_max per loop-carried value.)
+// The id selects are spelled out as v_cmp/v_cndmask in one asm block:
+// written as ternaries, hipcc turns them into exec-mask branches inside the
+// scan loop.  gfx950 needs two wait states between a VALU SGPR write and a
+// v_cndmask reading it as the lane mask (s_nop 1).
+__device__ __forceinline__ void lane_top_push(LaneTop &t, float key, int k) {
+    unsigned long long c1, c2;
+    int tmp;
+    asm("v_cmp_gt_f32_e64 %[c1], %[key], %[a1]\n\t"
+        "v_cmp_gt_f32_e64 %[c2], %[key], %[a2]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[tmp], %[k], %[q1], %[c1]\n\t"   // c1 ? q1 : k
+        "v_cndmask_b32_e64 %[q2], %[q2], %[tmp], %[c2]\n\t"  // c2 ? tmp : q2 (c1 implies c2)
+        "v_cndmask_b32_e64 %[q1], %[q1], %[k], %[c1]"         // c1 ? k : q1
+        : [q1] "+v"(t.q1), [q2] "+v"(t.q2), [tmp] "=&v"(tmp), [c1] "=&s"(c1), [c2] "=&s"(c2)
+        : [key] "v"(key), [a1] "v"(t.a1), [a2] "v"(t.a2), [k] "v"(k));
+    t.a3 = __builtin_amdgcn_fmed3f(t.a2, t.a3, key);
+    t.a2 = __builtin_amdgcn_fmed3f(t.a1, t.a2, key);
+    t.a1 = __builtin_amdgcn_fmed3f(t.a1, key, 3.4028235e38f);  // max (keys are finite)
+}
+
+// squared distance of a lane's entry (recomputed in the pinned order, so it
+// is bit-identical to the value the scan used)
+__device__ __forceinline__ float entry_d(float x1, float y1, float z1, const float *Qc, int n, int q) {
+    return (unsigned)q < (unsigned)n ? sqd_to(x1, y1, z1, Qc + 3 * (size_t)q) : 0.f;
 }
 
 // picks the cache entries; writes the ids and s = sqrtf(d) of the chosen
 // entries into cidx/cs (unused slots: id -1).  Returns K* (every uncached
 // key <= K*) or +inf when nothing could be cached.  s1/s2: this lane's
-// entries chosen.
-__device__ __forceinline__ float select_cache(const LaneTop &t, int32_t *__restrict__ cidx,
+// entries chosen; d1/d2: their squared distances.
+__device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float d2, int32_t *__restrict__ cidx,
                                               float *__restrict__ cs, bool &s1, bool &s2) {
     const int lane = threadIdx.x & 63;
     float Kstar = wave_max(t.a3);
@@ -195,12 +211,12 @@ __device__ __forceinline__ float select_cache(const LaneTop &t, int32_t *__restr
     if (s1) {
         const int p = __popcll(m1 & below);
         cidx[p] = t.q1;
-        cs[p] = __builtin_sqrtf(t.d1);
+        cs[p] = __builtin_sqrtf(d1);
     }
     if (s2) {
         const int p = __popcll(m1) + __popcll(m2 & below);
         cidx[p] = t.q2;
-        cs[p] = __builtin_sqrtf(t.d2);
+        cs[p] = __builtin_sqrtf(d2);
     }
     return Kstar;
 }
@@ -233,16 +249,19 @@ __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const fl
     const int lane = threadIdx.x & 63;
     LaneTop t;
     lane_top_init(t);
-#pragma unroll 4
-    for (int k = lane; k < n; k += 64) {
-        const float d = sqd_to(x1, y1, z1, Qc + 3 * (size_t)k);
-        lane_top_push(t, -d, k, d);
+    for (int k0 = lane; k0 < n; k0 += 4 * 64) {  // n % 1024 == 0 (launch_emd)
+        float key[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) key[r] = -sqd_to(x1, y1, z1, Qc + 3 * (size_t)(k0 + 64 * r));
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lane_top_push(t, key[r], k0 + 64 * r);
     }
     bool s1, s2;
-    const float Kstar = select_cache(t, cidx, cs, s1, s2);
+    const float d1 = -t.a1, d2 = -t.a2;  // negation is exact
+    const float Kstar = select_cache(t, d1, d2, cidx, cs, s1, s2);
     T = Kstar == PCM_INF ? PCM_INF : value_of(-Kstar, 0.f);
-    wave_top2(s1 ? value_of(t.d1, 0.f) : -PCM_INF, s1 ? t.q1 : 0x7fffffff,
-              s2 ? value_of(t.d2, 0.f) : -PCM_INF, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
+    wave_top2(s1 ? value_of(d1, 0.f) : -PCM_INF, s1 ? t.q1 : 0x7fffffff,
+              s2 ? value_of(d2, 0.f) : -PCM_INF, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
 }
 
 // ---- auction full scan, exact: key = the exact bid value.  Always exact
@@ -254,48 +273,55 @@ __device__ __noinline__ void scan_exact(float x1, float y1, float z1, const floa
     const int lane = threadIdx.x & 63;
     LaneTop t;
     lane_top_init(t);
-    for (int k = lane; k < n; k += 64) {
-        const float d = sqd_to(x1, y1, z1, Qc + 3 * (size_t)k);
-        lane_top_push(t, value_of(d, sPrice[k]), k, d);
+    for (int k0 = lane; k0 < n; k0 += 4 * 64) {
+        float key[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int k = k0 + 64 * r;
+            key[r] = value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), sPrice[k]);
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lane_top_push(t, key[r], k0 + 64 * r);
     }
     bool s1, s2;
-    T = select_cache(t, cidx, cs, s1, s2);
+    T = select_cache(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cidx, cs, s1, s2);
     wave_top2(t.a1, t.q1, t.a2, t.q2, b1, kb, b2);
 }
 
 // ---- auction full scan, fast: selection on an fp32 approximation
-//   v' = (3 - sqrt_approx(d)) - price    (v_sqrt_f32, <= 1 ulp)
-// |v' - v| <= 4u(s + price + 3) with u = 2^-23 (1.5 ulp of sqrt + 3 fp32
-// roundings + v's own rounding, with a 2x margin); with the wave maxima of s
-// and price that gives one delta for every object, so
-//   T = K*' + delta
-// bounds every uncached EXACT value.  Exact values are then computed for the
-// cached entries only; if their second best does not exceed T the exact scan
-// runs instead (rare).  Returns false when the fallback is needed.
+//   v' = (3 - s') - p,  s' = v_sqrt_f32(d) (<= 1 ulp; sqrtf is 0.5 ulp)
+// With u = 2^-23, s >= 0 and p >= 0 (prices start at 0 and only rise):
+//   |v - v'| <= 1.5us + 0.5u(3+s) + 2 * 0.5u(3+s+p) <= u(3(s+p) + 4.5)
+// and s + p = 3 - v (up to rounding), so v <= (v' + 13.5u) / (1 - 3u).  For
+// every uncached object v' <= K*', hence
+//   v <= T = K*' + 4u(6 + |K*'|)      (>= 1.7x margin on both terms)
+// independently of the object.  Exact values are computed for the cached
+// entries only; if their second best does not exceed T the exact scan runs
+// instead (~4% of scans).  Returns false when that fallback is needed.
 __device__ __forceinline__ bool scan_fast(float x1, float y1, float z1, const float *Qc,
                                           const float *sPrice, int n, int32_t *__restrict__ cidx,
                                           float *__restrict__ cs, float &b1, int &kb, float &b2,
                                           float &T) {
-    const int lane = threadIdx.x & 63;
     LaneTop t;
     lane_top_init(t);
-    float smax = 0.f, pmax = 0.f;
-#pragma unroll 4
-    for (int k = lane; k < n; k += 64) {
-        const float d = sqd_to(x1, y1, z1, Qc + 3 * (size_t)k);
-        const float s = __builtin_amdgcn_sqrtf(d);
-        const float p = sPrice[k];
-        smax = fmaxf(smax, s);
-        pmax = fmaxf(pmax, p);
-        lane_top_push(t, (3.f - s) - p, k, d);
+    const int lane = threadIdx.x & 63;
+    for (int k0 = lane; k0 < n; k0 += 4 * 64) {
+        float key[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int k = k0 + 64 * r;
+            key[r] = (3.f - __builtin_amdgcn_sqrtf(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k))) - sPrice[k];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) lane_top_push(t, key[r], k0 + 64 * r);
     }
     bool s1, s2;
-    const float Kp = select_cache(t, cidx, cs, s1, s2);
-    const float delta = 4.f * 1.1920929e-7f * (wave_max(smax) + wave_max(pmax) + 3.f);
-    T = Kp + delta;  // +inf stays +inf
+    const float d1 = entry_d(x1, y1, z1, Qc, n, t.q1), d2 = entry_d(x1, y1, z1, Qc, n, t.q2);
+    const float Kp = select_cache(t, d1, d2, cidx, cs, s1, s2);
+    T = Kp + 4.f * 1.1920929e-7f * (6.f + fabsf(Kp));  // +inf stays +inf
     // exact values of this lane's cached entries
-    const float v1 = s1 ? value_of(t.d1, sPrice[t.q1]) : -PCM_INF;
-    const float v2 = s2 ? value_of(t.d2, sPrice[t.q2]) : -PCM_INF;
+    const float v1 = s1 ? value_of(d1, sPrice[t.q1]) : -PCM_INF;
+    const float v2 = s2 ? value_of(d2, sPrice[t.q2]) : -PCM_INF;
     wave_top2(v1, s1 ? t.q1 : 0x7fffffff, v2, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
     return b2 > T;
 }
@@ -328,8 +354,9 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(
 // 2. auction kernel: one workgroup per batch element, all iterations
 // ===========================================================================
 
-// kStage: the target cloud is copied into LDS (LDS-DMA at kernel start) so
-// the bid evaluations read it with LDS latency instead of L2 latency.
+// kStage: both clouds are copied into LDS (LDS-DMA at kernel start) so the
+// scans read them with LDS latency instead of L2/HBM latency (the seed kernel
+// that last touched them ran on other XCDs, whose L2s this CU does not see).
 template <bool kStage>
 __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps, int iters,
@@ -348,16 +375,21 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
     int *sU = (int *)(sInc + n);          // [n] unassigned list
     int *sMiss = sU + n;                  // [n] points needing a full scan
     float *sQ = (float *)(sMiss + n);     // [3n] target cloud copy (kStage)
+    float *sP = sQ + 3 * n;               // [3n] bidder cloud copy (kStage)
     __shared__ int sNu, sNm;
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int batch = blockIdx.x;
-    const float *P = xyz1 + (size_t)batch * n * 3;
+    const float *Pg = xyz1 + (size_t)batch * n * 3;
     const float *Qg = xyz2 + (size_t)batch * n * 3;
-    if (kStage) pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kEmdThreads / 64);
+    if (kStage) {
+        pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kEmdThreads / 64);
+        pcm_dma_to_lds(sP, Pg, 12 * n, wave, kEmdThreads / 64);
+    }
     const float *Qc = kStage ? (const float *)sQ : Qg;
+    const float *P = kStage ? (const float *)sP : Pg;
     int32_t *C = cache_idx + (size_t)batch * n * kL;
     float *CS = cache_s + (size_t)batch * n * kL;
     float *CT = cache_T + (size_t)batch * n;
@@ -592,7 +624,7 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     hipLaunchKernelGGL(emd_seed_kernel, dim3((unsigned)(pts / (kSeedThreads / 64))),
                        dim3(kSeedThreads), 0, s, xyz1, xyz2, n, eps, cache_idx, cache_s, cache_T, bid0, inc0);
     const bool stage = n <= kEmdStageMaxN;
-    const size_t lds = emd_lds_bytes(n) + (stage ? (size_t)12 * n : 0);
+    const size_t lds = emd_lds_bytes(n) + (stage ? (size_t)24 * n : 0);
     const void *kfn = stage ? (const void *)emd_auction_kernel<true> : (const void *)emd_auction_kernel<false>;
     if (lds > 64 * 1024 &&
         hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

@@ -65,7 +65,8 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
     const int wave = tid >> 6;
 
     // ---- which (direction, batch, query block) this workgroup owns (uniform)
-    int bid = blockIdx.x;
+    int bid = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int slot = bid;  // logical block id (partials are stored in this order)
     const float *Q, *T;
     float *D;
     int32_t *I;
@@ -272,7 +273,7 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
             // hand-off without fences (MI355X_MICROARCH.md, visibility table
             // row 1): write-through (sc1) partial, drain, agent atomic ticket;
             // the last arriver reads every partial with sc1 loads.
-            __hip_atomic_store(&partials[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(&partials[slot], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             sLast = (t == gridDim.x - 1);
@@ -328,7 +329,8 @@ constexpr size_t kTicketBytes = (size_t)(kShards + 1) * kShardStride * 4;  // th
 // Returns 1 in thread 0 of the overall last-arriving workgroup, else 0.  The
 // caller tests it only after its remaining work, so the atomics' round trips
 // overlap that work instead of stalling the workgroup at the next barrier.
-__device__ __forceinline__ unsigned publish_partial(float v, float *partials, unsigned *ticket,
+template <int kMode = 1>
+__device__ __forceinline__ unsigned publish_partial(float v, int slot, float *partials, unsigned *ticket,
                                                     float (*sRed)[16]) {
     // deterministic workgroup sum, then (tid 0) write-through store, drain,
     // agent atomic ticket (MI355X_MICROARCH.md visibility table, row 1)
@@ -341,7 +343,11 @@ __device__ __forceinline__ unsigned publish_partial(float v, float *partials, un
         float s = 0.f;
         const int nw = blockDim.x >> 6;
         for (int w = 0; w < nw; ++w) s += sRed[0][w];
-        __hip_atomic_store(&partials[blockIdx.x], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if constexpr (kMode == 2) {  // reduced by chamfer_loss_finalize_kernel after the kernel boundary
+            partials[slot] = s;
+            return 0;
+        }
+        __hip_atomic_store(&partials[slot], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned nb = gridDim.x;
         const unsigned sh = blockIdx.x % kShards;
@@ -383,7 +389,7 @@ __device__ __forceinline__ void finish_loss(int nb1, int b, int n, int m, const 
     }
 }
 
-template <int W, int QPT, int C, bool kLoss>
+template <int W, int QPT, int C, int kLoss>
 __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1,
@@ -411,7 +417,8 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-    int bid = blockIdx.x;
+    int bid = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int slot = bid;  // logical block id (partials are stored in this order)
     const float *Q, *T;
     float *D;
     int32_t *I;
@@ -563,7 +570,7 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
             sFc[tid] = fc;
             if (qbase + tid < nq) fbv = fb;
         }
-        if constexpr (kLoss) tk = publish_partial(fbv, partials, ticket, sRed);  // has a barrier
+        if constexpr (kLoss != 0) tk = publish_partial<kLoss>(fbv, slot, partials, ticket, sRed);  // has a barrier
         else __syncthreads();
         // ---- rescan the winning chunk: item -> (query s, part)
 #pragma unroll
@@ -621,12 +628,39 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
             D[qi] = d;
             I[qi] = idx;
         }
-        if constexpr (kLoss) tk = publish_partial(myd, partials, ticket, sRed);
+        if constexpr (kLoss != 0) tk = publish_partial<kLoss>(myd, slot, partials, ticket, sRed);
     }
-    if constexpr (kLoss) {
+    if constexpr (kLoss == 1) {
         if (tid == 0) sLast[0] = tk;
         __syncthreads();
         if (sLast[0]) finish_loss(b * nblk1, b, n, m, partials, ticket, mean_out, sRed);
+    }
+}
+
+// Loss mode 2: the forward kernel only stores its workgroup partials; this
+// one-workgroup kernel, next on the stream, sums them in the same fixed order
+// as finish_loss (no atomics, no write-through: the kernel boundary is the
+// hand-off).
+__global__ __launch_bounds__(512) void chamfer_loss_finalize_kernel(const float *__restrict__ partials,
+                                                                    int nb1, int nbt, int b, int n, int m,
+                                                                    float *__restrict__ mean_out) {
+    __shared__ float sRed[2][16];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    float s1 = 0.f, s2 = 0.f;
+    for (int i = threadIdx.x; i < nbt; i += blockDim.x) {
+        const float v = partials[i];
+        if (i < nb1) s1 += v; else s2 += v;
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) { sRed[0][wave] = s1; sRed[1][wave] = s2; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float a1 = 0.f, a2 = 0.f;
+        const int nw = blockDim.x >> 6;
+        for (int w = 0; w < nw; ++w) { a1 += sRed[0][w]; a2 += sRed[1][w]; }
+        mean_out[0] = a1 / ((float)b * (float)n);
+        mean_out[1] = a2 / ((float)b * (float)m);
     }
 }
 
@@ -667,7 +701,7 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
     __shared__ int sWave[kBwdT / 64];
 
     const int tid = threadIdx.x;
-    int bid = blockIdx.x;
+    int bid = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
     // cloud 1 (direct term first) or cloud 2 (direct term last): reference
     // kernel order chamfer3D.cu:184-185.
     const float *self, *other, *gds, *gdo;
@@ -965,7 +999,7 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
 
     const int tid = threadIdx.x;
     const int wave = tid >> 6;
-    int bid = blockIdx.x;
+    int bid = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
     const float *self, *other, *gds, *gdo;
     const int32_t *ids, *ido;
     float *grad;
@@ -1085,16 +1119,16 @@ inline bool bad_dims(int b, int n, int m) { return b < 0 || n < 0 || m < 0; }
 typedef void (*fwd_kernel_t)(const float *, const float *, int, int, int, float *, float *,
                              int32_t *, int32_t *, int, int, float *, unsigned *, float *);
 struct FwdVariant {
-    fwd_kernel_t plain, loss;
+    fwd_kernel_t plain, loss, loss2;  // loss: in-kernel ticket; loss2: partials + finalize kernel
     int waves, qpt;
     bool sgpr;  // SGPR-stream form (else LDS-tile form)
 };
 #define PCM_FWD_LDS(W, Q)                                                              \
     FwdVariant{chamfer_fwd_kernel<W, Q, kChunk, kTile, false>,                         \
-               chamfer_fwd_kernel<W, Q, kChunk, kTile, true>, W, Q, false}
+               chamfer_fwd_kernel<W, Q, kChunk, kTile, true>, nullptr, W, Q, false}
 #define PCM_FWD_SGPR(W, Q, C)                                                          \
-    FwdVariant{chamfer_fwd_sgpr_kernel<W, Q, C, false>,                                \
-               chamfer_fwd_sgpr_kernel<W, Q, C, true>, W, Q, false}
+    FwdVariant{chamfer_fwd_sgpr_kernel<W, Q, C, 0>, chamfer_fwd_sgpr_kernel<W, Q, C, 1>, \
+               chamfer_fwd_sgpr_kernel<W, Q, C, 2>, W, Q, true}
 const FwdVariant kFwdVariants[] = {
     PCM_FWD_LDS(8, 2),       // 0: LDS-tile form
     PCM_FWD_LDS(8, 4),       // 1
@@ -1112,6 +1146,7 @@ constexpr int kNumFwdVariants = sizeof(kFwdVariants) / sizeof(kFwdVariants[0]);
 // SGPR-stream form wins everywhere; 2 queries per lane and 16-candidate chunks
 // for ShapeNet-size clouds (B=32, N=M=1024: 12.7 us vs 13.5 us LDS-tile), 4
 // queries per lane once a batch has >= 4M pairs (B=8, N=M=16384: 453 us).
+constexpr int kDefaultLossMode = 2;  // tools/tune_chamfer.py: 15.9 vs 16.3 us (B=32, N=M=1024)
 inline int default_fwd_variant(int n, int m) {
     return (long long)n * m >= (1LL << 22) ? 3 : 8;
 }
@@ -1125,9 +1160,11 @@ int fwd_grid(const FwdVariant &v, int b, int n, int m, int &nblk1, int &nblk2, l
     return blocks > 0x7fffffffLL ? PCM_ERR_UNSUPPORTED : PCM_OK;
 }
 
+// loss_mode (mean_out != nullptr): 1 = in-kernel arrival ticket + last-workgroup
+// reduction; 2 = workgroup partials + chamfer_loss_finalize_kernel.
 int launch_fwd(int variant, const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
                float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out, void *ws, size_t ws_bytes,
-               void *stream) {
+               void *stream, int loss_mode = kDefaultLossMode) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
     if (variant < 0 || variant >= kNumFwdVariants) return PCM_ERR_INVALID_ARG;
     const FwdVariant &v = kFwdVariants[variant];
@@ -1148,9 +1185,14 @@ int launch_fwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
         ticket = (unsigned *)ws;
         partials = (float *)((char *)ws + kTicketBytes);
     }
-    hipLaunchKernelGGL(loss ? v.loss : v.plain, dim3((unsigned)blocks), dim3(64 * v.waves), 0,
-                       (hipStream_t)stream, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nblk1,
-                       nblk2, partials, ticket, mean_out);
+    if (loss && loss_mode == 2 && !v.loss2) loss_mode = 1;
+    if (loss && (loss_mode < 1 || loss_mode > 2)) return PCM_ERR_INVALID_ARG;
+    fwd_kernel_t k = !loss ? v.plain : (loss_mode == 2 ? v.loss2 : v.loss);
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * v.waves), 0, (hipStream_t)stream, xyz1, xyz2,
+                       b, n, m, dist1, dist2, idx1, idx2, nblk1, nblk2, partials, ticket, mean_out);
+    if (loss && loss_mode == 2)
+        hipLaunchKernelGGL(chamfer_loss_finalize_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream,
+                           partials, b * nblk1, (int)blocks, b, n, m, mean_out);
     return pcm_launch_status();
 }
 
@@ -1189,6 +1231,16 @@ extern "C" int pcm_tune_chamfer_forward(int variant, const float *xyz1, const fl
                                         void *stream) {
     return launch_fwd(variant, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nullptr, nullptr, 0,
                       stream);
+}
+
+extern "C" int pcm_tune_chamfer_forward_loss(int variant, int loss_mode, const float *xyz1,
+                                             const float *xyz2, int b, int n, int m, float *dist1,
+                                             float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out,
+                                             void *workspace, size_t workspace_bytes, void *stream) {
+    if (!mean_out) return PCM_ERR_INVALID_ARG;
+    if (variant < 0) variant = default_fwd_variant(n, m);
+    return launch_fwd(variant, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, mean_out, workspace,
+                      workspace_bytes, stream, loss_mode);
 }
 
 extern "C" int pcm_tune_num_chamfer_variants(void) { return kNumFwdVariants; }

@@ -333,7 +333,7 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps,
     int32_t *__restrict__ cache_idx, float *__restrict__ cache_s, float *__restrict__ cache_T,
     int32_t *__restrict__ bid0, float *__restrict__ inc0) {
-    const int pt = blockIdx.x * (kSeedThreads / 64) + (threadIdx.x >> 6);  // global point id
+    const int pt = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x) * (kSeedThreads / 64) + (threadIdx.x >> 6);
     const int batch = pt / n;
     const int j = pt - batch * n;
     const float *P = xyz1 + (size_t)batch * n * 3;

@@ -79,6 +79,19 @@ __device__ __forceinline__ void pcm_dma_to_lds(void *lds_dst, const void *src, i
     }
 }
 
+// XCD-aware workgroup numbering.  The dispatcher places workgroup i on XCD
+// i % 8 (MI355X: 8 XCDs, each with its own 4 MB L2).  Giving every XCD a
+// contiguous range of logical ids keeps the workgroups of one batch element --
+// which all read the same clouds -- on one L2 instead of fetching those clouds
+// into all eight.  A bijection for any grid size; placement is only a speed
+// assumption (nothing depends on it for correctness).
+__device__ __forceinline__ int pcm_xcd_remap(int i, int g) {
+    constexpr int kXcd = 8;
+    const int per = g / kXcd, rem = g % kXcd;
+    const int x = i % kXcd, s = i / kXcd;
+    return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + s;
+}
+
 static inline int pcm_launch_status() {
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? PCM_OK : PCM_ERR_LAUNCH;

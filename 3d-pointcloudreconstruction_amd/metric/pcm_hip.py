@@ -62,6 +62,8 @@ def load_library():
     L.pcm_tune_chamfer_forward.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
     L.pcm_tune_chamfer_backward.restype = ci
     L.pcm_tune_chamfer_backward.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
+    L.pcm_tune_chamfer_forward_loss.restype = ci
+    L.pcm_tune_chamfer_forward_loss.argtypes = [ci, ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, cs, vp]
     L.pcm_tune_emd_forward_stats.restype = ci
     L.pcm_tune_emd_forward_stats.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, cs, vp, vp]
     L.pcm_emd_workspace_bytes.restype = cs
@@ -165,6 +167,22 @@ def tune_chamfer_backward(variant, xyz1, xyz2, graddist1, graddist2, idx1, idx2,
             int(variant), _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(graddist1), _ptr(graddist2),
             _ptr(idx1), _ptr(idx2), _ptr(gradxyz1), _ptr(gradxyz2), _stream(dev)),
             "pcm_tune_chamfer_backward")
+
+
+def tune_chamfer_forward_loss(variant, loss_mode, xyz1, xyz2, dist1, dist2, idx1, idx2, mean_out,
+                              workspace=None) -> None:
+    """Internal: fused-loss forward with an explicit variant (-1 = default) and
+    loss mode (1 = in-kernel ticket, 2 = partials + finalize kernel)."""
+    dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2, mean_out)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    if workspace is None:
+        workspace = chamfer_workspace(dev, b, n, m)
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_tune_chamfer_forward_loss(
+            int(variant), int(loss_mode), _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2),
+            _ptr(idx1), _ptr(idx2), _ptr(mean_out), _ptr(workspace), workspace.numel(), _stream(dev)),
+            "pcm_tune_chamfer_forward_loss")
 
 
 def tune_num_chamfer_variants() -> int:

@@ -9,15 +9,19 @@ directions, B=32, N=M=1024 per GPU -- BASELINE config 2), the loss partial sums
 mean(dist1)+mean(dist2) (loss/loss.py:36), the cross-rank RCCL all-reduce of
 that scalar when N>1, and the Chamfer3D backward with graddist = 1/(B*N) (the
 gradient torch's mean feeds it).  Inputs are resident in HBM before timing.
-By default one step is captured in a hipGraph and replayed (HIP graphs instead
-of a tracing compiler); --eager launches through the Python API each step.
+By default GRAPH_STEPS consecutive steps are captured in one hipGraph and
+replayed (HIP graphs instead of a tracing compiler: a step is two ~10 us
+kernels, so per-step host launches would leave the GPU idle); --eager launches
+through the Python API each step.
 
 value = point pairs evaluated per second over all ranks (2*B*N*M per rank per
 step / max-over-ranks wall time).  EMD (BASELINE config 3: B=16, N=1024,
 50 iterations, eps=0.005) is reported alongside as iterations/s.
 
 Multi-GPU: one process per GPU (torchrun), batches sharded (weak scaling: each
-rank owns its own B=32 clouds), one 8-byte all-reduce per step over RCCL.
+rank owns its own B=32 clouds).  Every step's loss pair is all-reduced over
+RCCL; the collectives are bucketed per graph of GRAPH_STEPS steps (one
+GRAPH_STEPS x 8-byte all-reduce after each replay, stream-ordered behind it).
 """
 from __future__ import annotations
 
@@ -37,6 +41,13 @@ import pcm_hip  # noqa: E402
 
 B, N, M = 32, 1024, 1024           # BASELINE config 2 (per GPU)
 EMD_B, EMD_N, EMD_EPS, EMD_ITERS = 16, 1024, 0.005, 50   # BASELINE config 3
+GRAPH_STEPS = 10                   # steps captured per hipGraph replay
+# the forward kernel instance the step launches at this size (csrc/chamfer.hip
+# default_fwd_variant) and the committed rocprofv3 counter summary it is looked
+# up in for roofline.traffic (tools/pmc_passes.sh + tools/pmc_summarize.py)
+FWD_KERNEL = "chamfer_fwd_sgpr_kernel<8, 2, 16, true>"
+BWD_KERNEL = "chamfer_bwd_staged_kernel"
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "pmc_summary.json")
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0
@@ -57,13 +68,19 @@ def parse():
     p.add_argument("--eager", action="store_true", help="no hipGraph capture")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-emd", action="store_true", help="skip the EMD leg")
+    p.add_argument("--dist-backend", default="nccl",
+                   help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
+                        "several ranks on one GPU)")
     return p.parse_args()
 
 
 class ChamferStep:
-    """Buffers + one hot-path step, all on the current stream."""
+    """Buffers + one hot-path step, all on the current stream.  The loss means
+    of consecutive steps go to consecutive rows of `loss` ([slots, 2]), so the
+    cross-rank all-reduce can take the losses of a whole graph of steps at once
+    (one bucketed collective instead of one 8-byte collective per step)."""
 
-    def __init__(self, dev, world, seed):
+    def __init__(self, dev, world, seed, slots):
         g = torch.Generator(device="cpu").manual_seed(seed)
         self.xyz1 = torch.rand(B, N, 3, generator=g).to(dev)
         self.xyz2 = torch.rand(B, M, 3, generator=g).to(dev)
@@ -76,26 +93,29 @@ class ChamferStep:
         self.g2 = torch.full((B, M), 1.0 / (world * B * M), device=dev)
         self.gx1 = torch.empty(B, N, 3, device=dev)
         self.gx2 = torch.empty(B, M, 3, device=dev)
-        self.loss = torch.zeros(2, device=dev)
+        self.loss = torch.zeros(slots, 2, device=dev)
         self.ws = pcm_hip.chamfer_workspace(dev, B, N, M)
         self.world = world
 
-    def __call__(self):
+    def __call__(self, slot=0):
         # forward + deterministic in-kernel mean(dist1), mean(dist2)
         pcm_hip.chamfer_forward_loss(self.xyz1, self.xyz2, self.d1, self.d2, self.i1, self.i2,
-                                     self.loss, self.ws)
-        if self.world > 1:
-            dist.all_reduce(self.loss)  # sum of per-rank means; /world = global mean
+                                     self.loss[slot], self.ws)
         pcm_hip.chamfer_backward(self.xyz1, self.xyz2, self.g1, self.g2, self.i1, self.i2,
                                  self.gx1, self.gx2)
 
+    def reduce_losses(self, rows):
+        """sum of per-rank means over RCCL (/world = global mean), stream-ordered"""
+        if self.world > 1:
+            dist.all_reduce(self.loss[:rows])
 
-def time_region(fn, steps, dev, world):
+
+def time_region(fn, calls, dev, world):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(steps):
+    for _ in range(calls):
         fn()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -108,16 +128,30 @@ def time_region(fn, steps, dev, world):
     return t
 
 
-def kernel_avg_us(launch, reps, dev):
-    """Average duration of one launch measured with HIP events on the stream
-    the kernel runs on (torch's current stream)."""
+def kernel_avg_us(launch, reps, dev, graph=True):
+    """Average device time of one launch: `reps` back-to-back launches captured
+    in a hipGraph, replayed between two HIP events recorded on the stream the
+    kernels run on (so the ~10 us host cost of a ctypes launch is not timed;
+    the inter-kernel gap inside the graph is).  graph=False: eager launches."""
     s = torch.cuda.current_stream(dev)
     for _ in range(5):
         launch()
+    run = lambda: [launch() for _ in range(reps)]  # noqa: E731
+    if graph:
+        cs = torch.cuda.Stream(dev)
+        cs.wait_stream(s)
+        with torch.cuda.stream(cs):
+            launch()
+        s.wait_stream(cs)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(reps):
+                launch()
+        run = g.replay
+        run()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(s)
-    for _ in range(reps):
-        launch()
+    run()
     e1.record(s)
     e1.synchronize()
     return e0.elapsed_time(e1) * 1000.0 / reps
@@ -135,9 +169,20 @@ def emd_leg(dev, reps=10):
     def run():
         pcm_hip.emd_forward(x1, x2, EMD_EPS, EMD_ITERS, d, a, None, ws)
 
-    us = kernel_avg_us(run, reps, dev)
+    us = kernel_avg_us(run, reps, dev, graph=False)  # ~400 us launches: host cost hidden
     return {"config": f"B={EMD_B} N=M={EMD_N} iters={EMD_ITERS} eps={EMD_EPS}",
             "ms_per_forward": us / 1000.0, "iters_per_s": EMD_ITERS / (us * 1e-6)}
+
+
+def pmc_bytes(kernel):
+    """HBM-side bytes per launch of `kernel` from the committed rocprofv3 PMC
+    summary (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), or None."""
+    try:
+        with open(PMC_SUMMARY) as fh:
+            ent = json.load(fh)["counters"][kernel]
+        return ent["hbm_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def cpu_baseline(target_s=10.0):
@@ -173,43 +218,62 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    # one GPU per rank; a rehearsal with more ranks than GPUs (gloo) shares them
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
-    step = ChamferStep(dev, world, seed=1234 + rank)
-    for _ in range(args.warmup):
-        step()
+    per = 1 if args.eager else max(1, min(GRAPH_STEPS, args.steps))
+    step = ChamferStep(dev, world, seed=1234 + rank, slots=per)
+
+    def run_eager(k):
+        for _ in range(k):
+            step(0)
+            step.reduce_losses(1)
+
+    run_eager(args.warmup)
     torch.cuda.synchronize(dev)
-
-    mode = "eager"
-    fn = step
-    if not args.eager and world == 1:
-        # capture one step (kernels + reductions) and replay it
+    run_steps, mode = run_eager, "eager"
+    if not args.eager:
+        # The step is launch-bound (two ~10 us kernels), so `per` consecutive
+        # steps are captured into one hipGraph (kernels only) and replayed,
+        # followed by one all-reduce of those steps' losses when N>1; a
+        # one-step graph covers a remainder, so exactly K steps run.
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
-            for _ in range(3):
-                step()
+            for i in range(3):
+                step(i % per)
         torch.cuda.current_stream(dev).wait_stream(s)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step()
-        fn = graph.replay
-        for _ in range(args.warmup):
-            fn()
-        mode = "hipgraph"
+        g_many, g_one = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_many):
+            for i in range(per):
+                step(i)
+        with torch.cuda.graph(g_one):
+            step(0)
 
-    t = time_region(fn, args.steps, dev, world)
+        def run_steps(k):
+            for _ in range(k // per):
+                g_many.replay()
+                step.reduce_losses(per)
+            for _ in range(k % per):
+                g_one.replay()
+                step.reduce_losses(1)
+        run_steps(args.warmup)
+        mode = f"hipgraph ({per} steps per graph" + (", one loss all-reduce per graph)" if world > 1 else ")")
+
+    t = time_region(lambda: run_steps(args.steps), 1, dev, world)
     pairs_per_step = 2 * B * N * M
     value = world * args.steps * pairs_per_step / t
     ms = t * 1000.0 / args.steps
 
-    # dominant kernel: the Chamfer forward launch, timed on its stream
-    fwd_us = kernel_avg_us(lambda: pcm_hip.chamfer_forward(step.xyz1, step.xyz2, step.d1, step.d2,
-                                                           step.i1, step.i2), 200, dev)
+    # dominant kernel: the step's Chamfer forward (fused-loss) launch, timed on its stream
+    fwd_us = kernel_avg_us(lambda: pcm_hip.chamfer_forward_loss(
+        step.xyz1, step.xyz2, step.d1, step.d2, step.i1, step.i2, step.loss[0], step.ws), 200, dev)
     bwd_us = kernel_avg_us(lambda: pcm_hip.chamfer_backward(step.xyz1, step.xyz2, step.g1, step.g2,
                                                             step.i1, step.i2, step.gx1, step.gx2),
                            200, dev)
@@ -231,17 +295,21 @@ def main():
                    "batch_per_gpu": B, "n_points": N, "m_points": M,
                    "global_batch": world * B, "parallelism": f"dp{world} (batch-sharded)",
                    "launch": mode},
-        "roofline": {"bound": "valu", "kernel": "chamfer_fwd_kernel",
+        "roofline": {"bound": "valu", "kernel": FWD_KERNEL,
                      "achieved": fwd_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": fwd_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": None,
+                     "frac": fwd_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": pmc_bytes(FWD_KERNEL),
+                     "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE*2+WRITE_SIZE, "
+                                     "profiles/r01/pmc_summary.json)",
                      "kernel_us": fwd_us,
                      "note": "FLOPs = 8 per point pair (algorithmic); VALU-bound, see DESIGN.md"},
-        "roofline_hbm": {"bound": "hbm", "kernel": "chamfer_fwd_kernel",
+        "roofline_hbm": {"bound": "hbm", "kernel": FWD_KERNEL,
                          "achieved": FWD_BYTES / (fwd_us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s",
                          "frac": FWD_BYTES / (fwd_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes": FWD_BYTES, "traffic": pmc_bytes(FWD_KERNEL),
                          "bwd_kernel_us": bwd_us,
-                         "bwd_achieved_gbs": BWD_BYTES / (bwd_us * 1e-6) / 1e9},
+                         "bwd_achieved_gbs": BWD_BYTES / (bwd_us * 1e-6) / 1e9,
+                         "bwd_algorithmic_bytes": BWD_BYTES, "bwd_traffic": pmc_bytes(BWD_KERNEL)},
     }
     if not args.no_emd:
         out["emd"] = emd_leg(dev)

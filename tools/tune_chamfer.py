@@ -90,6 +90,13 @@ def main():
         print(f"  bwd staged {out[0]:9.2f} us  global {out[1]:9.2f} us  per-batch-lds {out[2]:9.2f} us  "
               f"fused-loss fwd (default variant) {fl:9.2f} us")
         print(f"  mean=({mo[0].item():.7g},{mo[1].item():.7g}) torch=({d1.mean().item():.7g},{d2.mean().item():.7g})")
+        for mode in (1, 2):
+            mo2 = torch.empty(2, device=dev)
+            gm = graph_of(lambda mode=mode: pcm_hip.tune_chamfer_forward_loss(-1, mode, x1, x2, d1, d2, i1, i2,
+                                                                            mo2, ws), reps)
+            tm = statistics.median([time_graph_us(gm, reps) for _ in range(rounds)])
+            torch.cuda.synchronize()
+            print(f"  fused-loss mode {mode}: {tm:9.2f} us  mean=({mo2[0].item():.7g},{mo2[1].item():.7g})")
         # eager per-call cost through the Python API, for reference
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

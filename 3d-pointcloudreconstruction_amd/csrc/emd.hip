@@ -4,25 +4,30 @@
 // (metric/emd/emd_cuda.cu:256-269: clear, calc_unass_cnt, calc_unass_cnt_sum,
 // calc_unass_idx, Bid, GetMax, Assign) by two launches for any `iters`:
 //
-//  1. emd_seed_kernel (all CUs): iteration 0's bids.  With every price 0 the
-//     bid value v = (float)((3.0 - (double)sqrtf(d)) - 0.0) is a monotone
-//     non-increasing function of the squared distance d, so each point's
-//     nearest candidates by d (16 lanes per point, branch-free top-3 per lane,
-//     then a shuffle extraction of the L = 16 nearest) are exactly the top of
-//     its value list.  The exact bid (best, better, argbest) is read off the
-//     cached entries whenever the cache PROVES it: every uncached object has
-//     d >= D*, hence v <= T = v(D*), so if the cached second-best value > T
-//     nothing outside the cache can enter the top two.  Otherwise the point
-//     is flagged for a full scan.  The cache (16 object ids + T) is kept.
+//  1. emd_seed_kernel (all CUs, one wave per point): iteration 0's bids.  With
+//     every price 0 the bid value v = (float)((3.0 - (double)sqrtf(d)) - 0.0)
+//     is a monotone non-increasing function of the squared distance d, so the
+//     nearest candidates by d are the top of the value list.  Each lane keeps
+//     its top-3 keys (v_med3 insertion); the cache is every lane top-2 entry
+//     above K* = max over lanes of the 3rd keys (ballot compaction, <= kL = 32
+//     entries), and every uncached object has v <= T = v(-K*).  If the cached
+//     second-best value exceeds T nothing outside the cache can enter the top
+//     two, so the bid is exact; otherwise the point is flagged for a full scan.
+//     A cache entry is (object id, s = sqrtf(d)): s does not depend on prices.
 //
 //  2. emd_auction_kernel (one persistent workgroup per batch element): every
 //     auction iteration in-kernel with the whole auction state (assignment,
-//     owner, price, max increment, claim) in LDS and workgroup barriers only.
-//     An unassigned point re-bids from its cache (16 lanes evaluate the 16
-//     cached objects at CURRENT prices): prices only rise, so uncached values
-//     are still <= T and the same proof applies.  Points whose cache cannot
-//     prove the top two are re-scanned in full by one wave each, which also
-//     rebuilds their cache from the value-ordered candidates.
+//     owner, price, max increment, claim) and both clouds in LDS, and
+//     workgroup barriers only.  An unassigned point re-bids from its cache at
+//     CURRENT prices (two double subtractions per entry, one 16-lane DPP row
+//     per point): prices only rise, so uncached values are still <= T and the
+//     same proof applies.  Points whose cache cannot prove the top two are
+//     re-scanned by one wave each: selection on an fp32 approximation of the
+//     values with a proven error bound, exact evaluation of the chosen
+//     entries, cache rebuilt (exact scan as fallback).  (Measured and
+//     rejected: a lock-free LDS queue letting waves start full scans before
+//     every cache bid is placed, 408 -> 421 us; fewer lanes per point for
+//     large bidder sets, 421 -> 436 us.)
 //
 // The cache only skips evaluations that provably cannot change the bid, so
 // the results are identical to scanning every object every iteration (the

@@ -45,6 +45,7 @@
 namespace {
 
 constexpr int kL = 32;             // cache slots per point (unused slots hold -1)
+constexpr int kSelectSteps = 8;    // bisection steps when > kL entries clear K3
 constexpr int kSeedThreads = 256;  // one wave per point, 4 points per workgroup
 constexpr int kEmdThreads = 1024;  // auction workgroup (16 waves)
 constexpr int kEmdMaxN = 4096;     // LDS-resident auction state: 9 x 4 B x n
@@ -142,9 +143,13 @@ __device__ __forceinline__ float wave_max(float v) {
 // 3rd-best key.  Cache = every lane-top-2 entry strictly above K3 = max over
 // lanes of the 3rd-best keys (~30 on random clouds): every other object lies
 // at or below K3 -- it is either outside its lane's top-2 (<= that lane's 3rd
-// <= K3) or a top-2 entry not above K3.  If more than kL qualify, fall back
-// to the lane-top-1 entries strictly above K2 = max over lanes of the 2nd
-// keys (same argument).  Two ballots, popcounts, mbcnt.
+// <= K3) or a top-2 entry not above K3.  If more than kL qualify (common:
+// ~30 is the typical count), the threshold is raised by bisection between K3
+// and the largest key until at most kL lane-top-2 entries lie above it; the
+// bound then stays exact for every uncached key.  (The earlier fallback -- the
+// lane-top-1 entries above K2 = max of the 2nd keys -- loses the global
+// second best whenever it shares a lane with the best, which sent ~4% of the
+// auction's full scans to the exact re-scan.)  Ballots, popcounts, mbcnt.
 // ===========================================================================
 struct LaneTop {
     float a1, a2, a3;  // the lane's three largest keys (multiset order)
@@ -197,19 +202,22 @@ __device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float 
     s2 = t.a2 > Kstar;
     unsigned long long m1 = __ballot(s1), m2 = __ballot(s2);
     int cnt = __popcll(m1) + __popcll(m2);
-    if (cnt > kL) {  // wave-uniform
-        Kstar = wave_max(t.a2);
+    if (cnt > kL) {  // wave-uniform: raise the threshold by bisection
+        // invariant: count(> lo) > kL >= count(> hi); every uncached key is
+        // <= max(K3, hi) = hi, so hi is a valid bound at every step
+        float lo = Kstar, hi = wave_max(t.a1);
+#pragma unroll 1
+        for (int step = 0; step < kSelectSteps; ++step) {
+            const float mid = lo + 0.5f * (hi - lo);
+            const int c = __popcll(__ballot(t.a1 > mid)) + __popcll(__ballot(t.a2 > mid));
+            if (c > kL) lo = mid; else hi = mid;
+        }
+        Kstar = hi;
         s1 = t.a1 > Kstar;
-        s2 = false;
+        s2 = t.a2 > Kstar;
         m1 = __ballot(s1);
-        m2 = 0ull;
-        cnt = __popcll(m1);
-    }
-    if (cnt > kL) {
-        s1 = s2 = false;
-        m1 = m2 = 0ull;
-        cnt = 0;
-        Kstar = PCM_INF;
+        m2 = __ballot(s2);
+        cnt = __popcll(m1) + __popcll(m2);
     }
     const unsigned long long below = (1ull << lane) - 1ull;
     if (lane < kL && lane >= cnt) cidx[lane] = -1;  // unused slots

@@ -458,28 +458,37 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
                 }
             }
         } else {
-            // one 16-lane DPP row per point, two cached (id, s) entries per lane
-            static_assert(kL == 32, "one cache = one 16-lane DPP row x 2 entries");
+            // one 16-lane DPP row per point, kL/16 cached (id, s) entries per lane
+            static_assert(kL % 16 == 0, "one cache = one 16-lane DPP row x kL/16 entries");
+            constexpr int E = kL / 16;
             const int g = tid >> 4, gl = tid & 15;
             for (int u0 = 0; u0 < nu; u0 += kEmdThreads / 16) {
                 const int u = u0 + g;
                 const bool act = u < nu;
                 const int j = act ? sU[u] : 0;
-                const int ka = C[(size_t)j * kL + gl];  // -1: unused slot
-                const int kc = C[(size_t)j * kL + gl + 16];
-                const float sa = CS[(size_t)j * kL + gl];
-                const float sc = CS[(size_t)j * kL + gl + 16];
-                float b1 = ka >= 0 ? value_from_s(sa, sPrice[ka]) : -PCM_INF;
-                int kb = ka >= 0 ? ka : 0x7fffffff;
-                float b2 = kc >= 0 ? value_from_s(sc, sPrice[kc]) : -PCM_INF;
-                int k2 = kc >= 0 ? kc : 0x7fffffff;
-                if (vk_better(b2, k2, b1, kb)) {
-                    const float tv = b1; b1 = b2; b2 = tv;
-                    kb = k2;
+                const float tj = CT[j];
+                int ke[E];
+                float se[E];
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    ke[e] = C[(size_t)j * kL + gl + 16 * e];  // -1: unused slot
+                    se[e] = CS[(size_t)j * kL + gl + 16 * e];
+                }
+                float b1 = -PCM_INF, b2 = -PCM_INF;
+                int kb = 0x7fffffff;
+#pragma unroll
+                for (int e = 0; e < E; ++e) {
+                    const int k = ke[e];
+                    const float v = k >= 0 ? value_from_s(se[e], sPrice[k]) : -PCM_INF;
+                    const int kk = k >= 0 ? k : 0x7fffffff;
+                    const bool better = vk_better(v, kk, b1, kb);
+                    b2 = better ? b1 : fmaxf(b2, v);
+                    b1 = better ? v : b1;
+                    kb = better ? kk : kb;
                 }
                 row_top2(b1, kb, b2);  // row result in lane 15
                 if (act && gl == 15) {
-                    if (b2 > CT[j]) {
+                    if (b2 > tj) {
                         const float inc = b1 - b2 + eps;
                         sBid[j] = kb;
                         sInc[j] = inc;

@@ -19,9 +19,9 @@
 //     auction iteration in-kernel with the whole auction state (assignment,
 //     owner, price, max increment, claim) and both clouds in LDS, and
 //     workgroup barriers only.  An unassigned point re-bids from its cache at
-//     CURRENT prices (two double subtractions per entry, one 16-lane DPP row
-//     per point): prices only rise, so uncached values are still <= T and the
-//     same proof applies.  Points whose cache cannot prove the top two are
+//     CURRENT prices (two double subtractions per entry; 16, 8 or 4 lanes per
+//     point by bidder count, reduced with DPP row shifts): prices only rise,
+//     so uncached values are still <= T and the same proof applies.  Points whose cache cannot prove the top two are
 //     re-scanned by one wave each: selection on an fp32 approximation of the
 //     values with a proven error bound, exact evaluation of the chosen
 //     entries, cache rebuilt (exact scan as fallback).  (Measured and
@@ -46,6 +46,7 @@ namespace {
 
 constexpr int kL = 32;             // cache slots per point (unused slots hold -1)
 constexpr int kSelectSteps = 8;    // bisection steps when > kL entries clear K3
+typedef int16_t cid_t;             // cached object id (n <= kEmdMaxN = 4096), -1 = unused
 constexpr int kSeedThreads = 256;  // one wave per point, 4 points per workgroup
 constexpr int kEmdThreads = 1024;  // auction workgroup (16 waves)
 constexpr int kEmdMaxN = 4096;     // LDS-resident auction state: 9 x 4 B x n
@@ -76,15 +77,53 @@ __device__ __forceinline__ bool vk_better(float va, int ka, float vb, int kb) {
     return va > vb || (va == vb && ka < kb);
 }
 
-// top-2 triple merge (b1, k1, b2): b2 = second largest value of the union
-__device__ __forceinline__ void top2_merge(float &b1, int &k1, float &b2, float ob1, int ok1, float ob2) {
-    if (vk_better(ob1, ok1, b1, k1)) {
-        b2 = fmaxf(b1, ob2);
-        b1 = ob1;
-        k1 = ok1;
-    } else {
-        b2 = fmaxf(b2, ob1);
-    }
+// Top-2 triples (b1, k1, b2): best value, its (lowest) id, second largest
+// value of the multiset.  Written as one asm block each: as C++ ternaries
+// hipcc emits exec-mask branches plus NaN-canonicalising v_max pairs here.
+// "Better" = larger value, then lower id (vk_better).  The trailing s_nop
+// covers the VALU-write -> DPP-read hazard of the next reduction step, and
+// the one before v_cndmask the VALU/SALU-SGPR-write -> lane-mask read.
+//
+// merge of two triples: b2 = max(min(b1, o1), max(b2, o2)), b1 = max(b1, o1)
+__device__ __forceinline__ void top2_merge(float &b1, int &k1, float &b2, float o1, int ok1, float o2) {
+    unsigned long long g, e, l;
+    float t, u, n1, n2;
+    asm("v_cmp_gt_f32_e64 %[g], %[o1], %[b1]\n\t"
+        "v_cmp_eq_f32_e64 %[e], %[o1], %[b1]\n\t"
+        "v_cmp_lt_i32_e64 %[l], %[ok1], %[k1]\n\t"
+        "v_min_f32 %[t], %[b1], %[o1]\n\t"
+        "v_max_f32 %[u], %[b2], %[o2]\n\t"
+        "v_max_f32 %[n1], %[b1], %[o1]\n\t"
+        "v_max_f32 %[n2], %[t], %[u]\n\t"
+        "s_and_b64 %[e], %[e], %[l]\n\t"
+        "s_or_b64 %[g], %[g], %[e]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[k1], %[k1], %[ok1], %[g]\n\t"
+        "s_nop 1"
+        : [k1] "+v"(k1), [t] "=&v"(t), [u] "=&v"(u), [n1] "=&v"(n1), [n2] "=&v"(n2), [g] "=&s"(g),
+          [e] "=&s"(e), [l] "=&s"(l)
+        : [o1] "v"(o1), [ok1] "v"(ok1), [o2] "v"(o2), [b1] "v"(b1), [b2] "v"(b2));
+    b1 = n1;
+    b2 = n2;
+}
+// push of one entry (v, k): b2 = med3(b1, b2, v), b1 = max(b1, v)
+__device__ __forceinline__ void top2_push(float &b1, int &k1, float &b2, float v, int k) {
+    unsigned long long g, e, l;
+    float n1, n2;
+    asm("v_cmp_gt_f32_e64 %[g], %[v], %[b1]\n\t"
+        "v_cmp_eq_f32_e64 %[e], %[v], %[b1]\n\t"
+        "v_cmp_lt_i32_e64 %[l], %[k], %[k1]\n\t"
+        "v_med3_f32 %[n2], %[b1], %[b2], %[v]\n\t"
+        "v_max_f32 %[n1], %[b1], %[v]\n\t"
+        "s_and_b64 %[e], %[e], %[l]\n\t"
+        "s_or_b64 %[g], %[g], %[e]\n\t"
+        "s_nop 1\n\t"
+        "v_cndmask_b32_e64 %[k1], %[k1], %[k], %[g]\n\t"
+        "s_nop 1"
+        : [k1] "+v"(k1), [n1] "=&v"(n1), [n2] "=&v"(n2), [g] "=&s"(g), [e] "=&s"(e), [l] "=&s"(l)
+        : [v] "v"(v), [k] "v"(k), [b1] "v"(b1), [b2] "v"(b2));
+    b1 = n1;
+    b2 = n2;
 }
 
 // ---- DPP cross-lane steps (VALU operand modifiers: no LDS crossbar round trip).
@@ -113,13 +152,6 @@ __device__ __forceinline__ void dpp_top2_step(float &b1, int &k1, float &b2) {
     top2_merge(b1, k1, b2, ob1, ok1, ob2);
 }
 
-// 16-lane row reductions: result valid in lane 15 of each row
-__device__ __forceinline__ void row_top2(float &b1, int &k1, float &b2) {
-    dpp_top2_step<kDppRowShr1, 0xf>(b1, k1, b2);
-    dpp_top2_step<kDppRowShr2, 0xf>(b1, k1, b2);
-    dpp_top2_step<kDppRowShr4, 0xf>(b1, k1, b2);
-    dpp_top2_step<kDppRowShr8, 0xf>(b1, k1, b2);
-}
 // full-wave reductions: result returned wave-uniform (read from lane 63)
 __device__ __forceinline__ float wave_max(float v) {
     v = fmaxf(v, dpp_f<kDppRowShr1, 0xf>(v));
@@ -194,7 +226,7 @@ __device__ __forceinline__ float entry_d(float x1, float y1, float z1, const flo
 // entries into cidx/cs (unused slots: id -1).  Returns K* (every uncached
 // key <= K*) or +inf when nothing could be cached.  s1/s2: this lane's
 // entries chosen; d1/d2: their squared distances.
-__device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float d2, int32_t *__restrict__ cidx,
+__device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float d2, cid_t *__restrict__ cidx,
                                               float *__restrict__ cs, bool &s1, bool &s2) {
     const int lane = threadIdx.x & 63;
     float Kstar = wave_max(t.a3);
@@ -223,13 +255,13 @@ __device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float 
     if (lane < kL && lane >= cnt) cidx[lane] = -1;  // unused slots
     if (s1) {
         const int p = __popcll(m1 & below);
-        cidx[p] = t.q1;
-        cs[p] = __builtin_sqrtf(d1);
+        cidx[p] = (cid_t)t.q1;
+        if (cs) cs[p] = __builtin_sqrtf(d1);
     }
     if (s2) {
         const int p = __popcll(m1) + __popcll(m2 & below);
-        cidx[p] = t.q2;
-        cs[p] = __builtin_sqrtf(d2);
+        cidx[p] = (cid_t)t.q2;
+        if (cs) cs[p] = __builtin_sqrtf(d2);
     }
     return Kstar;
 }
@@ -257,7 +289,7 @@ __device__ __forceinline__ void wave_top2(float v1, int k1, float v2, int k2, fl
 // non-increasing in d).  T = v(-K*) bounds every uncached value.  The bid is
 // exact whenever b2 > T (caller checks).
 __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const float *Qc, int n,
-                                          int32_t *__restrict__ cidx, float *__restrict__ cs,
+                                          cid_t *__restrict__ cidx, float *__restrict__ cs,
                                           float &b1, int &kb, float &b2, float &T) {
     const int lane = threadIdx.x & 63;
     LaneTop t;
@@ -280,7 +312,7 @@ __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const fl
 // ---- auction full scan, exact: key = the exact bid value.  Always exact
 // bid (the lanes' top-2 hold the global top-2); T = K*.
 __device__ __noinline__ void scan_exact(float x1, float y1, float z1, const float *Qc,
-                                        const float *sPrice, int n, int32_t *__restrict__ cidx,
+                                        const float *sPrice, int n, cid_t *__restrict__ cidx,
                                         float *__restrict__ cs, float &b1, int &kb, float &b2,
                                         float &T) {
     const int lane = threadIdx.x & 63;
@@ -312,7 +344,7 @@ __device__ __noinline__ void scan_exact(float x1, float y1, float z1, const floa
 // entries only; if their second best does not exceed T the exact scan runs
 // instead (~4% of scans).  Returns false when that fallback is needed.
 __device__ __forceinline__ bool scan_fast(float x1, float y1, float z1, const float *Qc,
-                                          const float *sPrice, int n, int32_t *__restrict__ cidx,
+                                          const float *sPrice, int n, cid_t *__restrict__ cidx,
                                           float *__restrict__ cs, float &b1, int &kb, float &b2,
                                           float &T) {
     LaneTop t;
@@ -344,7 +376,7 @@ __device__ __forceinline__ bool scan_fast(float x1, float y1, float z1, const fl
 // ===========================================================================
 __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps,
-    int32_t *__restrict__ cache_idx, float *__restrict__ cache_s, float *__restrict__ cache_T,
+    cid_t *__restrict__ cache_idx, float *__restrict__ cache_s, float *__restrict__ cache_T,
     int32_t *__restrict__ bid0, float *__restrict__ inc0) {
     const int pt = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x) * (kSeedThreads / 64) + (threadIdx.x >> 6);
     const int batch = pt / n;
@@ -364,16 +396,81 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(
 }
 
 // ===========================================================================
+// Cache bids: G lanes per bidder, kL/G cached (id, s) entries per lane at
+// current prices, a row_shr reduction over the G lanes (G divides the 16-lane
+// DPP row); the group's last lane places the bid or lists a full scan.
+// ===========================================================================
+#ifndef PCM_EMD_FORCE_G
+__device__ __forceinline__ int cache_bid_lanes(int nu) {
+    // measured per bidder count on MI355X (tools/tune_emd.py, profiles/r01):
+    // few bidders are latency-bound (more lanes per bidder), many are
+    // VALU-bound (fewer lanes, fewer reduction steps per bidder)
+    return nu <= 64 ? 16 : (nu <= 256 ? 8 : 4);
+}
+#else
+__device__ __forceinline__ int cache_bid_lanes(int) { return PCM_EMD_FORCE_G; }
+#endif
+
+template <int G>
+__device__ __forceinline__ void cache_bids(int nu, float eps, const int *sU, const cid_t *C, const float *CS,
+                                           const float *CT, const float *sPrice, int *sBid, float *sInc, int *sMax,
+                                           int *sMiss, int *sNm) {
+    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
+    static_assert(kL % G == 0, "entries split evenly");
+    constexpr int E = kL / G;
+    const int gi = threadIdx.x / G, gl = threadIdx.x % G;
+    for (int u0 = 0; u0 < nu; u0 += kEmdThreads / G) {
+        const int u = u0 + gi;
+        const bool act = u < nu;
+        const int j = act ? sU[u] : 0;
+        const float tj = CT[j];
+        int ke[E];
+        float se[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) ke[e] = C[(size_t)j * kL + gl + G * e];  // -1: unused slot
+#pragma unroll
+        for (int e = 0; e < E; ++e) se[e] = CS[(size_t)j * kL + gl + G * e];
+        float b1 = -PCM_INF, b2 = -PCM_INF;
+        int kb = 0x7fffffff;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            // branch-free: an unused slot (k = -1) evaluates object 0 and is
+            // then forced to (-inf, INT_MAX)
+            const int k = ke[e];
+            const int neg = k >> 31;
+            const float v0 = value_from_s(se[e], sPrice[k & ~neg]);
+            const float v = __int_as_float((__float_as_int(v0) & ~neg) | (int)(0xff800000u & (unsigned)neg));
+            top2_push(b1, kb, b2, v, k & 0x7fffffff);
+        }
+        if constexpr (G >= 2) dpp_top2_step<kDppRowShr1, 0xf>(b1, kb, b2);
+        if constexpr (G >= 4) dpp_top2_step<kDppRowShr2, 0xf>(b1, kb, b2);
+        if constexpr (G >= 8) dpp_top2_step<kDppRowShr4, 0xf>(b1, kb, b2);
+        if constexpr (G >= 16) dpp_top2_step<kDppRowShr8, 0xf>(b1, kb, b2);
+        if (act && gl == G - 1) {
+            if (b2 > tj) {
+                sBid[j] = kb;
+                sInc[j] = b1 - b2 + eps;
+                atomicMax(&sMax[kb], f2key(b1 - b2 + eps));
+            } else {
+                sMiss[atomicAdd(sNm, 1)] = j;
+            }
+        }
+    }
+}
+
+// ===========================================================================
 // 2. auction kernel: one workgroup per batch element, all iterations
 // ===========================================================================
 
 // kStage: both clouds are copied into LDS (LDS-DMA at kernel start) so the
 // scans read them with LDS latency instead of L2/HBM latency (the seed kernel
 // that last touched them ran on other XCDs, whose L2s this CU does not see).
+// (Measured and rejected: the cached ids in LDS with s recomputed from the
+// staged clouds -- fewer L2 round trips, more VALU: 287 -> 294 us.)
 template <bool kStage>
 __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps, int iters,
-    int32_t *__restrict__ cache_idx, float *__restrict__ cache_s, float *__restrict__ cache_T,
+    cid_t *__restrict__ cache_idx, float *__restrict__ cache_s, float *__restrict__ cache_T,
     const int32_t *__restrict__ bid0,
     const float *__restrict__ inc0, float *__restrict__ dist, int32_t *__restrict__ assignment_out,
     float *__restrict__ price_out, int32_t *__restrict__ stats) {
@@ -403,7 +500,7 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
     }
     const float *Qc = kStage ? (const float *)sQ : Qg;
     const float *P = kStage ? (const float *)sP : Pg;
-    int32_t *C = cache_idx + (size_t)batch * n * kL;
+    cid_t *C = cache_idx + (size_t)batch * n * kL;
     float *CS = cache_s + (size_t)batch * n * kL;
     float *CT = cache_T + (size_t)batch * n;
 
@@ -458,48 +555,16 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
                 }
             }
         } else {
-            // one 16-lane DPP row per point, kL/16 cached (id, s) entries per lane
-            static_assert(kL % 16 == 0, "one cache = one 16-lane DPP row x kL/16 entries");
-            constexpr int E = kL / 16;
-            const int g = tid >> 4, gl = tid & 15;
-            for (int u0 = 0; u0 < nu; u0 += kEmdThreads / 16) {
-                const int u = u0 + g;
-                const bool act = u < nu;
-                const int j = act ? sU[u] : 0;
-                const float tj = CT[j];
-                int ke[E];
-                float se[E];
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    ke[e] = C[(size_t)j * kL + gl + 16 * e];  // -1: unused slot
-                    se[e] = CS[(size_t)j * kL + gl + 16 * e];
-                }
-                float b1 = -PCM_INF, b2 = -PCM_INF;
-                int kb = 0x7fffffff;
-#pragma unroll
-                for (int e = 0; e < E; ++e) {
-                    const int k = ke[e];
-                    const float v = k >= 0 ? value_from_s(se[e], sPrice[k]) : -PCM_INF;
-                    const int kk = k >= 0 ? k : 0x7fffffff;
-                    const bool better = vk_better(v, kk, b1, kb);
-                    b2 = better ? b1 : fmaxf(b2, v);
-                    b1 = better ? v : b1;
-                    kb = better ? kk : kb;
-                }
-                row_top2(b1, kb, b2);  // row result in lane 15
-                if (act && gl == 15) {
-                    if (b2 > tj) {
-                        const float inc = b1 - b2 + eps;
-                        sBid[j] = kb;
-                        sInc[j] = inc;
-                        atomicMax(&sMax[kb], f2key(inc));
-                    } else {
-                        sMiss[atomicAdd(&sNm, 1)] = j;
-                    }
-                }
-            }
+            const int G = cache_bid_lanes(nu);
+            if (G == 16) cache_bids<16>(nu, eps, sU, C, CS, CT, sPrice, sBid, sInc, sMax, sMiss, &sNm);
+            else if (G == 8) cache_bids<8>(nu, eps, sU, C, CS, CT, sPrice, sBid, sInc, sMax, sMiss, &sNm);
+            else if (G == 4) cache_bids<4>(nu, eps, sU, C, CS, CT, sPrice, sBid, sInc, sMax, sMiss, &sNm);
+            else if (G == 2) cache_bids<2>(nu, eps, sU, C, CS, CT, sPrice, sBid, sInc, sMax, sMiss, &sNm);
+            else cache_bids<1>(nu, eps, sU, C, CS, CT, sPrice, sBid, sInc, sMax, sMiss, &sNm);
         }
         __syncthreads();
+        if (stats && tid == 0 && blockIdx.x == 0)  // per-iteration cache-bid time of batch 0
+            stats[2 * iters + 16 + it] = (int)(__builtin_amdgcn_s_memrealtime() - tprev);
         PCM_EMD_PHASE(1);
         // ---- B2: full scans (one wave per missed point), cache rebuilt
         const int nm = sNm;
@@ -512,7 +577,7 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
             float b1, b2, T;
             int kb;
             const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
-            int32_t *cj = C + (size_t)j * kL;
+            cid_t *cj = C + (size_t)j * kL;
             float *sj = CS + (size_t)j * kL;
             const unsigned long long ts0 = stats ? __builtin_amdgcn_s_memrealtime() : 0ull;
             const bool fast_ok = scan_fast(x1, y1, z1, Qc, sPrice, n, cj, sj, b1, kb, b2, T);
@@ -612,11 +677,11 @@ __global__ void emd_bwd_kernel(const float *__restrict__ xyz1, const float *__re
 
 size_t emd_lds_bytes(int n) { return (size_t)9 * 4 * n; }
 
-// workspace layout: cache_idx [b*n*kL] i32 | cache_s [b*n*kL] f32 | cache_T [b*n] f32 |
+// workspace layout: cache_idx [b*n*kL] i16 | cache_s [b*n*kL] f32 | cache_T [b*n] f32 |
 //                   bid0 [b*n] i32 | inc0 [b*n] f32
 size_t ws_bytes(int b, int n) {
     const size_t pts = (size_t)b * n;
-    return pts * kL * 8 + pts * 4 * 3;
+    return pts * kL * (sizeof(cid_t) + 4) + pts * 4 * 3;
 }
 
 }  // namespace
@@ -637,7 +702,7 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     if (n > kEmdMaxN) return PCM_ERR_UNSUPPORTED;
     if (!workspace || workspace_bytes < ws_bytes(b, n)) return PCM_ERR_WORKSPACE;
     const size_t pts = (size_t)b * n;
-    int32_t *cache_idx = (int32_t *)workspace;
+    cid_t *cache_idx = (cid_t *)workspace;
     float *cache_s = (float *)(cache_idx + pts * kL);
     float *cache_T = cache_s + pts * kL;
     int32_t *bid0 = (int32_t *)(cache_T + pts);
@@ -647,16 +712,17 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
                        dim3(kSeedThreads), 0, s, xyz1, xyz2, n, eps, cache_idx, cache_s, cache_T, bid0, inc0);
     const bool stage = n <= kEmdStageMaxN;
     const size_t lds = emd_lds_bytes(n) + (stage ? (size_t)24 * n : 0);
-    const void *kfn = stage ? (const void *)emd_auction_kernel<true> : (const void *)emd_auction_kernel<false>;
-    if (lds > 64 * 1024 &&
-        hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return PCM_ERR_LAUNCH;
-    if (stage)
-        hipLaunchKernelGGL(emd_auction_kernel<true>, dim3(b), dim3(kEmdThreads), lds, s, xyz1, xyz2, n, eps,
-                           iters, cache_idx, cache_s, cache_T, bid0, inc0, dist, assignment, price, stats);
-    else
-        hipLaunchKernelGGL(emd_auction_kernel<false>, dim3(b), dim3(kEmdThreads), lds, s, xyz1, xyz2, n,
-                           eps, iters, cache_idx, cache_s, cache_T, bid0, inc0, dist, assignment, price, stats);
+    auto launch = [&](auto kfn) -> int {
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+                hipSuccess)
+            return PCM_ERR_LAUNCH;
+        hipLaunchKernelGGL(kfn, dim3(b), dim3(kEmdThreads), lds, s, xyz1, xyz2, n, eps, iters, cache_idx,
+                           cache_s, cache_T, bid0, inc0, dist, assignment, price, stats);
+        return PCM_OK;
+    };
+    const int rc = stage ? launch(emd_auction_kernel<true>) : launch(emd_auction_kernel<false>);
+    if (rc != PCM_OK) return rc;
     return pcm_launch_status();
 }
 }  // namespace

@@ -343,14 +343,11 @@ __device__ __noinline__ void scan_exact(float x1, float y1, float z1, const floa
 // independently of the object.  Exact values are computed for the cached
 // entries only; if their second best does not exceed T the exact scan runs
 // instead (~4% of scans).  Returns false when that fallback is needed.
-__device__ __forceinline__ bool scan_fast(float x1, float y1, float z1, const float *Qc,
-                                          const float *sPrice, int n, cid_t *__restrict__ cidx,
-                                          float *__restrict__ cs, float &b1, int &kb, float &b2,
-                                          float &T) {
-    LaneTop t;
-    lane_top_init(t);
+// approximate keys of objects [kbeg, kend) (a multiple of 256 long) into t
+__device__ __forceinline__ void scan_fast_keys(LaneTop &t, float x1, float y1, float z1, const float *Qc,
+                                               const float *sPrice, int kbeg, int kend) {
     const int lane = threadIdx.x & 63;
-    for (int k0 = lane; k0 < n; k0 += 4 * 64) {
+    for (int k0 = kbeg + lane; k0 < kend; k0 += 4 * 64) {
         float key[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -360,6 +357,13 @@ __device__ __forceinline__ bool scan_fast(float x1, float y1, float z1, const fl
 #pragma unroll
         for (int r = 0; r < 4; ++r) lane_top_push(t, key[r], k0 + 64 * r);
     }
+}
+
+// selection, bound and exact bid from the lanes' approximate-key tops
+__device__ __forceinline__ bool scan_fast_finish(const LaneTop &t, float x1, float y1, float z1,
+                                                 const float *Qc, const float *sPrice, int n,
+                                                 cid_t *__restrict__ cidx, float *__restrict__ cs, float &b1,
+                                                 int &kb, float &b2, float &T) {
     bool s1, s2;
     const float d1 = entry_d(x1, y1, z1, Qc, n, t.q1), d2 = entry_d(x1, y1, z1, Qc, n, t.q2);
     const float Kp = select_cache(t, d1, d2, cidx, cs, s1, s2);
@@ -369,6 +373,16 @@ __device__ __forceinline__ bool scan_fast(float x1, float y1, float z1, const fl
     const float v2 = s2 ? value_of(d2, sPrice[t.q2]) : -PCM_INF;
     wave_top2(v1, s1 ? t.q1 : 0x7fffffff, v2, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
     return b2 > T;
+}
+
+__device__ __forceinline__ bool scan_fast(float x1, float y1, float z1, const float *Qc,
+                                          const float *sPrice, int n, cid_t *__restrict__ cidx,
+                                          float *__restrict__ cs, float &b1, int &kb, float &b2,
+                                          float &T) {
+    LaneTop t;
+    lane_top_init(t);
+    scan_fast_keys(t, x1, y1, z1, Qc, sPrice, 0, n);
+    return scan_fast_finish(t, x1, y1, z1, Qc, sPrice, n, cidx, cs, b1, kb, b2, T);
 }
 
 // ===========================================================================
@@ -517,6 +531,7 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
 
     // diagnostics only (stats != nullptr): per-phase wall time of batch 0
     unsigned long long tprev = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long t_start = tprev;
 #define PCM_EMD_PHASE(i)                                                               \
     if (stats && tid == 0 && blockIdx.x == 0) {                                        \
         const unsigned long long tn = __builtin_amdgcn_s_memrealtime();               \
@@ -645,6 +660,8 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
         PCM_EMD_PHASE(5);
     }
 
+    if (stats && tid == 0)  // diagnostics: whole-auction wall time per batch element
+        stats[3 * iters + 16 + blockIdx.x] = (int)(__builtin_amdgcn_s_memrealtime() - t_start);
     // ---- CalcDist (emd_cuda.cu:217-226): deltas xyz1 - xyz2
     for (int j = tid; j < n; j += kEmdThreads) {
         const int k = sAss[j];

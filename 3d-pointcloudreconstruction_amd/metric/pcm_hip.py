@@ -231,11 +231,12 @@ def emd_backward(xyz1, xyz2, graddist, assignment, gradxyz1) -> None:
 
 def tune_emd_forward_stats(xyz1, xyz2, eps: float, iters: int, dist, assignment, stats) -> None:
     """Internal: EMD forward that also accumulates diagnostics into stats (int32,
-    zero-filled, at least 3*iters + 16 entries): [iters, 2] unassigned points and
-    full scans, 16 phase timers and scan counters, then per-iteration cache-bid
-    time of batch 0 (tools/tune_emd.py)."""
-    if stats.numel() < 3 * int(iters) + 16:
-        raise ValueError("stats needs 3*iters + 16 int32 entries")
+    zero-filled, at least 3*iters + 16 + B entries): [iters, 2] unassigned points
+    and full scans, 16 phase timers and scan counters, per-iteration cache-bid
+    time of batch 0, then the auction wall time of each batch element
+    (tools/tune_emd.py)."""
+    if stats.numel() < 3 * int(iters) + 16 + xyz1.shape[0]:
+        raise ValueError("stats needs 3*iters + 16 + B int32 entries")
     dev = _require_device(xyz1, xyz2, dist, assignment, stats)
     b, n, _ = xyz1.shape
     ws_bytes = emd_workspace_bytes(b, n)

@@ -18,12 +18,13 @@ def main(b=16, n=1024, eps=0.005, iters=50):
     x2 = torch.rand(b, n, 3, generator=g).to(dev)
     d = torch.empty(b, n, device=dev)
     a = torch.empty(b, n, dtype=torch.int32, device=dev)
-    st = torch.zeros(3 * iters + 16, dtype=torch.int32, device=dev)
+    st = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=dev)
     pcm_hip.tune_emd_forward_stats(x1, x2, eps, iters, d, a, st)
     torch.cuda.synchronize()
     st = st.cpu()
     ph = st[2 * iters:2 * iters + 6].tolist()
     b1t = st[2 * iters + 16:3 * iters + 16].tolist()
+    wall = st[3 * iters + 16:3 * iters + 16 + b].tolist()
     fb, nw0, tf, te = st[2 * iters + 6:2 * iters + 10].tolist()
     print(f"fast-scan fallbacks (all batches): {fb}; batch-0 wave-0 scans: {nw0}, "
           f"fast {tf / 100.0 / max(nw0, 1):.2f} us/scan, exact-fallback {te / 100.0 / max(nw0, 1):.2f} us/scan")
@@ -34,6 +35,7 @@ def main(b=16, n=1024, eps=0.005, iters=50):
     print("iter: unassigned(sum over batch) full-scans")
     print(" ".join(f"{i}:{int(st[i,0])}/{int(st[i,1])}" for i in range(iters)))
     print("batch-0 cache-bid time per iteration (us):", " ".join(f"{v / 100.0:.2f}" for v in b1t))
+    print("auction wall time per batch element (us):", " ".join(f"{v / 100.0:.1f}" for v in wall))
     print("total unassigned", int(st[:, 0].sum()), "total full scans", int(st[:, 1].sum()))
     pcm_hip.emd_forward(x1, x2, eps, iters, d, a)
     s = torch.cuda.Stream()

@@ -331,7 +331,7 @@ constexpr size_t kTicketBytes = (size_t)(kShards + 1) * kShardStride * 4;  // th
 // overlap that work instead of stalling the workgroup at the next barrier.
 template <int kMode = 1>
 __device__ __forceinline__ unsigned publish_partial(float v, int slot, float *partials, unsigned *ticket,
-                                                    float (*sRed)[16]) {
+                                                    float (*sRed)[16], unsigned epoch = 0) {
     // deterministic workgroup sum, then (tid 0) write-through store, drain,
     // agent atomic ticket (MI355X_MICROARCH.md visibility table, row 1)
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -345,6 +345,12 @@ __device__ __forceinline__ unsigned publish_partial(float v, int slot, float *pa
         for (int w = 0; w < nw; ++w) s += sRed[0][w];
         if constexpr (kMode == 2) {  // reduced by chamfer_loss_finalize_kernel after the kernel boundary
             partials[slot] = s;
+            return 0;
+        }
+        if constexpr (kMode == 3) {  // one {epoch, value} granule, swept by poll_loss
+            __hip_atomic_store(reinterpret_cast<unsigned long long *>(partials) + slot,
+                               ((unsigned long long)epoch << 32) | __float_as_uint(s), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
             return 0;
         }
         __hip_atomic_store(&partials[slot], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -389,6 +395,63 @@ __device__ __forceinline__ void finish_loss(int nb1, int b, int n, int m, const 
     }
 }
 
+// Loss mode 3: the data is the flag.  Every producer workgroup stores its
+// partial as ONE 8-byte {tag = epoch, value} granule (agent-scope relaxed
+// store = sc1 write-through; MI355X_MICROARCH.md visibility, R2: no drain, no
+// fence, no counter), and one extra workgroup -- the grid's last -- sweeps the
+// granules with sc1 loads until every tag carries this call's epoch, then sums
+// them in a fixed order.  The epoch lives in the workspace (word kEpochWord of
+// the ticket line): producers and poller read it at start, the poller
+// advances it at the end, so stream-ordered calls (and graph replays) never
+// match a previous call's granules and nothing needs re-zeroing.  The poll is
+// bounded: after kPollMaxSpins sweeps it writes NaN means and still advances
+// the epoch (no hang, no stale match on the next call).
+constexpr int kEpochWord = 1;
+constexpr unsigned kPollMaxSpins = 1u << 22;
+
+__device__ __forceinline__ void poll_loss(int nb1, int nbt, int b, int n, int m,
+                                          const unsigned long long *__restrict__ gran, unsigned *ticket,
+                                          float *__restrict__ mean_out) {
+    if (threadIdx.x >= 64) return;  // one polling wave
+    const int lane = threadIdx.x;
+    const unsigned epoch = ticket[kEpochWord] + 1u;
+    float s1 = 0.f, s2 = 0.f;
+    bool ok = true;
+    constexpr int R = 8;  // granules per lane per sweep
+    for (int base = 0; base < nbt && ok; base += 64 * R) {
+        unsigned long long x[R];
+        for (unsigned spins = 0;; ++spins) {
+            bool ready = true;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int i = base + r * 64 + lane;
+                x[r] = i < nbt ? __hip_atomic_load(gran + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                               : ((unsigned long long)epoch << 32);
+                ready &= (unsigned)(x[r] >> 32) == epoch;
+            }
+            if (__all(ready)) break;
+            if (spins >= kPollMaxSpins) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int i = base + r * 64 + lane;
+            const float v = __uint_as_float((unsigned)x[r]);
+            if (i < nb1) s1 += v;
+            else if (i < nbt) s2 += v;
+        }
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+        mean_out[0] = ok ? s1 / ((float)b * (float)n) : __builtin_nanf("");
+        mean_out[1] = ok ? s2 / ((float)b * (float)m) : __builtin_nanf("");
+        ticket[kEpochWord] = epoch;
+    }
+}
+
+constexpr int kFwdChk = 8;  // target floats per thread loaded up front (finiteness check + rescan copy)
+
 template <int W, int QPT, int C, int kLoss>
 __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
@@ -417,7 +480,18 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
 
-    int bid = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    int nprod = (int)gridDim.x;  // producer workgroups
+    unsigned epoch = 0;
+    if constexpr (kLoss == 3) {
+        nprod -= 1;
+        if ((int)blockIdx.x == nprod) {  // the grid's last workgroup polls
+            poll_loss(b * nblk1, nprod, b, n, m, reinterpret_cast<const unsigned long long *>(partials), ticket,
+                      mean_out);
+            return;
+        }
+        epoch = ticket[kEpochWord] + 1u;  // plain load: written by an earlier launch
+    }
+    int bid = pcm_xcd_remap((int)blockIdx.x, nprod);
     const int slot = bid;  // logical block id (partials are stored in this order)
     const float *Q, *T;
     float *D;
@@ -468,7 +542,7 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
     }
     // finiteness of the target cloud: issue the loads now, test after the scan
     // (kChk per thread covers 3*nt <= kChk*NT; larger clouds loop at the end)
-    constexpr int kChk = 8;
+    constexpr int kChk = kFwdChk;
     float chk[kChk];
     const bool chk_all = 3 * nt <= kChk * NT;
 #pragma unroll
@@ -570,7 +644,7 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
             sFc[tid] = fc;
             if (qbase + tid < nq) fbv = fb;
         }
-        if constexpr (kLoss != 0) tk = publish_partial<kLoss>(fbv, slot, partials, ticket, sRed);  // has a barrier
+        if constexpr (kLoss != 0) tk = publish_partial<kLoss>(fbv, slot, partials, ticket, sRed, epoch);  // has a barrier
         else __syncthreads();
         // ---- rescan the winning chunk: item -> (query s, part)
 #pragma unroll
@@ -595,6 +669,9 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
                     }
                 }
                 const int k0 = fc * C + part * CP;
+                // (measured and rejected: the up-front finiteness loads parked in
+                // LDS and rescanned from there -- every SGPR variant 0.6-1.5 us
+                // slower at B=32, N=M=1024)
 #pragma unroll
                 for (int k = 0; k < CP; ++k) {
                     const int kk = k0 + k;
@@ -628,7 +705,7 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
             D[qi] = d;
             I[qi] = idx;
         }
-        if constexpr (kLoss != 0) tk = publish_partial<kLoss>(myd, slot, partials, ticket, sRed);
+        if constexpr (kLoss != 0) tk = publish_partial<kLoss>(myd, slot, partials, ticket, sRed, epoch);
     }
     if constexpr (kLoss == 1) {
         if (tid == 0) sLast[0] = tk;
@@ -1119,16 +1196,17 @@ inline bool bad_dims(int b, int n, int m) { return b < 0 || n < 0 || m < 0; }
 typedef void (*fwd_kernel_t)(const float *, const float *, int, int, int, float *, float *,
                              int32_t *, int32_t *, int, int, float *, unsigned *, float *);
 struct FwdVariant {
-    fwd_kernel_t plain, loss, loss2;  // loss: in-kernel ticket; loss2: partials + finalize kernel
+    fwd_kernel_t plain, loss, loss2, loss3;  // loss: in-kernel ticket; loss2: partials + finalize kernel;
+                                             // loss3: granules + polling workgroup
     int waves, qpt;
     bool sgpr;  // SGPR-stream form (else LDS-tile form)
 };
 #define PCM_FWD_LDS(W, Q)                                                              \
     FwdVariant{chamfer_fwd_kernel<W, Q, kChunk, kTile, false>,                         \
-               chamfer_fwd_kernel<W, Q, kChunk, kTile, true>, nullptr, W, Q, false}
+               chamfer_fwd_kernel<W, Q, kChunk, kTile, true>, nullptr, nullptr, W, Q, false}
 #define PCM_FWD_SGPR(W, Q, C)                                                          \
     FwdVariant{chamfer_fwd_sgpr_kernel<W, Q, C, 0>, chamfer_fwd_sgpr_kernel<W, Q, C, 1>, \
-               chamfer_fwd_sgpr_kernel<W, Q, C, 2>, W, Q, true}
+               chamfer_fwd_sgpr_kernel<W, Q, C, 2>, chamfer_fwd_sgpr_kernel<W, Q, C, 3>, W, Q, true}
 const FwdVariant kFwdVariants[] = {
     PCM_FWD_LDS(8, 2),       // 0: LDS-tile form
     PCM_FWD_LDS(8, 4),       // 1
@@ -1146,7 +1224,7 @@ constexpr int kNumFwdVariants = sizeof(kFwdVariants) / sizeof(kFwdVariants[0]);
 // SGPR-stream form wins everywhere; 2 queries per lane and 16-candidate chunks
 // for ShapeNet-size clouds (B=32, N=M=1024: 12.7 us vs 13.5 us LDS-tile), 4
 // queries per lane once a batch has >= 4M pairs (B=8, N=M=16384: 453 us).
-constexpr int kDefaultLossMode = 2;  // tools/tune_chamfer.py: 15.9 vs 16.3 us (B=32, N=M=1024)
+constexpr int kDefaultLossMode = 3;  // tools/tune_chamfer.py (profiles/r01): mode 3 vs 2 vs 1
 inline int default_fwd_variant(int n, int m) {
     return (long long)n * m >= (1LL << 22) ? 3 : 8;
 }
@@ -1157,11 +1235,12 @@ int fwd_grid(const FwdVariant &v, int b, int n, int m, int &nblk1, int &nblk2, l
     nblk1 = (m > 0) ? (n + QW - 1) / QW : 0;
     nblk2 = (n > 0) ? (m + QW - 1) / QW : 0;
     blocks = (long long)b * (nblk1 + nblk2);
-    return blocks > 0x7fffffffLL ? PCM_ERR_UNSUPPORTED : PCM_OK;
+    return blocks > 0x7ffffffeLL ? PCM_ERR_UNSUPPORTED : PCM_OK;  // + 1 polling workgroup (mode 3)
 }
 
 // loss_mode (mean_out != nullptr): 1 = in-kernel arrival ticket + last-workgroup
-// reduction; 2 = workgroup partials + chamfer_loss_finalize_kernel.
+// reduction; 2 = workgroup partials + chamfer_loss_finalize_kernel; 3 = granules
+// swept by one extra polling workgroup (poll_loss).
 int launch_fwd(int variant, const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
                float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out, void *ws, size_t ws_bytes,
                void *stream, int loss_mode = kDefaultLossMode) {
@@ -1185,10 +1264,11 @@ int launch_fwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
         ticket = (unsigned *)ws;
         partials = (float *)((char *)ws + kTicketBytes);
     }
-    if (loss && loss_mode == 2 && !v.loss2) loss_mode = 1;
-    if (loss && (loss_mode < 1 || loss_mode > 2)) return PCM_ERR_INVALID_ARG;
-    fwd_kernel_t k = !loss ? v.plain : (loss_mode == 2 ? v.loss2 : v.loss);
-    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * v.waves), 0, (hipStream_t)stream, xyz1, xyz2,
+    if (loss && loss_mode >= 2 && !v.loss2) loss_mode = 1;
+    if (loss && (loss_mode < 1 || loss_mode > 3)) return PCM_ERR_INVALID_ARG;
+    fwd_kernel_t k = !loss ? v.plain : (loss_mode == 3 ? v.loss3 : (loss_mode == 2 ? v.loss2 : v.loss));
+    const long long grid = blocks + ((loss && loss_mode == 3) ? 1 : 0);  // + the polling workgroup
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * v.waves), 0, (hipStream_t)stream, xyz1, xyz2,
                        b, n, m, dist1, dist2, idx1, idx2, nblk1, nblk2, partials, ticket, mean_out);
     if (loss && loss_mode == 2)
         hipLaunchKernelGGL(chamfer_loss_finalize_kernel, dim3(1), dim3(512), 0, (hipStream_t)stream,
@@ -1207,7 +1287,7 @@ extern "C" size_t pcm_chamfer_workspace_bytes(int b, int n, int m) {
         fwd_grid(kFwdVariants[i], b, n, m, n1, n2, blocks);
         most = blocks > most ? blocks : most;
     }
-    return kTicketBytes + (size_t)most * sizeof(float);
+    return kTicketBytes + (size_t)most * sizeof(unsigned long long);  // 8-B granules (mode 3)
 }
 
 extern "C" int pcm_chamfer_forward(const float *xyz1, const float *xyz2, int b, int n, int m,

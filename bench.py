@@ -45,7 +45,7 @@ GRAPH_STEPS = 10                   # steps captured per hipGraph replay
 # the forward kernel instance the step launches at this size (csrc/chamfer.hip
 # default_fwd_variant) and the committed rocprofv3 counter summary it is looked
 # up in for roofline.traffic (tools/pmc_passes.sh + tools/pmc_summarize.py)
-FWD_KERNEL = "chamfer_fwd_sgpr_kernel<8, 2, 16, true>"
+FWD_KERNEL = "chamfer_fwd_sgpr_kernel<8, 2, 16, 3>"
 BWD_KERNEL = "chamfer_bwd_staged_kernel"
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "pmc_summary.json")
 

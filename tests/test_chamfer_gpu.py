@@ -263,3 +263,40 @@ def test_backward_paths_identical(cuda, oracle, b, n, m):
     for o1, o2 in outs:
         np.testing.assert_array_equal(o1.view(np.int32), r1.view(np.int32))
         np.testing.assert_array_equal(o2.view(np.int32), r2.view(np.int32))
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_fused_loss_modes(cuda, oracle, mode):
+    # every loss hand-off (1: arrival ticket, 2: finalize kernel, 3: granules +
+    # polling workgroup) gives the oracle's per-point outputs and a deterministic
+    # mean, also when the workspace is reused by consecutive and graph-replayed calls
+    import pcm_hip
+    b, n, m = 32, 1024, 1024
+    a, c = _clouds(71, b, n, m)
+    x1, x2 = a.to(cuda), c.to(cuda)
+    d1 = torch.empty(b, n, device=cuda)
+    d2 = torch.empty(b, m, device=cuda)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+    ws = torch.zeros(pcm_hip.chamfer_workspace(cuda, b, n, m).numel(), dtype=torch.uint8, device=cuda)
+    mo = torch.zeros(8, 2, device=cuda)
+    for k in range(4):
+        pcm_hip.tune_chamfer_forward_loss(-1, mode, x1, x2, d1, d2, i1, i2, mo[k], ws)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        pcm_hip.tune_chamfer_forward_loss(-1, mode, x1, x2, d1, d2, i1, i2, mo[4], ws)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for k in (5, 6, 7):
+            pcm_hip.tune_chamfer_forward_loss(-1, mode, x1, x2, d1, d2, i1, i2, mo[k], ws)
+    g.replay()
+    g.replay()
+    torch.cuda.synchronize()
+    mo = mo.cpu()
+    assert all(torch.equal(mo[0], mo[k]) for k in range(8)), mo
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    _assert_fwd_equal((d1.cpu().numpy(), d2.cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()), ref)
+    r = np.array([ref[0].astype(np.float64).mean(), ref[1].astype(np.float64).mean()])
+    np.testing.assert_allclose(mo[0].numpy(), r, rtol=2e-6)

@@ -15,13 +15,13 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o bench --outpu
     -- python3 bench.py --steps 50 --warmup 10 --no-cpu > "$OUT/kt_bench.log" 2>&1
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/kt_eager" -o eager --output-format csv \
     -- python3 "$PROG" > "$OUT/kt_eager.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv \
+timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv \
     -- python3 "$PROG" > "$OUT/fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv \
+timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv \
     -- python3 "$PROG" > "$OUT/write.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/l2" -o l2 --output-format csv \
+timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/l2" -o l2 --output-format csv \
     -- python3 "$PROG" > "$OUT/l2.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES \
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES \
     SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sq" -o sq --output-format csv \
     -- python3 "$PROG" > "$OUT/sq.log" 2>&1
 echo "pmc passes done"

@@ -90,7 +90,7 @@ def main():
         print(f"  bwd staged {out[0]:9.2f} us  global {out[1]:9.2f} us  per-batch-lds {out[2]:9.2f} us  "
               f"fused-loss fwd (default variant) {fl:9.2f} us")
         print(f"  mean=({mo[0].item():.7g},{mo[1].item():.7g}) torch=({d1.mean().item():.7g},{d2.mean().item():.7g})")
-        for mode in (1, 2):
+        for mode in (1, 2, 3):
             mo2 = torch.empty(2, device=dev)
             gm = graph_of(lambda mode=mode: pcm_hip.tune_chamfer_forward_loss(-1, mode, x1, x2, d1, d2, i1, i2,
                                                                             mo2, ws), reps)

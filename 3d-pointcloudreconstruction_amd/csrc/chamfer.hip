@@ -41,9 +41,9 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-template <int W, int QPT, int C, int TILE, bool kLoss>
+template <typename TIn, int W, int QPT, int C, int TILE, bool kLoss>
 __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
-    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
+    const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2, int b, int n, int m,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1,
     int32_t *__restrict__ idx2, int nblk1, int nblk2, float *__restrict__ partials,
     unsigned *__restrict__ ticket, float *__restrict__ mean_out) {
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
     // ---- which (direction, batch, query block) this workgroup owns (uniform)
     int bid = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
     const int slot = bid;  // logical block id (partials are stored in this order)
-    const float *Q, *T;
+    const TIn *Q, *T;
     float *D;
     int32_t *I;
     int nq, nt, blk;
@@ -101,9 +101,9 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
         const int qi = qbase + qq * 64 + lane;
         float x = 0.f, y = 0.f, z = 0.f;
         if (qi < nq) {
-            x = Q[3 * (size_t)qi + 0];
-            y = Q[3 * (size_t)qi + 1];
-            z = Q[3 * (size_t)qi + 2];
+            x = pcm_ld(Q + 3 * (size_t)qi + 0);
+            y = pcm_ld(Q + 3 * (size_t)qi + 1);
+            z = pcm_ld(Q + 3 * (size_t)qi + 2);
             nonfinite |= !(pcm_finite(x) && pcm_finite(y) && pcm_finite(z));
         }
         px[qq] = pcm_f2{x, x};
@@ -123,13 +123,13 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
         // coalesced flat read of the AoS tile, scattered to SoA; pad = +inf.
         // All of a thread's loads are issued before any LDS write, so the
         // tile costs one memory latency, not one per element.
-        const float *src = T + 3 * (size_t)t0;
+        const TIn *src = T + 3 * (size_t)t0;
         constexpr int kFill = (3 * TILE + NT - 1) / NT;
         float v[kFill];
 #pragma unroll
         for (int r = 0; r < kFill; ++r) {
             const int f = tid + r * NT;
-            v[r] = (f < 3 * cnt) ? src[f] : PCM_INF;
+            v[r] = (f < 3 * cnt) ? pcm_ld(src + f) : PCM_INF;
         }
 #pragma unroll
         for (int r = 0; r < kFill; ++r) {
@@ -225,8 +225,8 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
                     for (int k = 0; k < CP; ++k) {
                         const int kk = k0 + k;
                         if (kk >= nt) break;
-                        const float *q = T + 3 * (size_t)kk;
-                        const float d = pcm_sqd(q[0] - x, q[1] - y, q[2] - z);
+                        const TIn *q = T + 3 * (size_t)kk;
+                        const float d = pcm_sqd(pcm_ld(q) - x, pcm_ld(q + 1) - y, pcm_ld(q + 2) - z);
                         if (d == fb) { hit = kk; break; }
                     }
                 }
@@ -253,7 +253,8 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
             if (qi >= nq) continue;
             float d;
             int idx;
-            pcm_ref_nn_scan(Q[3 * (size_t)qi + 0], Q[3 * (size_t)qi + 1], Q[3 * (size_t)qi + 2], T, nt,
+            pcm_ref_nn_scan(pcm_ld(Q + 3 * (size_t)qi + 0), pcm_ld(Q + 3 * (size_t)qi + 1),
+                            pcm_ld(Q + 3 * (size_t)qi + 2), T, nt,
                             d, idx);
             my_d = d;
             D[qi] = d;
@@ -766,10 +767,11 @@ __device__ inline int block_exclusive_scan(int v, int *wave_tot) {
     return before + x - v;
 }
 
+template <typename TIn>
 __global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
-    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
+    const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2, int b, int n, int m,
     const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
-    const int32_t *__restrict__ idx2, float *__restrict__ grad1, float *__restrict__ grad2,
+    const int32_t *__restrict__ idx2, TIn *__restrict__ grad1, TIn *__restrict__ grad2,
     int nblk1, int nblk2) {
     __shared__ int sCnt[kBwdT];
     __shared__ int sOff[kBwdT + 1];
@@ -781,9 +783,10 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
     int bid = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
     // cloud 1 (direct term first) or cloud 2 (direct term last): reference
     // kernel order chamfer3D.cu:184-185.
-    const float *self, *other, *gds, *gdo;
+    const TIn *self, *other;
+    const float *gds, *gdo;
     const int32_t *ids, *ido;
-    float *grad;
+    TIn *grad;
     int ns, no, blk;
     bool direct_first;
     if (bid < b * nblk1) {
@@ -822,14 +825,14 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
     const bool own = tid < T;
     float sx = 0.f, sy = 0.f, sz = 0.f, dir0 = 0.f, dir1 = 0.f, dir2 = 0.f;
     if (own) {
-        sx = self[3 * (size_t)i + 0];
-        sy = self[3 * (size_t)i + 1];
-        sz = self[3 * (size_t)i + 2];
+        sx = pcm_ld(self + 3 * (size_t)i + 0);
+        sy = pcm_ld(self + 3 * (size_t)i + 1);
+        sz = pcm_ld(self + 3 * (size_t)i + 2);
         const int k = ids[i];
         const float g = __fmul_rn(gds[i], 2.f);
-        dir0 = __fmul_rn(g, __fsub_rn(sx, other[3 * (size_t)k + 0]));
-        dir1 = __fmul_rn(g, __fsub_rn(sy, other[3 * (size_t)k + 1]));
-        dir2 = __fmul_rn(g, __fsub_rn(sz, other[3 * (size_t)k + 2]));
+        dir0 = __fmul_rn(g, __fsub_rn(sx, pcm_ld(other + 3 * (size_t)k + 0)));
+        dir1 = __fmul_rn(g, __fsub_rn(sy, pcm_ld(other + 3 * (size_t)k + 1)));
+        dir2 = __fmul_rn(g, __fsub_rn(sz, pcm_ld(other + 3 * (size_t)k + 2)));
     }
 
     // 1. histogram of the other direction's argmins that land in [t0, t0+T)
@@ -881,9 +884,9 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
     }
     auto scatter = [&](int j) {
         const float g = __fmul_rn(gdo[j], 2.f);
-        ax = __fadd_rn(ax, -__fmul_rn(g, __fsub_rn(other[3 * (size_t)j + 0], sx)));
-        ay = __fadd_rn(ay, -__fmul_rn(g, __fsub_rn(other[3 * (size_t)j + 1], sy)));
-        az = __fadd_rn(az, -__fmul_rn(g, __fsub_rn(other[3 * (size_t)j + 2], sz)));
+        ax = __fadd_rn(ax, -__fmul_rn(g, __fsub_rn(pcm_ld(other + 3 * (size_t)j + 0), sx)));
+        ay = __fadd_rn(ay, -__fmul_rn(g, __fsub_rn(pcm_ld(other + 3 * (size_t)j + 1), sy)));
+        az = __fadd_rn(az, -__fmul_rn(g, __fsub_rn(pcm_ld(other + 3 * (size_t)j + 2), sz)));
     };
     if (fits) {
         const int lo = sOff[tid], hi = sOff[tid + 1];
@@ -899,9 +902,9 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
         ay = __fadd_rn(ay, dir1);
         az = __fadd_rn(az, dir2);
     }
-    grad[3 * (size_t)i + 0] = ax;
-    grad[3 * (size_t)i + 1] = ay;
-    grad[3 * (size_t)i + 2] = az;
+    pcm_st(grad + 3 * (size_t)i + 0, ax);
+    pcm_st(grad + 3 * (size_t)i + 1, ay);
+    pcm_st(grad + 3 * (size_t)i + 2, az);
 }
 
 // ---------------------------------------------------------------------------
@@ -1202,8 +1205,8 @@ struct FwdVariant {
     bool sgpr;  // SGPR-stream form (else LDS-tile form)
 };
 #define PCM_FWD_LDS(W, Q)                                                              \
-    FwdVariant{chamfer_fwd_kernel<W, Q, kChunk, kTile, false>,                         \
-               chamfer_fwd_kernel<W, Q, kChunk, kTile, true>, nullptr, nullptr, W, Q, false}
+    FwdVariant{chamfer_fwd_kernel<float, W, Q, kChunk, kTile, false>,                  \
+               chamfer_fwd_kernel<float, W, Q, kChunk, kTile, true>, nullptr, nullptr, W, Q, false}
 #define PCM_FWD_SGPR(W, Q, C)                                                          \
     FwdVariant{chamfer_fwd_sgpr_kernel<W, Q, C, 0>, chamfer_fwd_sgpr_kernel<W, Q, C, 1>, \
                chamfer_fwd_sgpr_kernel<W, Q, C, 2>, chamfer_fwd_sgpr_kernel<W, Q, C, 3>, W, Q, true}
@@ -1357,7 +1360,7 @@ int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
                            gradxyz1, gradxyz2);
         return pcm_launch_status();
     }
-    hipLaunchKernelGGL(chamfer_bwd_kernel, dim3((unsigned)blocks), dim3(kBwdT), 0,
+    hipLaunchKernelGGL(chamfer_bwd_kernel<float>, dim3((unsigned)blocks), dim3(kBwdT), 0,
                        (hipStream_t)stream, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2,
                        gradxyz1, gradxyz2, nblk1, nblk2);
     return pcm_launch_status();
@@ -1379,4 +1382,83 @@ extern "C" int pcm_tune_chamfer_backward(int variant, const float *xyz1, const f
                                          void *stream) {
     return launch_bwd(variant, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1,
                       gradxyz2, stream);
+}
+
+// ---------------------------------------------------------------------------
+// fp16 clouds (BASELINE config 5, an extension: the reference read
+// Tensor::data<float>() only).  Coordinates are widened to fp32 on load
+// (exact), so every result equals the fp32 path on the widened clouds; the
+// gradients are rounded to fp16 once, at the store.  The forward uses the
+// LDS-tile form, which widens each tile as it stages it (one cvt per loaded
+// coordinate per workgroup); the SGPR-stream form would convert every
+// candidate in every wave (3 more VALU per candidate per wave).
+// ---------------------------------------------------------------------------
+namespace {
+typedef void (*fwd16_kernel_t)(const pcm_h *, const pcm_h *, int, int, int, float *, float *, int32_t *,
+                               int32_t *, int, int, float *, unsigned *, float *);
+struct Fwd16Variant {
+    fwd16_kernel_t k;
+    int waves, qpt;
+};
+const Fwd16Variant kFwd16Variants[] = {
+    {chamfer_fwd_kernel<pcm_h, 8, 2, kChunk, kTile, false>, 8, 2},  // 0
+    {chamfer_fwd_kernel<pcm_h, 8, 4, kChunk, kTile, false>, 8, 4},  // 1
+};
+constexpr int kNumFwd16Variants = sizeof(kFwd16Variants) / sizeof(kFwd16Variants[0]);
+inline int default_fwd16_variant(int n, int m) { return (long long)n * m >= (1LL << 22) ? 1 : 0; }
+
+int launch_fwd16(int variant, const pcm_h *xyz1, const pcm_h *xyz2, int b, int n, int m, float *dist1,
+                 float *dist2, int32_t *idx1, int32_t *idx2, void *stream) {
+    if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
+    if (variant < 0 || variant >= kNumFwd16Variants) return PCM_ERR_INVALID_ARG;
+    if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
+    if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2)))
+        return PCM_ERR_INVALID_ARG;
+    const Fwd16Variant &v = kFwd16Variants[variant];
+    const int QW = 64 * v.qpt;
+    const int nblk1 = (m > 0) ? (n + QW - 1) / QW : 0;
+    const int nblk2 = (n > 0) ? (m + QW - 1) / QW : 0;
+    const long long blocks = (long long)b * (nblk1 + nblk2);
+    if (blocks > 0x7fffffffLL) return PCM_ERR_UNSUPPORTED;
+    if (blocks == 0) return PCM_OK;
+    hipLaunchKernelGGL(v.k, dim3((unsigned)blocks), dim3(64 * v.waves), 0, (hipStream_t)stream, xyz1, xyz2, b,
+                       n, m, dist1, dist2, idx1, idx2, nblk1, nblk2, nullptr, nullptr, nullptr);
+    return pcm_launch_status();
+}
+}  // namespace
+
+extern "C" int pcm_chamfer_forward_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
+                                       float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                                       void *stream) {
+    return launch_fwd16(default_fwd16_variant(n, m), (const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n, m, dist1,
+                        dist2, idx1, idx2, stream);
+}
+
+extern "C" int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, const uint16_t *xyz2, int b,
+                                            int n, int m, float *dist1, float *dist2, int32_t *idx1,
+                                            int32_t *idx2, void *stream) {
+    if (variant < 0) variant = default_fwd16_variant(n, m);
+    return launch_fwd16(variant, (const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n, m, dist1, dist2, idx1, idx2,
+                        stream);
+}
+
+extern "C" int pcm_tune_num_chamfer_f16_variants(void) { return kNumFwd16Variants; }
+
+extern "C" int pcm_chamfer_backward_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
+                                        const float *graddist1, const float *graddist2,
+                                        const int32_t *idx1, const int32_t *idx2, uint16_t *gradxyz1,
+                                        uint16_t *gradxyz2, void *stream) {
+    if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
+    if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
+    if (n == 0 || m == 0) return PCM_ERR_INVALID_ARG;
+    if (!xyz1 || !xyz2 || !graddist1 || !graddist2 || !idx1 || !idx2 || !gradxyz1 || !gradxyz2)
+        return PCM_ERR_INVALID_ARG;
+    const int nblk1 = (n + kBwdT - 1) / kBwdT;
+    const int nblk2 = (m + kBwdT - 1) / kBwdT;
+    const long long blocks = (long long)b * (nblk1 + nblk2);
+    if (blocks > 0x7fffffffLL) return PCM_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(chamfer_bwd_kernel<pcm_h>, dim3((unsigned)blocks), dim3(kBwdT), 0, (hipStream_t)stream,
+                       (const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n, m, graddist1, graddist2, idx1, idx2,
+                       (pcm_h *)gradxyz1, (pcm_h *)gradxyz2, nblk1, nblk2);
+    return pcm_launch_status();
 }

@@ -27,11 +27,21 @@ __device__ __forceinline__ bool pcm_finite(float v) {
     return __builtin_isfinite(v);
 }
 
+// Input element types: fp32, or IEEE binary16 (BASELINE config 5) widened to
+// fp32 on load -- exact, so every fp16 result equals the fp32 result on the
+// widened cloud.
+typedef _Float16 pcm_h;
+__device__ __forceinline__ float pcm_ld(const float *p) { return *p; }
+__device__ __forceinline__ float pcm_ld(const pcm_h *p) { return (float)*p; }
+__device__ __forceinline__ void pcm_st(float *p, float v) { *p = v; }
+__device__ __forceinline__ void pcm_st(pcm_h *p, float v) { *p = (pcm_h)v; }  // round to nearest even
+
 // Reference-exact single-query scan (NmDistanceKernel, chamfer3D.cu:12-134):
 // 512-point tiles, best = d(first) per tile, strict '<' inside, strict '>'
 // across tiles.  Used only when non-finite coordinates are present, where the
 // tile boundaries decide which NaN wins.  `t` = target cloud [m,3] in global.
-__device__ inline void pcm_ref_nn_scan(float x1, float y1, float z1, const float *__restrict__ t,
+template <typename TIn>
+__device__ inline void pcm_ref_nn_scan(float x1, float y1, float z1, const TIn *__restrict__ t,
                                        int m, float &out_d, int &out_i) {
     float res = 0.f;
     int res_i = 0;
@@ -40,8 +50,8 @@ __device__ inline void pcm_ref_nn_scan(float x1, float y1, float z1, const float
         float best = 0.f;
         int best_i = 0;
         for (int k = 0; k < end_k; ++k) {
-            const float *q = t + 3 * (size_t)(k2 + k);
-            const float d = pcm_sqd(q[0] - x1, q[1] - y1, q[2] - z1);
+            const TIn *q = t + 3 * (size_t)(k2 + k);
+            const float d = pcm_sqd(pcm_ld(q) - x1, pcm_ld(q + 1) - y1, pcm_ld(q + 2) - z1);
             if (k == 0 || d < best) { best = d; best_i = k + k2; }
         }
         if (k2 == 0 || res > best) { res = best; res_i = best_i; }

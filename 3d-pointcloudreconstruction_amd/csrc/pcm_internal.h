@@ -16,6 +16,9 @@ int pcm_tune_chamfer_backward(int variant, const float *xyz1, const float *xyz2,
 int pcm_tune_chamfer_forward_loss(int variant, int loss_mode, const float *xyz1, const float *xyz2, int b,
                                   int n, int m, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                   float *mean_out, void *workspace, size_t workspace_bytes, void *stream);
+int pcm_tune_num_chamfer_f16_variants(void);
+int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
+                                 float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, void *stream);
 int pcm_tune_emd_forward_stats(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
                                float *dist, int32_t *assignment, void *workspace,
                                size_t workspace_bytes, int32_t *stats, void *stream);

@@ -5,6 +5,9 @@ Same module name, classes and signatures as the reference
 (dist1, dist2, idx1, idx2)``, ``.backward(ctx, graddist1, graddist2, gradidx1,
 gradidx2) -> (gradxyz1, gradxyz2)`` and ``chamfer_3DDist()(input1, input2)``.
 Outputs keep the reference dtypes: float32 distances, int32 indices.
+Extension: float16 clouds are accepted as well (BASELINE config 5); distances
+stay float32 and gradients come back in float16 (the fp32 gradient of the
+widened clouds, rounded once).
 
 Differences, all on the "stricter" side:
   * outputs are allocated directly on the device (the reference built them on
@@ -34,9 +37,10 @@ class chamfer_3DFunction(Function):
         _, m, dim = xyz2.size()
         assert dim == 3, "Wrong last dimension for the chamfer distance 's input! Check with .size()"
         assert xyz2.size(0) == batchsize, "batch sizes of the two clouds differ"
-        if xyz1.dtype != torch.float32 or xyz2.dtype != torch.float32:
-            # the reference read Tensor::data<float>() and threw otherwise
-            raise TypeError("chamfer_3DFunction expects float32 clouds")
+        if xyz1.dtype != xyz2.dtype or xyz1.dtype not in (torch.float32, torch.float16):
+            # the reference read Tensor::data<float>() and threw otherwise;
+            # float16 is this build's extension
+            raise TypeError("chamfer_3DFunction expects float32 (or float16) clouds of one dtype")
         xyz1 = xyz1.contiguous()
         xyz2 = xyz2.contiguous()
         device = xyz1.device

@@ -25,6 +25,7 @@ EXPORTED = (
     "pcm_chamfer_forward", "pcm_chamfer_backward",
     "pcm_chamfer_workspace_bytes", "pcm_chamfer_forward_loss",
     "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward",
+    "pcm_chamfer_forward_f16", "pcm_chamfer_backward_f16",
 )
 
 
@@ -66,6 +67,14 @@ def load_library():
     L.pcm_tune_chamfer_forward_loss.argtypes = [ci, ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, cs, vp]
     L.pcm_tune_emd_forward_stats.restype = ci
     L.pcm_tune_emd_forward_stats.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, cs, vp, vp]
+    L.pcm_chamfer_forward_f16.restype = ci
+    L.pcm_chamfer_forward_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
+    L.pcm_chamfer_backward_f16.restype = ci
+    L.pcm_chamfer_backward_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
+    L.pcm_tune_num_chamfer_f16_variants.restype = ci
+    L.pcm_tune_num_chamfer_f16_variants.argtypes = []
+    L.pcm_tune_chamfer_forward_f16.restype = ci
+    L.pcm_tune_chamfer_forward_f16.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
     L.pcm_emd_workspace_bytes.restype = cs
     L.pcm_emd_workspace_bytes.argtypes = [ci, ci]
     L.pcm_emd_forward.restype = ci
@@ -105,15 +114,38 @@ def _stream(dev: torch.device):
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
 
 
+def _cloud_kind(xyz1, xyz2) -> str:
+    if xyz1.dtype != xyz2.dtype or xyz1.dtype not in (torch.float32, torch.float16):
+        raise TypeError(f"Chamfer clouds must both be float32 or both float16 (got {xyz1.dtype}, {xyz2.dtype})")
+    return "f16" if xyz1.dtype == torch.float16 else "f32"
+
+
 def chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:
-    """pcm_chamfer_forward on contiguous [B,N,3]/[B,M,3] float32 device tensors."""
+    """pcm_chamfer_forward (float32 clouds) or pcm_chamfer_forward_f16 (float16
+    clouds) on contiguous [B,N,3]/[B,M,3] device tensors; dist is float32."""
+    dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    fn = "pcm_chamfer_forward_f16" if _cloud_kind(xyz1, xyz2) == "f16" else "pcm_chamfer_forward"
+    with torch.cuda.device(dev):
+        _check(getattr(load_library(), fn)(
+            _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
+            _stream(dev)), fn)
+
+
+def tune_chamfer_forward_f16(variant, xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:
+    """Internal: fp16 forward variant `variant` (-1 = default)."""
     dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2)
     b, n, _ = xyz1.shape
     m = xyz2.shape[1]
     with torch.cuda.device(dev):
-        _check(load_library().pcm_chamfer_forward(
-            _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
-            _stream(dev)), "pcm_chamfer_forward")
+        _check(load_library().pcm_tune_chamfer_forward_f16(
+            int(variant), _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1),
+            _ptr(idx2), _stream(dev)), "pcm_tune_chamfer_forward_f16")
+
+
+def tune_num_chamfer_f16_variants() -> int:
+    return int(load_library().pcm_tune_num_chamfer_f16_variants())
 
 
 _ws_cache = {}
@@ -190,13 +222,19 @@ def tune_num_chamfer_variants() -> int:
 
 
 def chamfer_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2) -> None:
+    """pcm_chamfer_backward (float32 clouds and gradients) or pcm_chamfer_backward_f16
+    (float16 clouds and gradients); graddist is float32 in both."""
     dev = _require_device(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
     b, n, _ = xyz1.shape
     m = xyz2.shape[1]
+    kind = _cloud_kind(xyz1, xyz2)
+    if gradxyz1.dtype != xyz1.dtype or gradxyz2.dtype != xyz2.dtype:
+        raise TypeError("gradients must have the clouds' dtype")
+    fn = "pcm_chamfer_backward_f16" if kind == "f16" else "pcm_chamfer_backward"
     with torch.cuda.device(dev):
-        _check(load_library().pcm_chamfer_backward(
+        _check(getattr(load_library(), fn)(
             _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(graddist1), _ptr(graddist2), _ptr(idx1),
-            _ptr(idx2), _ptr(gradxyz1), _ptr(gradxyz2), _stream(dev)), "pcm_chamfer_backward")
+            _ptr(idx2), _ptr(gradxyz1), _ptr(gradxyz2), _stream(dev)), fn)
 
 
 def emd_workspace_bytes(b: int, n: int) -> int:

@@ -16,7 +16,8 @@ through the Python API each step.
 
 value = point pairs evaluated per second over all ranks (2*B*N*M per rank per
 step / max-over-ranks wall time).  EMD (BASELINE config 3: B=16, N=1024,
-50 iterations, eps=0.005) is reported alongside as iterations/s.
+50 iterations, eps=0.005) is reported alongside as iterations/s, and the dense
+fp16 Chamfer (BASELINE config 5: B=8, N=M=16384) as point-pairs/s.
 
 Multi-GPU: one process per GPU (torchrun), batches sharded (weak scaling: each
 rank owns its own B=32 clouds).  Every step's loss pair is all-reduced over
@@ -68,6 +69,7 @@ def parse():
     p.add_argument("--eager", action="store_true", help="no hipGraph capture")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-emd", action="store_true", help="skip the EMD leg")
+    p.add_argument("--no-dense", action="store_true", help="skip the dense fp16 (config 5) leg")
     p.add_argument("--dist-backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -172,6 +174,35 @@ def emd_leg(dev, reps=10):
     us = kernel_avg_us(run, reps, dev, graph=False)  # ~400 us launches: host cost hidden
     return {"config": f"B={EMD_B} N=M={EMD_N} iters={EMD_ITERS} eps={EMD_EPS}",
             "ms_per_forward": us / 1000.0, "iters_per_s": EMD_ITERS / (us * 1e-6)}
+
+
+def dense_f16_leg(dev, reps=10):
+    """BASELINE config 5: dense Chamfer fwd+bwd, B=8, N=M=16384, fp16 clouds
+    (fp32 arithmetic on the exactly-widened coordinates), graph-timed."""
+    b, n = 8, 16384
+    g = torch.Generator(device="cpu").manual_seed(5)
+    x1 = torch.rand(b, n, 3, generator=g).half().to(dev)
+    x2 = torch.rand(b, n, 3, generator=g).half().to(dev)
+    d1, d2 = torch.empty(b, n, device=dev), torch.empty(b, n, device=dev)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=dev)
+    i2 = torch.empty(b, n, dtype=torch.int32, device=dev)
+    g1 = torch.full((b, n), 1.0 / (b * n), device=dev)
+    g2 = torch.full((b, n), 1.0 / (b * n), device=dev)
+    gx1 = torch.empty_like(x1)
+    gx2 = torch.empty_like(x2)
+
+    def fwd():
+        pcm_hip.chamfer_forward(x1, x2, d1, d2, i1, i2)
+
+    def bwd():
+        pcm_hip.chamfer_backward(x1, x2, g1, g2, i1, i2, gx1, gx2)
+
+    f_us = kernel_avg_us(fwd, reps, dev)
+    b_us = kernel_avg_us(bwd, reps, dev)
+    pairs = 2 * b * n * n
+    return {"config": f"B={b} N=M={n} fp16 clouds, fp32 arithmetic", "fwd_us": f_us, "bwd_us": b_us,
+            "pairs_per_s": pairs / ((f_us + b_us) * 1e-6),
+            "fwd_tflops": pairs * FLOP_PER_PAIR / (f_us * 1e-6) / 1e12}
 
 
 def pmc_bytes(kernel):
@@ -313,6 +344,8 @@ def main():
     }
     if not args.no_emd:
         out["emd"] = emd_leg(dev)
+    if not args.no_dense:
+        out["dense_fp16"] = dense_f16_leg(dev)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -98,6 +98,21 @@ int pcm_chamfer_backward(const float *xyz1, const float *xyz2, int b, int n, int
                          const int32_t *idx1, const int32_t *idx2,
                          float *gradxyz1, float *gradxyz2, void *stream);
 
+/*
+ * fp16 clouds (extension for BASELINE config 5; the reference accepted fp32
+ * only).  xyz1/xyz2 hold IEEE binary16 values.  Coordinates are widened to
+ * fp32 exactly, so dist/idx are bit-identical to pcm_chamfer_forward on the
+ * widened clouds (fp32 outputs, as the reference's), and the gradients are the
+ * fp32 path's gradients rounded once to binary16 (nearest even).
+ */
+int pcm_chamfer_forward_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
+                            float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                            void *stream);
+int pcm_chamfer_backward_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
+                             const float *graddist1, const float *graddist2,
+                             const int32_t *idx1, const int32_t *idx2,
+                             uint16_t *gradxyz1, uint16_t *gradxyz2, void *stream);
+
 /* ---------------------------------------------------------------------- */
 /* EMD (auction approximation)                                             */
 /* ---------------------------------------------------------------------- */

@@ -25,6 +25,9 @@ def test_chamfer_rejects_non_float32():
     import dist_chamfer_3D
     with pytest.raises(TypeError):
         dist_chamfer_3D.chamfer_3DFunction.apply(torch.rand(2, 8, 3).double(), torch.rand(2, 9, 3))
+    # float16 is accepted (extension), but only with both clouds float16
+    with pytest.raises(TypeError):
+        dist_chamfer_3D.chamfer_3DFunction.apply(torch.rand(2, 8, 3).half(), torch.rand(2, 9, 3))
 
 
 def test_emd_contract_asserts():

@@ -53,6 +53,11 @@ def test_invalid_arguments_rejected_without_device(lib):
     assert L.pcm_emd_forward(null, null, 2, 1000, 0.005, 50, null, null, null, null, 0, null) == -1
     assert L.pcm_emd_forward(null, null, 513, 1024, 0.005, 50, null, null, null, null, 0, null) == -1
     assert L.pcm_emd_forward(null, null, 2, 1024, 0.005, 0, null, null, null, null, 0, null) == -1
+    # fp16 entry points validate the same way
+    assert L.pcm_chamfer_forward_f16(null, null, -1, 4, 4, null, null, null, null, null) == -1
+    assert L.pcm_chamfer_forward_f16(null, null, 2, 4, 4, null, null, null, null, null) == -1
+    assert L.pcm_chamfer_backward_f16(null, null, 2, 0, 4, null, null, null, null, null, null, null) == -1
+    assert L.pcm_chamfer_forward_f16(null, null, 0, 4, 4, null, null, null, null, null) == 0
     # empty problems are no-ops
     assert L.pcm_chamfer_forward(null, null, 0, 4, 4, null, null, null, null, null) == 0
     assert L.pcm_emd_forward(null, null, 0, 1024, 0.005, 50, null, null, null, null, 0, null) == 0

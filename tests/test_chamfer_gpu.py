@@ -300,3 +300,69 @@ def test_fused_loss_modes(cuda, oracle, mode):
     _assert_fwd_equal((d1.cpu().numpy(), d2.cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()), ref)
     r = np.array([ref[0].astype(np.float64).mean(), ref[1].astype(np.float64).mean()])
     np.testing.assert_allclose(mo[0].numpy(), r, rtol=2e-6)
+
+
+# ---- fp16 clouds (BASELINE config 5; an extension of the reference's fp32-only API)
+@pytest.mark.parametrize("b,n,m,seed", [(4, 256, 256, 80), (32, 1024, 1024, 81), (3, 1000, 2000, 82),
+                                        (1, 2049, 2047, 83), (2, 33, 31, 84)])
+def test_forward_f16_matches_widened_oracle(cuda, oracle, b, n, m, seed):
+    a, c = _clouds(seed, b, n, m)
+    ah, ch = a.half(), c.half()
+    got = _run_fwd(ah, ch, cuda)
+    ref = oracle.chamfer_forward(ah.float().numpy(), ch.float().numpy())
+    _assert_fwd_equal(got, ref)
+
+
+def test_forward_f16_config5_dense(cuda, oracle):
+    # BASELINE config 5: B=8, N=M=16384, fp16 clouds
+    a, c = _clouds(85, 8, 16384, 16384)
+    ah, ch = a.half(), c.half()
+    got = _run_fwd(ah, ch, cuda)
+    ref = oracle.chamfer_forward(ah.float().numpy(), ch.float().numpy())
+    _assert_fwd_equal(got, ref)
+
+
+def test_f16_duplicates_and_nonfinite(cuda, oracle):
+    a, c = _clouds(86, 2, 700, 300)
+    c = torch.cat([c, c], dim=1)
+    a[:, :40] = c[:, 5:45]
+    c[1, 512, 0] = float("nan")          # tile-start NaN: reference tile semantics
+    ah, ch = a.half(), c.half()
+    got = _run_fwd(ah, ch, cuda)
+    ref = oracle.chamfer_forward(ah.float().numpy(), ch.float().numpy())
+    for g, r in zip(got[2:], ref[2:]):
+        np.testing.assert_array_equal(g, r)
+    for g, r in zip(got[:2], ref[:2]):
+        np.testing.assert_array_equal(np.isnan(g), np.isnan(r))
+        fin = ~np.isnan(r)
+        np.testing.assert_array_equal(g[fin].view(np.int32), r[fin].view(np.int32))
+
+
+@pytest.mark.parametrize("b,n,m,seed", [(4, 256, 256, 90), (8, 1024, 1024, 91), (2, 3000, 1500, 92)])
+def test_backward_f16_is_rounded_fp32_gradient(cuda, oracle, b, n, m, seed):
+    a, c = _clouds(seed, b, n, m)
+    ah, ch = a.half(), c.half()
+    gen = torch.Generator().manual_seed(200 + seed)
+    g1 = torch.rand(b, n, generator=gen)
+    g2 = torch.rand(b, m, generator=gen)
+    gx1, gx2, i1, i2 = _grads(ah, ch, g1, g2, cuda)
+    assert gx1.dtype == np.float16 and gx2.dtype == np.float16
+    r1, r2 = oracle.chamfer_backward(ah.float().numpy(), ch.float().numpy(), g1.numpy(), g2.numpy(), i1, i2)
+    np.testing.assert_array_equal(gx1.view(np.int16), r1.astype(np.float16).view(np.int16))
+    np.testing.assert_array_equal(gx2.view(np.int16), r2.astype(np.float16).view(np.int16))
+
+
+def test_all_f16_variants_bit_identical(cuda, oracle):
+    import pcm_hip
+    a, c = _clouds(93, 3, 1500, 700, "normal")
+    ah, ch = a.half(), c.half()
+    ref = oracle.chamfer_forward(ah.float().numpy(), ch.float().numpy())
+    x1, x2 = ah.to(cuda), ch.to(cuda)
+    for v in range(pcm_hip.tune_num_chamfer_f16_variants()):
+        d1 = torch.empty(3, 1500, device=cuda)
+        d2 = torch.empty(3, 700, device=cuda)
+        i1 = torch.empty(3, 1500, dtype=torch.int32, device=cuda)
+        i2 = torch.empty(3, 700, dtype=torch.int32, device=cuda)
+        pcm_hip.tune_chamfer_forward_f16(v, x1, x2, d1, d2, i1, i2)
+        torch.cuda.synchronize()
+        _assert_fwd_equal((d1.cpu().numpy(), d2.cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()), ref)

@@ -107,5 +107,31 @@ def main():
         print(f"  eager python-API bwd call: {e0.elapsed_time(e1) * 1000 / reps:9.2f} us/call")
 
 
+def main_f16():
+    """fp16-cloud forward variants (BASELINE config 5) and the fp16 backward."""
+    dev = torch.device("cuda:0")
+    nv = pcm_hip.tune_num_chamfer_f16_variants()
+    for (b, n, m, reps, rounds) in [(32, 1024, 1024, 50, 5), (8, 16384, 16384, 2, 3)]:
+        x1, x2, d1, d2, i1, i2 = bufs(b, n, m, dev)
+        x1, x2 = x1.half(), x2.half()
+        graphs = {v: graph_of(lambda v=v: pcm_hip.tune_chamfer_forward_f16(v, x1, x2, d1, d2, i1, i2), reps)
+                  for v in range(nv)}
+        res = {v: [] for v in range(nv)}
+        for _ in range(rounds):
+            for v in range(nv):
+                res[v].append(time_graph_us(graphs[v], reps))
+        pairs = 2 * b * n * m
+        print(f"fp16 config B={b} N={n} M={m}")
+        for v in range(nv):
+            med = statistics.median(res[v])
+            print(f"  f16 fwd variant {v}: median {med:9.2f} us  {pairs / med / 1e6:8.3f} Tpairs/s")
+        g1 = torch.full((b, n), 1.0 / (b * n), device=dev)
+        g2 = torch.full((b, m), 1.0 / (b * m), device=dev)
+        gx1, gx2 = torch.empty_like(x1), torch.empty_like(x2)
+        gr = graph_of(lambda: pcm_hip.chamfer_backward(x1, x2, g1, g2, i1, i2, gx1, gx2), reps)
+        print(f"  f16 bwd: {statistics.median([time_graph_us(gr, reps) for _ in range(rounds)]):9.2f} us")
+
+
 if __name__ == "__main__":
     main()
+    main_f16()

@@ -29,17 +29,14 @@
 // no float atomics), in the reference's kernel order (chamfer3D.cu:184-185).
 #include "pcm_common.h"
 #include "pcm_internal.h"
+#include "chamfer_loss.h"
+
+using namespace pcm_loss;
 
 namespace {
 
 constexpr int kTile = 2048;  // candidates per LDS tile (3 x 8 KiB SoA)
 constexpr int kChunk = 32;   // candidates per chunk (rescan granularity)
-
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
 
 template <typename TIn, int W, int QPT, int C, int TILE, bool kLoss>
 __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
@@ -204,7 +201,7 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
                 for (int w = 1; w < W; ++w) {
                     const float v = sBest[w][s];
                     const int c = sChunk[w][s];
-                    if (v < fb || (v == fb && c < fc)) { fb = v; fc = c; }
+                    pcm_lexmin(fb, fc, v, c);
                 }
                 // item % 64 == lane, so query s is this lane's register copy
                 // number (item / 64) % QPT -- wave-uniform, no reload
@@ -317,139 +314,6 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
 // workgroup's partial sum is published right after the merge and the arrival
 // ticket's round trip overlaps the rescan.
 // ---------------------------------------------------------------------------
-
-// Arrival tickets are sharded two-level: one arrival counter per 128-byte line
-// for each of kShards shards (block id mod kShards), and a top counter that
-// only each shard's last arriver increments.  512 arrivals on ONE counter
-// serialise at ~12 ns each (MI355X_MICROARCH.md price list, row "fanin");
-// sharded, the tail sees ~16 + 32 arrivals.
-constexpr int kShards = 32;
-constexpr int kShardStride = 32;  // unsigned words = 128 B per counter line
-constexpr size_t kTicketBytes = (size_t)(kShards + 1) * kShardStride * 4;  // then the partials
-
-// Returns 1 in thread 0 of the overall last-arriving workgroup, else 0.  The
-// caller tests it only after its remaining work, so the atomics' round trips
-// overlap that work instead of stalling the workgroup at the next barrier.
-template <int kMode = 1>
-__device__ __forceinline__ unsigned publish_partial(float v, int slot, float *partials, unsigned *ticket,
-                                                    float (*sRed)[16], unsigned epoch = 0) {
-    // deterministic workgroup sum, then (tid 0) write-through store, drain,
-    // agent atomic ticket (MI355X_MICROARCH.md visibility table, row 1)
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const float ws = wave_sum(v);
-    if (lane == 0) sRed[0][wave] = ws;
-    __syncthreads();
-    unsigned last = 0;
-    if (threadIdx.x == 0) {
-        float s = 0.f;
-        const int nw = blockDim.x >> 6;
-        for (int w = 0; w < nw; ++w) s += sRed[0][w];
-        if constexpr (kMode == 2) {  // reduced by chamfer_loss_finalize_kernel after the kernel boundary
-            partials[slot] = s;
-            return 0;
-        }
-        if constexpr (kMode == 3) {  // one {epoch, value} granule, swept by poll_loss
-            __hip_atomic_store(reinterpret_cast<unsigned long long *>(partials) + slot,
-                               ((unsigned long long)epoch << 32) | __float_as_uint(s), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            return 0;
-        }
-        __hip_atomic_store(&partials[slot], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned nb = gridDim.x;
-        const unsigned sh = blockIdx.x % kShards;
-        const unsigned in_shard = (nb - sh + kShards - 1) / kShards;
-        const unsigned active = nb < kShards ? nb : kShards;
-        const unsigned t = __hip_atomic_fetch_add(ticket + kShardStride * (1 + sh), 1u, __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT);
-        if (t == in_shard - 1) {
-            const unsigned u = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            last = (u == active - 1);
-        }
-    }
-    return last;
-}
-
-__device__ __forceinline__ void finish_loss(int nb1, int b, int n, int m, const float *partials,
-                                            unsigned *ticket, float *mean_out, float (*sRed)[16]) {
-    // the last-arriving workgroup: fixed-order reduction of every partial
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int nbt = (int)gridDim.x;
-    float s1 = 0.f, s2 = 0.f;
-    for (int i = threadIdx.x; i < nbt; i += blockDim.x) {
-        const float v = __hip_atomic_load(&partials[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (i < nb1) s1 += v; else s2 += v;
-    }
-    s1 = wave_sum(s1);
-    s2 = wave_sum(s2);
-    if (lane == 0) { sRed[0][wave] = s1; sRed[1][wave] = s2; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float a1 = 0.f, a2 = 0.f;
-        const int nw = blockDim.x >> 6;
-        for (int w = 0; w < nw; ++w) { a1 += sRed[0][w]; a2 += sRed[1][w]; }
-        mean_out[0] = a1 / ((float)b * (float)n);
-        mean_out[1] = a2 / ((float)b * (float)m);
-        // every arrival is in: re-arm the counters for the next stream-ordered call
-        for (int s = 0; s <= kShards; ++s)
-            __hip_atomic_store(ticket + kShardStride * s, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-}
-
-// Loss mode 3: the data is the flag.  Every producer workgroup stores its
-// partial as ONE 8-byte {tag = epoch, value} granule (agent-scope relaxed
-// store = sc1 write-through; MI355X_MICROARCH.md visibility, R2: no drain, no
-// fence, no counter), and one extra workgroup -- the grid's last -- sweeps the
-// granules with sc1 loads until every tag carries this call's epoch, then sums
-// them in a fixed order.  The epoch lives in the workspace (word kEpochWord of
-// the ticket line): producers and poller read it at start, the poller
-// advances it at the end, so stream-ordered calls (and graph replays) never
-// match a previous call's granules and nothing needs re-zeroing.  The poll is
-// bounded: after kPollMaxSpins sweeps it writes NaN means and still advances
-// the epoch (no hang, no stale match on the next call).
-constexpr int kEpochWord = 1;
-constexpr unsigned kPollMaxSpins = 1u << 22;
-
-__device__ __forceinline__ void poll_loss(int nb1, int nbt, int b, int n, int m,
-                                          const unsigned long long *__restrict__ gran, unsigned *ticket,
-                                          float *__restrict__ mean_out) {
-    if (threadIdx.x >= 64) return;  // one polling wave
-    const int lane = threadIdx.x;
-    const unsigned epoch = ticket[kEpochWord] + 1u;
-    float s1 = 0.f, s2 = 0.f;
-    bool ok = true;
-    constexpr int R = 8;  // granules per lane per sweep
-    for (int base = 0; base < nbt && ok; base += 64 * R) {
-        unsigned long long x[R];
-        for (unsigned spins = 0;; ++spins) {
-            bool ready = true;
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const int i = base + r * 64 + lane;
-                x[r] = i < nbt ? __hip_atomic_load(gran + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                               : ((unsigned long long)epoch << 32);
-                ready &= (unsigned)(x[r] >> 32) == epoch;
-            }
-            if (__all(ready)) break;
-            if (spins >= kPollMaxSpins) { ok = false; break; }
-            __builtin_amdgcn_s_sleep(1);
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int i = base + r * 64 + lane;
-            const float v = __uint_as_float((unsigned)x[r]);
-            if (i < nb1) s1 += v;
-            else if (i < nbt) s2 += v;
-        }
-    }
-    s1 = wave_sum(s1);
-    s2 = wave_sum(s2);
-    if (lane == 0) {
-        mean_out[0] = ok ? s1 / ((float)b * (float)n) : __builtin_nanf("");
-        mean_out[1] = ok ? s2 / ((float)b * (float)m) : __builtin_nanf("");
-        ticket[kEpochWord] = epoch;
-    }
-}
 
 constexpr int kFwdChk = 8;  // target floats per thread loaded up front (finiteness check + rescan copy)
 
@@ -633,14 +497,17 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
         // ---- merge: thread s < QW owns query slot s
         float fbv = 0.f;
         if (tid < QW) {
-            float fb = sBest[0][tid];
-            int fc = sChunk[0][tid];
+            float vb[W];
+            int vc[W];
 #pragma unroll
-            for (int w = 1; w < W; ++w) {
-                const float v = sBest[w][tid];
-                const int c = sChunk[w][tid];
-                if (v < fb || (v == fb && c < fc)) { fb = v; fc = c; }
+            for (int w = 0; w < W; ++w) {  // every load first, then branch-free selects
+                vb[w] = sBest[w][tid];
+                vc[w] = sChunk[w][tid];
             }
+            float fb = vb[0];
+            int fc = vc[0];
+#pragma unroll
+            for (int w = 1; w < W; ++w) pcm_lexmin(fb, fc, vb[w], vc[w]);
             sFb[tid] = fb;
             sFc[tid] = fc;
             if (qbase + tid < nq) fbv = fb;
@@ -1196,14 +1063,8 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
 inline bool bad_dims(int b, int n, int m) { return b < 0 || n < 0 || m < 0; }
 
 // ---- forward variant table (tuning: tools/tune_chamfer.py) -----------------
-typedef void (*fwd_kernel_t)(const float *, const float *, int, int, int, float *, float *,
-                             int32_t *, int32_t *, int, int, float *, unsigned *, float *);
-struct FwdVariant {
-    fwd_kernel_t plain, loss, loss2, loss3;  // loss: in-kernel ticket; loss2: partials + finalize kernel;
-                                             // loss3: granules + polling workgroup
-    int waves, qpt;
-    bool sgpr;  // SGPR-stream form (else LDS-tile form)
-};
+typedef pcm_fwd_kernel_t fwd_kernel_t;
+typedef PcmFwdVariant FwdVariant;
 #define PCM_FWD_LDS(W, Q)                                                              \
     FwdVariant{chamfer_fwd_kernel<float, W, Q, kChunk, kTile, false>,                  \
                chamfer_fwd_kernel<float, W, Q, kChunk, kTile, true>, nullptr, nullptr, W, Q, false}
@@ -1222,7 +1083,12 @@ const FwdVariant kFwdVariants[] = {
     PCM_FWD_SGPR(8, 2, 16),  // 8
     PCM_FWD_SGPR(16, 2, 16), // 9
 };
-constexpr int kNumFwdVariants = sizeof(kFwdVariants) / sizeof(kFwdVariants[0]);
+constexpr int kNumBaseFwdVariants = sizeof(kFwdVariants) / sizeof(kFwdVariants[0]);
+// variant ids >= kNumBaseFwdVariants index the filtered-scan table (chamfer_filt.hip)
+inline int num_fwd_variants() { return kNumBaseFwdVariants + kPcmNumFiltVariants; }
+inline const FwdVariant &fwd_variant(int i) {
+    return i < kNumBaseFwdVariants ? kFwdVariants[i] : kPcmFiltVariants[i - kNumBaseFwdVariants];
+}
 // Default policy from tools/tune_chamfer.py on MI355X (profiles/r01): the
 // SGPR-stream form wins everywhere; 2 queries per lane and 16-candidate chunks
 // for ShapeNet-size clouds (B=32, N=M=1024: 12.7 us vs 13.5 us LDS-tile), 4
@@ -1248,8 +1114,8 @@ int launch_fwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
                float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out, void *ws, size_t ws_bytes,
                void *stream, int loss_mode = kDefaultLossMode) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
-    if (variant < 0 || variant >= kNumFwdVariants) return PCM_ERR_INVALID_ARG;
-    const FwdVariant &v = kFwdVariants[variant];
+    if (variant < 0 || variant >= num_fwd_variants()) return PCM_ERR_INVALID_ARG;
+    const FwdVariant &v = fwd_variant(variant);
     const bool loss = mean_out != nullptr;
     if (loss && (b == 0 || n == 0 || m == 0)) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
@@ -1267,7 +1133,9 @@ int launch_fwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
         ticket = (unsigned *)ws;
         partials = (float *)((char *)ws + kTicketBytes);
     }
-    if (loss && loss_mode >= 2 && !v.loss2) loss_mode = 1;
+    if (loss && loss_mode == 2 && !v.loss2) loss_mode = 1;
+    if (loss && loss_mode == 3 && !v.loss3) loss_mode = 1;
+    if (loss && loss_mode == 1 && !v.loss) loss_mode = 3;  // filtered variants: granules only
     if (loss && (loss_mode < 1 || loss_mode > 3)) return PCM_ERR_INVALID_ARG;
     fwd_kernel_t k = !loss ? v.plain : (loss_mode == 3 ? v.loss3 : (loss_mode == 2 ? v.loss2 : v.loss));
     const long long grid = blocks + ((loss && loss_mode == 3) ? 1 : 0);  // + the polling workgroup
@@ -1281,16 +1149,21 @@ int launch_fwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
 
 }  // namespace
 
-extern "C" size_t pcm_chamfer_workspace_bytes(int b, int n, int m) {
+size_t pcm_chamfer_loss_ws_offset(int b, int n, int m) {
     if (b <= 0 || n < 0 || m < 0) return kTicketBytes;
     long long most = 0;
-    for (int i = 0; i < kNumFwdVariants; ++i) {
+    for (int i = 0; i < num_fwd_variants(); ++i) {
         int n1, n2;
         long long blocks;
-        fwd_grid(kFwdVariants[i], b, n, m, n1, n2, blocks);
+        fwd_grid(fwd_variant(i), b, n, m, n1, n2, blocks);
         most = blocks > most ? blocks : most;
     }
-    return kTicketBytes + (size_t)most * sizeof(unsigned long long);  // 8-B granules (mode 3)
+    const size_t bytes = kTicketBytes + (size_t)most * sizeof(unsigned long long);  // 8-B granules (mode 3)
+    return (bytes + 127) / 128 * 128;
+}
+
+extern "C" size_t pcm_chamfer_workspace_bytes(int b, int n, int m) {
+    return pcm_chamfer_loss_ws_offset(b, n, m) + pcm_chamfer_grad_ws_bytes(b, n, m);
 }
 
 extern "C" int pcm_chamfer_forward(const float *xyz1, const float *xyz2, int b, int n, int m,
@@ -1326,7 +1199,7 @@ extern "C" int pcm_tune_chamfer_forward_loss(int variant, int loss_mode, const f
                       workspace_bytes, stream, loss_mode);
 }
 
-extern "C" int pcm_tune_num_chamfer_variants(void) { return kNumFwdVariants; }
+extern "C" int pcm_tune_num_chamfer_variants(void) { return num_fwd_variants(); }
 
 namespace {
 int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,

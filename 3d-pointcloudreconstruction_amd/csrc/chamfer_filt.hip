@@ -1,0 +1,1068 @@
+// chamfer_filt.hip -- Chamfer3D forward, filtered form, and the fused
+// loss + gradient kernel (gfx950).
+//
+// Same results as NmDistanceKernel (metric/chamfer3D/chamfer3D.cu:12-134): per
+// query the minimum of the pinned squared distance fma(dz,dz,fma(dy,dy,dx*dx))
+// over the other cloud and the LOWEST index attaining it, bit-identical.  What
+// changes is how the minimum is found:
+//
+//   1. Filter.  The workgroup stages the target cloud in LDS as
+//      (u, w) = (-2 t', |t'|^2), t' = t - c (c = mean of the workgroup's
+//      queries), and every lane evaluates a(q, t) = |t'|^2 - 2 q'.t' with
+//      three packed FMAs per two candidates (v_pk_fma_f32) -- 1.5 VALU
+//      instructions per pair plus the min fold, against 3 for the exact
+//      difference form.  Per query it keeps the best chunk (C candidates) and
+//      the best value of any OTHER chunk ("second"), one v_med3 per chunk.
+//   2. Proof.  a + |q'|^2 differs from the exact fp32 distance by at most
+//      E = 16 u (R + |q'|)^2 (u = 2^-24, R = max |t'| over the targets; the
+//      bound sums the rounding of w and the three FMAs (6u), the centering
+//      (2u) and the exact formula's own rounding (5u)).  If second - best > 2E,
+//      every candidate outside the best chunk is provably farther than the
+//      best chunk's minimum, so the exact answer (value and lowest index) lies
+//      in that chunk.
+//   3. Exact rescan of that chunk with the pinned formula on the original
+//      coordinates (from LDS when the cloud is one tile); queries whose gap is
+//      within 2E (near-ties, ~0.1 % of random queries) get a cooperative exact
+//      scan of the whole cloud by the workgroup, several queries per pass.
+//
+// Non-finite coordinates divert the workgroup to the reference-exact 512-tile
+// scan (NaN placement depends on the reference's tile boundaries).
+//
+// Fused loss + gradient (pcm_chamfer_loss_grad): the training step of
+// loss/loss.py:31-37 and its backward (chamfer3D.cu:155-195) in ONE launch.
+// Every workgroup runs its forward share, stores dist/idx write-through (sc1)
+// and its partial distance sum, drains, and adds to its batch element's
+// arrival counter; the LAST arriver of a batch element (told by the value its
+// add returned -- MI355X_MICROARCH.md visibility table, "the workgroup whose
+// add came last") computes that element's gradients with both clouds,
+// argmins and the two inverse-index counting sorts in LDS, in the reference's
+// kernel order (identical bits to pcm_chamfer_backward with constant
+// graddists), publishes the element's loss sums, and the last element's
+// finisher sums those in a fixed order.  No workgroup ever waits on another.
+#include "pcm_common.h"
+#include "pcm_internal.h"
+#include "chamfer_loss.h"
+
+namespace {
+using namespace pcm_loss;
+
+constexpr float kFiltU16 = 9.5367431640625e-07f;  // 16 u = 2^-20 (bound derivation above)
+
+// Phase stamps for tools/stamp_filt.py (profiling build only: make stamps).
+// Thread 0 of every workgroup records s_memrealtime (100 MHz) at 8 points.
+#ifdef PCM_STAMPS
+constexpr int kStampSlots = 1 << 16;
+__device__ unsigned long long g_pcm_stamps[kStampSlots * 8];
+#define PCM_STAMP(i)                                                                           \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x < kStampSlots)                                      \
+            g_pcm_stamps[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime();            \
+    } while (0)
+// the fused kernel's own 8 stamps go to the table's upper half
+#define PCM_STAMP2(i)                                                                          \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x < kStampSlots / 2)                                  \
+            g_pcm_stamps[(kStampSlots / 2 + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define PCM_STAMP(i) \
+    do {             \
+    } while (0)
+#define PCM_STAMP2(i) \
+    do {              \
+    } while (0)
+#endif
+
+// The workgroup's LDS arena: one static array per size, shared by every
+// phase of a kernel that asks for the same size.
+template <int kBytes>
+__device__ __forceinline__ unsigned char *lds_arena() {
+    __shared__ __attribute__((aligned(16))) unsigned char arena[kBytes];
+    return arena;
+}
+
+// Arena bytes of the filtered forward: the scan tile (u, w), then -- after the
+// scan, in the same bytes -- the raw target cloud (single-tile clouds) and the
+// per-wave merge arrays.
+template <int W, int QPT, int TILE>
+struct FiltLds {
+    static constexpr int kScan = 4 * TILE * 4;
+    static constexpr int kTail = 3 * TILE * 4 + 3 * W * 64 * QPT * 4;
+    static constexpr int kBytes = kScan > kTail ? kScan : kTail;
+};
+
+// forward outputs: plain stores, or write-through (sc1) when another
+// workgroup of the same launch reads them (fused loss + gradient)
+template <bool kSc1, typename Tv>
+__device__ __forceinline__ void out_st(Tv *p, Tv v) {
+    if constexpr (kSc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *p = v;
+}
+
+// One workgroup's share of the forward: queries [qbase, qbase + 64 QPT) of
+// cloud Q (nq points) against the nt points of T.  Writes D[q], I[q]; returns
+// the distance of query slot threadIdx.x (0 past nq and for threads >= 64 QPT),
+// for the loss partial.  `arena` holds FiltLds<W, QPT, TILE>::kBytes.
+template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1>
+__device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const TIn *__restrict__ T, int nq, int nt, int qbase,
+                              float *__restrict__ D, int32_t *__restrict__ I, unsigned char *arena) {
+    static_assert(C % 4 == 0 && TILE % C == 0, "tile must hold whole chunks of 4-candidate groups");
+    constexpr int QW = 64 * QPT;
+    constexpr int NT = 64 * W;
+    static_assert(NT >= QW, "one thread per query slot in the merge");
+    static_assert(TILE % NT == 0, "whole points per thread when staging");
+    constexpr int PARTS = NT / QW;
+    constexpr int CP = C / PARTS;
+    static_assert(C % PARTS == 0, "chunk must split evenly");
+    constexpr int kPer = TILE / NT;  // staged points per thread per tile
+    constexpr int kTB = 4;           // near-tie queries per cooperative pass
+    float(*sU)[TILE] = reinterpret_cast<float(*)[TILE]>(arena);  // ux, uy, uz, w (SoA)
+    float(*sT)[TILE] = reinterpret_cast<float(*)[TILE]>(arena);  // raw x, y, z (after the scan)
+    float(*sBest)[QW] = reinterpret_cast<float(*)[QW]>(arena + 3 * TILE * 4);
+    float(*sSec)[QW] = reinterpret_cast<float(*)[QW]>(arena + 3 * TILE * 4 + W * QW * 4);
+    int(*sChunk)[QW] = reinterpret_cast<int(*)[QW]>(arena + 3 * TILE * 4 + 2 * W * QW * 4);
+    __shared__ float sD[QW];  // final (distance, index) per query slot
+    __shared__ int sK[QW];
+    __shared__ int sFc[QW];   // proven chunk, or -1 (cooperative scan)
+    __shared__ float sTD[kTB * W];  // near-tie pass: per-wave partials
+    __shared__ int sTK[kTB * W];
+    __shared__ float sHD[PARTS][QW];
+    __shared__ int sHK[PARTS][QW];
+    __shared__ float sRmax[16];
+    __shared__ float sCen[4];
+    __shared__ int sList[QW];
+    __shared__ int sNList;
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // raw-tile slot of point p: rotated by its chunk index inside the chunk, so
+    // the rescan's lanes -- one query each, random chunks -- hit 32 banks, not 2
+    static_assert((C & (C - 1)) == 0, "chunk is a power of two");
+    auto slot = [](int p) { return (p & ~(C - 1)) | ((p + p / C) & (C - 1)); };
+
+    // ---- queries (every wave holds the same QW queries: lane + 64 qq)
+    float rx[QPT], ry[QPT], rz[QPT];
+    bool nonfinite = false;
+    float cx = 0.f, cy = 0.f, cz = 0.f;
+    int qcnt = 0;
+#pragma unroll
+    for (int qq = 0; qq < QPT; ++qq) {
+        // unconditional (clamped) loads: every load of the prologue -- these and
+        // the first tile's -- is in flight at once (a branch around a load makes
+        // hipcc wait for it inside the branch)
+        const int qc = min(qbase + qq * 64 + lane, nq - 1);
+        rx[qq] = pcm_ld(Q + 3 * (size_t)qc + 0);
+        ry[qq] = pcm_ld(Q + 3 * (size_t)qc + 1);
+        rz[qq] = pcm_ld(Q + 3 * (size_t)qc + 2);
+    }
+
+    float tv[kPer][3];
+    auto load_tile = [&](int t0) {
+        const int last = min(TILE, nt - t0) - 1;
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) {
+            const int p = min(tid + r * NT, last);
+#pragma unroll
+            for (int d = 0; d < 3; ++d) tv[r][d] = pcm_ld(T + 3 * (size_t)(t0 + p) + d);
+        }
+    };
+    load_tile(0);
+
+#pragma unroll
+    for (int qq = 0; qq < QPT; ++qq) {
+        if (qbase + qq * 64 + lane < nq) {
+            nonfinite |= !(pcm_finite(rx[qq]) && pcm_finite(ry[qq]) && pcm_finite(rz[qq]));
+            cx += rx[qq];
+            cy += ry[qq];
+            cz += rz[qq];
+            ++qcnt;
+        }
+    }
+
+    if (wave == 0) {
+        cx = wave_sum(cx);
+        cy = wave_sum(cy);
+        cz = wave_sum(cz);
+        float cn = (float)qcnt;
+        cn = wave_sum(cn);
+        if (lane == 0) {
+            sCen[0] = cx / cn;
+            sCen[1] = cy / cn;
+            sCen[2] = cz / cn;
+        }
+    }
+    if (tid == 0) sNList = 0;
+    __syncthreads();
+    PCM_STAMP(1);
+    const float c0 = sCen[0], c1 = sCen[1], c2 = sCen[2];
+
+    // centred queries, splatted for the packed math
+    pcm_f2 px[QPT], py[QPT], pz[QPT];
+#pragma unroll
+    for (int qq = 0; qq < QPT; ++qq) {
+        const float x = rx[qq] - c0, y = ry[qq] - c1, z = rz[qq] - c2;
+        px[qq] = pcm_f2{x, x};
+        py[qq] = pcm_f2{y, y};
+        pz[qq] = pcm_f2{z, z};
+    }
+
+    float best[QPT], sec[QPT];
+    int bchunk[QPT];
+#pragma unroll
+    for (int qq = 0; qq < QPT; ++qq) { best[qq] = PCM_INF; sec[qq] = PCM_INF; bchunk[qq] = 0; }
+    float rt2 = 0.f;  // max |t'|^2 (as computed) over the targets this thread staged
+
+    for (int t0 = 0; t0 < nt; t0 += TILE) {
+        const int cnt = min(TILE, nt - t0);
+        const int padded = (cnt + C - 1) / C * C;
+        if (t0 > 0) {
+            load_tile(t0);
+            __syncthreads();  // previous tile fully consumed
+        }
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) {
+            const int p = tid + r * NT;
+            if (p < padded) {
+                float ux = 0.f, uy = 0.f, uz = 0.f, w = PCM_INF;  // pad: a = +inf
+                if (p < cnt) {
+                    nonfinite |= !(pcm_finite(tv[r][0]) && pcm_finite(tv[r][1]) && pcm_finite(tv[r][2]));
+                    const float x = tv[r][0] - c0, y = tv[r][1] - c1, z = tv[r][2] - c2;
+                    w = __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
+                    rt2 = __builtin_fmaxf(rt2, w);
+                    ux = -2.f * x;
+                    uy = -2.f * y;
+                    uz = -2.f * z;
+                }
+                sU[0][p] = ux;
+                sU[1][p] = uy;
+                sU[2][p] = uz;
+                sU[3][p] = w;
+            }
+        }
+        __syncthreads();
+        if (t0 == 0) PCM_STAMP(2);
+
+        const int nch = padded / C;
+        const int gc0 = t0 / C;
+        // software-pipelined: the next 4-candidate group's four ds_read_b128
+        // are issued before the current group is evaluated (the last group of
+        // a chunk prefetches the wave's next chunk, or re-reads this one)
+        constexpr int G = C / 4;
+        pcm_f4 X4n, Y4n, Z4n, W4n;
+        auto fetch = [&](int cc, int g) {
+            const int o = cc * C + 4 * g;
+            X4n = *reinterpret_cast<const pcm_f4 *>(&sU[0][o]);
+            Y4n = *reinterpret_cast<const pcm_f4 *>(&sU[1][o]);
+            Z4n = *reinterpret_cast<const pcm_f4 *>(&sU[2][o]);
+            W4n = *reinterpret_cast<const pcm_f4 *>(&sU[3][o]);
+        };
+        if (wave < nch) fetch(wave, 0);
+        for (int c = wave; c < nch; c += W) {
+            float mn[QPT];
+#pragma unroll
+            for (int qq = 0; qq < QPT; ++qq) mn[qq] = PCM_INF;
+            const int cn = (c + W < nch) ? c + W : c;
+#pragma unroll
+            for (int g = 0; g < G; ++g) {
+                const pcm_f4 X4 = X4n, Y4 = Y4n, Z4 = Z4n, W4 = W4n;
+                if (g + 1 < G) fetch(c, g + 1);
+                else fetch(cn, 0);
+#pragma unroll
+                for (int qq = 0; qq < QPT; ++qq) {
+                    const pcm_f2 a01 = __builtin_elementwise_fma(
+                        px[qq], X4.xy,
+                        __builtin_elementwise_fma(py[qq], Y4.xy, __builtin_elementwise_fma(pz[qq], Z4.xy, W4.xy)));
+                    const pcm_f2 a23 = __builtin_elementwise_fma(
+                        px[qq], X4.zw,
+                        __builtin_elementwise_fma(py[qq], Y4.zw, __builtin_elementwise_fma(pz[qq], Z4.zw, W4.zw)));
+                    mn[qq] = __builtin_fminf(__builtin_fminf(mn[qq], a01.x), a01.y);
+                    mn[qq] = __builtin_fminf(__builtin_fminf(mn[qq], a23.x), a23.y);
+                }
+            }
+#pragma unroll
+            for (int qq = 0; qq < QPT; ++qq) {
+                // best <= sec always: sec' = median(mn, best, sec)
+                sec[qq] = __builtin_amdgcn_fmed3f(mn[qq], best[qq], sec[qq]);
+                if (mn[qq] < best[qq]) { best[qq] = mn[qq]; bchunk[qq] = gc0 + c; }
+            }
+        }
+    }
+
+    // ---- per-wave (best, second, chunk) to LDS (after the scan tile)
+    {
+        float v = rt2;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v = __builtin_fmaxf(v, __shfl_xor(v, o, 64));
+        if (lane == 0) sRmax[wave] = v;
+    }
+    __syncthreads();  // every wave is done reading sU
+    PCM_STAMP(3);
+    // a single-tile cloud is still in this thread's registers: park it in LDS
+    // (raw coordinates) for the exact rescans
+    const bool resident = nt <= TILE;
+    if (resident) {
+#pragma unroll
+        for (int r = 0; r < kPer; ++r) {
+            const int p = tid + r * NT;
+            if (p < nt) {
+                sT[0][slot(p)] = tv[r][0];
+                sT[1][slot(p)] = tv[r][1];
+                sT[2][slot(p)] = tv[r][2];
+            }
+        }
+    }
+#pragma unroll
+    for (int qq = 0; qq < QPT; ++qq) {
+        sBest[wave][qq * 64 + lane] = best[qq];
+        sSec[wave][qq * 64 + lane] = sec[qq];
+        sChunk[wave][qq * 64 + lane] = bchunk[qq];
+    }
+    const int any_nonfinite = __syncthreads_or(nonfinite ? 1 : 0);
+
+    float my_d = 0.f;
+    if (!any_nonfinite) {
+        // ---- merge the waves; decide per query whether the best chunk is proven
+        if (tid < QW) {
+            float vb[W], vs[W];
+            int vc[W];
+#pragma unroll
+            for (int w = 0; w < W; ++w) {  // every load first, then branch-free selects
+                vb[w] = sBest[w][tid];
+                vs[w] = sSec[w][tid];
+                vc[w] = sChunk[w][tid];
+            }
+            float fb = vb[0], fs = vs[0];
+            int fc = vc[0];
+#pragma unroll
+            for (int w = 1; w < W; ++w) {
+                const bool better = (vb[w] < fb) | ((vb[w] == fb) & (vc[w] < fc));
+                fs = __builtin_fminf(__builtin_fminf(fs, vs[w]), better ? fb : vb[w]);
+                fb = better ? vb[w] : fb;
+                fc = better ? vc[w] : fc;
+            }
+            float rmax2 = sRmax[0];
+#pragma unroll
+            for (int w = 1; w < W; ++w) rmax2 = __builtin_fmaxf(rmax2, sRmax[w]);
+            // this thread's register copy of query tid is qq = tid >> 6 (= wave)
+            float qn2 = 0.f;
+#pragma unroll
+            for (int qq = 0; qq < QPT; ++qq)
+                if (qq == wave)
+                    qn2 = __builtin_fmaf(pz[qq].x, pz[qq].x, __builtin_fmaf(py[qq].x, py[qq].x, px[qq].x * px[qq].x));
+            const float rr = __builtin_sqrtf(rmax2) + __builtin_sqrtf(qn2);
+            const float e2 = 2.f * kFiltU16 * (rr * rr) * 1.001f;
+            const bool proven = (fs - fb) > e2;  // false for NaN
+            sFc[tid] = proven ? fc : -1;
+        }
+        __syncthreads();
+        PCM_STAMP(4);
+
+        // ---- exact rescan of the proven chunk: item -> (query slot s, part)
+#pragma unroll
+        for (int r = 0; r < (QW * PARTS + NT - 1) / NT; ++r) {
+            const int item = tid + r * NT;
+            if (item >= QW * PARTS) break;
+            const int s = item % QW;
+            const int part = item / QW;
+            const int fc = sFc[s];
+            float hd = PCM_INF;
+            int hk = 0x7fffffff;
+            if (qbase + s < nq && fc >= 0) {
+                const int qsel = (item >> 6) % QPT;
+                float x = rx[0], y = ry[0], z = rz[0];
+#pragma unroll
+                for (int qq = 1; qq < QPT; ++qq)
+                    if (qsel == qq) { x = rx[qq]; y = ry[qq]; z = rz[qq]; }
+                const int k0 = fc * C + part * CP;
+                if (resident) {
+                    float tx[CP], ty[CP], tz[CP];
+#pragma unroll
+                    for (int k = 0; k < CP; ++k) {
+                        const int kk = slot(min(k0 + k, nt - 1));
+                        tx[k] = sT[0][kk];
+                        ty[k] = sT[1][kk];
+                        tz[k] = sT[2][kk];
+                    }
+#pragma unroll
+                    for (int k = 0; k < CP; ++k) {  // ascending k: strict '<' keeps the lowest
+                        const float d = pcm_sqd(tx[k] - x, ty[k] - y, tz[k] - z);
+                        const bool take = (d < hd) & (k0 + k < nt);
+                        hd = take ? d : hd;
+                        hk = take ? k0 + k : hk;
+                    }
+                } else {
+                    float tx[CP], ty[CP], tz[CP];  // all loads in flight at once
+#pragma unroll
+                    for (int k = 0; k < CP; ++k) {
+                        const int kk = min(k0 + k, nt - 1);
+                        tx[k] = pcm_ld(T + 3 * (size_t)kk);
+                        ty[k] = pcm_ld(T + 3 * (size_t)kk + 1);
+                        tz[k] = pcm_ld(T + 3 * (size_t)kk + 2);
+                    }
+#pragma unroll
+                    for (int k = 0; k < CP; ++k) {
+                        const int kk = k0 + k;
+                        const float d = pcm_sqd(tx[k] - x, ty[k] - y, tz[k] - z);
+                        const bool take = (d < hd) & (kk < nt);
+                        hd = take ? d : hd;
+                        hk = take ? kk : hk;
+                    }
+                }
+            }
+            sHD[part][s] = hd;
+            sHK[part][s] = hk;
+        }
+        __syncthreads();
+        if (tid < QW && qbase + tid < nq) {
+            if (sFc[tid] >= 0) {
+                float d = sHD[0][tid];
+                int k = sHK[0][tid];
+#pragma unroll
+                for (int p = 1; p < PARTS; ++p) {
+                    const float dv = sHD[p][tid];
+                    const int kv = sHK[p][tid];
+                    pcm_lexmin(d, k, dv, kv);
+                }
+                sD[tid] = d;
+                sK[tid] = k;
+            } else {
+                sList[atomicAdd(&sNList, 1)] = tid;
+            }
+        }
+        __syncthreads();
+        PCM_STAMP(5);
+
+        // ---- near-ties: cooperative exact scans of the whole target cloud,
+        // kTB queries per pass (one pass over the candidates serves them all)
+        const int nl = sNList;
+        for (int e0 = 0; e0 < nl; e0 += kTB) {
+            float qx[kTB], qy[kTB], qz[kTB], bd[kTB];
+            int bk[kTB];
+#pragma unroll
+            for (int j = 0; j < kTB; ++j) {
+                // query slot s lives in register copy s >> 6 of lane s & 63
+                // (every wave holds every query): broadcast it with ds_bpermute
+                const int s = sList[min(e0 + j, nl - 1)];
+                float x = rx[0], y = ry[0], z = rz[0];
+#pragma unroll
+                for (int qq = 1; qq < QPT; ++qq)
+                    if ((s >> 6) == qq) { x = rx[qq]; y = ry[qq]; z = rz[qq]; }
+                qx[j] = __shfl(x, s & 63, 64);
+                qy[j] = __shfl(y, s & 63, 64);
+                qz[j] = __shfl(z, s & 63, 64);
+                bd[j] = PCM_INF;
+                bk[j] = 0x7fffffff;
+            }
+            auto visit = [&](int k, float x, float y, float z) {
+#pragma unroll
+                for (int j = 0; j < kTB; ++j) {
+                    const float d = pcm_sqd(x - qx[j], y - qy[j], z - qz[j]);
+                    pcm_lexmin(bd[j], bk[j], d, k);
+                }
+            };
+            if (resident) {
+                for (int k = tid; k < nt; k += NT) visit(k, sT[0][slot(k)], sT[1][slot(k)], sT[2][slot(k)]);
+            } else {
+                constexpr int U = 8;  // candidates per thread with loads in flight together
+                for (int k0 = tid; k0 < nt; k0 += U * NT) {
+                    float tx[U], ty[U], tz[U];
+#pragma unroll
+                    for (int u = 0; u < U; ++u) {
+                        const int k = min(k0 + u * NT, nt - 1);
+                        tx[u] = pcm_ld(T + 3 * (size_t)k);
+                        ty[u] = pcm_ld(T + 3 * (size_t)k + 1);
+                        tz[u] = pcm_ld(T + 3 * (size_t)k + 2);
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (k0 + u * NT < nt) visit(k0 + u * NT, tx[u], ty[u], tz[u]);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < kTB; ++j) {
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    const float od = __shfl_xor(bd[j], o, 64);
+                    const int ok = __shfl_xor(bk[j], o, 64);
+                    pcm_lexmin(bd[j], bk[j], od, ok);
+                }
+            }
+            if (lane == 0) {
+#pragma unroll
+                for (int j = 0; j < kTB; ++j) {
+                    sTD[j * W + wave] = bd[j];
+                    sTK[j * W + wave] = bk[j];
+                }
+            }
+            __syncthreads();
+            if (tid < kTB && e0 + tid < nl) {
+                float d = sTD[tid * W];
+                int k = sTK[tid * W];
+                for (int w = 1; w < W; ++w) {
+                    const float dv = sTD[tid * W + w];
+                    const int kv = sTK[tid * W + w];
+                    pcm_lexmin(d, k, dv, kv);
+                }
+                const int s = sList[e0 + tid];
+                sD[s] = d;
+                sK[s] = k;
+            }
+            __syncthreads();
+        }
+        PCM_STAMP(6);
+        // ---- one store phase for the workgroup's outputs
+        if (tid < QW && qbase + tid < nq) {
+            my_d = sD[tid];
+            out_st<kSc1>(D + qbase + tid, my_d);
+            out_st<kSc1>(I + qbase + tid, (int32_t)sK[tid]);
+        }
+    } else {
+        for (int s = tid; s < QW; s += NT) {
+            const int qi = qbase + s;
+            if (qi >= nq) continue;
+            float d;
+            int idx;
+            pcm_ref_nn_scan(pcm_ld(Q + 3 * (size_t)qi + 0), pcm_ld(Q + 3 * (size_t)qi + 1),
+                            pcm_ld(Q + 3 * (size_t)qi + 2), T, nt, d, idx);
+            my_d = d;
+            out_st<kSc1>(D + qi, d);
+            out_st<kSc1>(I + qi, (int32_t)idx);
+        }
+    }
+    return my_d;
+}
+
+// ---------------------------------------------------------------------------
+// Forward kernel: direction-major workgroup numbering (as the other forward
+// forms), optional loss granule (mode 3, chamfer_loss.h).
+// ---------------------------------------------------------------------------
+// amdgpu_waves_per_eu(4): at most 128 VGPRs, so two 512-thread workgroups fit
+// a CU (left to itself hipcc spends 200+ VGPRs on the epilogue's unrolled
+// loads and halves the occupancy of the scan)
+template <typename TIn, int W, int QPT, int C, int TILE, int kLoss>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_fwd_filt_kernel(
+    const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2, int b, int n, int m,
+    float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1,
+    int32_t *__restrict__ idx2, int nblk1, int nblk2, float *__restrict__ partials,
+    unsigned *__restrict__ ticket, float *__restrict__ mean_out) {
+    static_assert(kLoss == 0 || kLoss == 3, "filtered forward publishes granules only");
+    static_assert(W <= 16, "sRed holds 16 waves");
+    constexpr int QW = 64 * QPT;
+    __shared__ float sRed[2][16];
+
+    int nprod = (int)gridDim.x;
+    unsigned epoch = 0;
+    if constexpr (kLoss == 3) {
+        nprod -= 1;
+        if ((int)blockIdx.x == nprod) {  // the grid's last workgroup polls
+            poll_loss(b * nblk1, nprod, b, n, m, reinterpret_cast<const unsigned long long *>(partials), ticket,
+                      mean_out);
+            return;
+        }
+        epoch = ticket[kEpochWord] + 1u;  // plain load: written by an earlier launch
+    }
+    PCM_STAMP(0);
+    int bid = pcm_xcd_remap((int)blockIdx.x, nprod);
+    const int slot = bid;
+    const TIn *Q, *T;
+    float *D;
+    int32_t *I;
+    int nq, nt, blk;
+    if (bid < b * nblk1) {
+        const int batch = bid / nblk1;
+        blk = bid - batch * nblk1;
+        Q = xyz1 + (size_t)batch * n * 3;
+        T = xyz2 + (size_t)batch * m * 3;
+        D = dist1 + (size_t)batch * n;
+        I = idx1 + (size_t)batch * n;
+        nq = n;
+        nt = m;
+    } else {
+        bid -= b * nblk1;
+        const int batch = bid / nblk2;
+        blk = bid - batch * nblk2;
+        Q = xyz2 + (size_t)batch * m * 3;
+        T = xyz1 + (size_t)batch * n * 3;
+        D = dist2 + (size_t)batch * m;
+        I = idx2 + (size_t)batch * m;
+        nq = m;
+        nt = n;
+    }
+    const float my_d = filt_forward<TIn, W, QPT, C, TILE, false>(Q, T, nq, nt, blk * QW, D, I,
+                                                                 lds_arena<FiltLds<W, QPT, TILE>::kBytes>());
+    if constexpr (kLoss == 3) publish_partial<3>(my_d, slot, partials, ticket, sRed, epoch);
+#ifdef PCM_STAMPS
+    if (threadIdx.x == 0 && blockIdx.x < kStampSlots)
+        g_pcm_stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// Fused loss + gradient
+// ---------------------------------------------------------------------------
+constexpr int kGradCap = 1024;   // points per cloud the per-element backward holds in LDS
+constexpr int kGradSlots = 8;    // inverse-index entries per target kept in LDS (more: ordered rescan)
+// arena of the per-element backward: both clouds (AoS floats), a count per
+// point, kGradSlots 16-bit source ids per point
+constexpr int kGradBytes = 2 * kGradCap * 12 + 2 * kGradCap * 4 + 2 * kGradCap * kGradSlots * 2;
+
+// write-through / L1-bypassing accesses of the bytes handed between
+// workgroups (MI355X_MICROARCH.md, inter-workgroup visibility: sc1 stores,
+// drained, then sc1 loads to registers by the consumer)
+__device__ __forceinline__ int32_t ld_sc1(const int32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Sum of the scatter terms -h (A[src] - s) over the <= kGradSlots sources of
+// one target (ids in tab, in arbitrary order) in ascending source index -- the
+// reference's fp32 accumulation made deterministic: selection in registers.
+__device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, float sx, float sy, float sz,
+                                            float h, const float *A, const uint16_t *tab, int cnt) {
+    int e[kGradSlots];
+#pragma unroll
+    for (int u = 0; u < kGradSlots; ++u) e[u] = u < cnt ? (int)tab[u] : 0x7fffffff;
+    int last = -1;
+    for (int t = 0; t < cnt; ++t) {
+        int nxt = 0x7fffffff;
+#pragma unroll
+        for (int u = 0; u < kGradSlots; ++u) nxt = (e[u] > last && e[u] < nxt) ? e[u] : nxt;
+        ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(A[3 * nxt], sx)));
+        ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(A[3 * nxt + 1], sy)));
+        az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(A[3 * nxt + 2], sz)));
+        last = nxt;
+    }
+}
+
+// Gradients of L = w1 sum(dist1) + w2 sum(dist2) for ONE batch element, by one
+// workgroup, clouds and inverse indices in LDS (chamfer3D.cu:155-195, g = 2 w):
+//   grad1[j] = g1 (p_j - q_I1[j])  then  - g2 (q_k - p_j) for k in S2(j) ascending
+//   grad2[k] = - g1 (p_j - q_k) for j in S1(k) ascending  then  g2 (q_k - p_I2[k])
+// S2(j) = {k : I2[k] = j}, S1(k) = {j : I1[j] = k}: each source claims a slot
+// of its target's bucket with one LDS atomic; the target's thread orders them.
+// A target with more than kGradSlots sources (random clouds: ~1 in 30k; a
+// collapsed cloud: all of them) is finished by the whole workgroup: ballots
+// list its sources in ascending order, one thread sums them.
+// Identical bits to chamfer_bwd_staged_kernel fed graddist = w.
+template <int NT>
+__device__ __forceinline__ void element_grad(const float *__restrict__ X1, const float *__restrict__ X2, int n,
+                                             int m, float w1, float w2, const int32_t *__restrict__ I1g,
+                                             const int32_t *__restrict__ I2g, float *__restrict__ G1,
+                                             float *__restrict__ G2, unsigned char *arena) {
+    constexpr int kPerT = (kGradCap + NT - 1) / NT;
+    constexpr int NW = NT / 64;
+    constexpr int kOvfCap = 2 * kGradCap / (kGradSlots + 1) + 1;  // > kGradSlots sources each
+    __shared__ int sOvf[kOvfCap];   // overflowed targets: j (cloud 1) or kGradCap + k (cloud 2)
+    __shared__ int sOvfD[kOvfCap];  // their own argmin (direct term)
+    __shared__ int sNOvf;
+    __shared__ int sWcnt[kPerT][NW];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    float *P1 = reinterpret_cast<float *>(arena);                    // [3n]
+    float *P2 = P1 + 3 * kGradCap;                                    // [3m]
+    int *cnt1 = reinterpret_cast<int *>(P2 + 3 * kGradCap);           // [n] cloud-2 sources per cloud-1 point
+    int *cnt2 = cnt1 + kGradCap;                                      // [m]
+    uint16_t *tab1 = reinterpret_cast<uint16_t *>(cnt2 + kGradCap);  // [n][slots]
+    uint16_t *tab2 = tab1 + kGradCap * kGradSlots;                    // [m][slots]
+
+    pcm_dma_to_lds(P1, X1, 12 * n, wave, NW);
+    pcm_dma_to_lds(P2, X2, 12 * m, wave, NW);
+    int i1r[kPerT], i2r[kPerT];  // argmins of this thread's points (written by other workgroups: sc1)
+#pragma unroll
+    for (int r = 0; r < kPerT; ++r) {
+        const int i = tid + r * NT;
+        i1r[r] = ld_sc1(I1g + min(i, n - 1));
+        i2r[r] = ld_sc1(I2g + min(i, m - 1));
+        if (i < n) cnt1[i] = 0;
+        if (i < m) cnt2[i] = 0;
+    }
+    if (tid == 0) sNOvf = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA of the clouds landed
+    __syncthreads();
+    PCM_STAMP2(3);
+#pragma unroll
+    for (int r = 0; r < kPerT; ++r) {
+        const int i = tid + r * NT;
+        if (i < m) {  // cloud-2 point i scatters onto cloud-1 point i2r
+            const int slot = atomicAdd(&cnt1[i2r[r]], 1);
+            if (slot < kGradSlots) tab1[i2r[r] * kGradSlots + slot] = (uint16_t)i;
+        }
+        if (i < n) {  // cloud-1 point i scatters onto cloud-2 point i1r
+            const int slot = atomicAdd(&cnt2[i1r[r]], 1);
+            if (slot < kGradSlots) tab2[i1r[r] * kGradSlots + slot] = (uint16_t)i;
+        }
+    }
+    __syncthreads();
+    PCM_STAMP2(4);
+
+    const float g1 = __fmul_rn(w1, 2.f), g2 = __fmul_rn(w2, 2.f);
+#pragma unroll
+    for (int r = 0; r < kPerT; ++r) {
+        const int j = tid + r * NT;
+        if (j < n) {  // cloud 1: direct term first (chamfer3D.cu:184), then the cloud-2 scatters
+            const int c = cnt1[j];
+            if (c <= kGradSlots) {
+                const float sx = P1[3 * j], sy = P1[3 * j + 1], sz = P1[3 * j + 2];
+                const int k = i1r[r];
+                float ax = __fadd_rn(0.f, __fmul_rn(g1, __fsub_rn(sx, P2[3 * k])));
+                float ay = __fadd_rn(0.f, __fmul_rn(g1, __fsub_rn(sy, P2[3 * k + 1])));
+                float az = __fadd_rn(0.f, __fmul_rn(g1, __fsub_rn(sz, P2[3 * k + 2])));
+                scatter_sum(ax, ay, az, sx, sy, sz, g2, P2, tab1 + j * kGradSlots, c);
+                G1[3 * j] = ax;
+                G1[3 * j + 1] = ay;
+                G1[3 * j + 2] = az;
+            } else {
+                const int e = atomicAdd(&sNOvf, 1);
+                sOvf[e] = j;
+                sOvfD[e] = i1r[r];
+            }
+        }
+        if (j < m) {  // cloud 2: cloud-1 scatters first (kernel 1 ran before kernel 2), then direct
+            const int c = cnt2[j];
+            if (c <= kGradSlots) {
+                const float sx = P2[3 * j], sy = P2[3 * j + 1], sz = P2[3 * j + 2];
+                float ax = 0.f, ay = 0.f, az = 0.f;
+                scatter_sum(ax, ay, az, sx, sy, sz, g1, P1, tab2 + j * kGradSlots, c);
+                const int k = i2r[r];
+                ax = __fadd_rn(ax, __fmul_rn(g2, __fsub_rn(sx, P1[3 * k])));
+                ay = __fadd_rn(ay, __fmul_rn(g2, __fsub_rn(sy, P1[3 * k + 1])));
+                az = __fadd_rn(az, __fmul_rn(g2, __fsub_rn(sz, P1[3 * k + 2])));
+                G2[3 * j] = ax;
+                G2[3 * j + 1] = ay;
+                G2[3 * j + 2] = az;
+            } else {
+                const int e = atomicAdd(&sNOvf, 1);
+                sOvf[e] = kGradCap + j;
+                sOvfD[e] = i2r[r];
+            }
+        }
+    }
+    __syncthreads();
+
+    // ---- overflowed buckets: ascending source list by ballots, one summing thread
+    const int nov = sNOvf;
+    int *lst = reinterpret_cast<int *>(tab1);  // the bucket tables are dead now
+    for (int e = 0; e < nov; ++e) {
+        const int code = sOvf[e];
+        const bool c1 = code < kGradCap;  // target in cloud 1 (sources: cloud-2 points)
+        const int j = c1 ? code : code - kGradCap;
+        unsigned long long bal[kPerT];
+#pragma unroll
+        for (int r = 0; r < kPerT; ++r) {
+            const int i = tid + r * NT;
+            const bool match = c1 ? (i < m && i2r[r] == j) : (i < n && i1r[r] == j);
+            bal[r] = __ballot(match);
+            if (lane == 0) sWcnt[r][wave] = __popcll(bal[r]);
+        }
+        __syncthreads();
+        int total = 0;
+#pragma unroll
+        for (int r = 0; r < kPerT; ++r) {
+            int base = total;
+            for (int w = 0; w < NW; ++w) {
+                base += (w < wave) ? sWcnt[r][w] : 0;
+                total += sWcnt[r][w];
+            }
+            if ((bal[r] >> lane) & 1ull) lst[base + __popcll(bal[r] & ((1ull << lane) - 1ull))] = tid + r * NT;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            const float *S = c1 ? P1 : P2, *A = c1 ? P2 : P1;
+            const float sx = S[3 * j], sy = S[3 * j + 1], sz = S[3 * j + 2];
+            const float gs = c1 ? g1 : g2, h = c1 ? g2 : g1;
+            const int k = sOvfD[e];
+            const float dx = __fmul_rn(gs, __fsub_rn(sx, A[3 * k]));
+            const float dy = __fmul_rn(gs, __fsub_rn(sy, A[3 * k + 1]));
+            const float dz = __fmul_rn(gs, __fsub_rn(sz, A[3 * k + 2]));
+            float ax = 0.f, ay = 0.f, az = 0.f;
+            if (c1) {
+                ax = __fadd_rn(ax, dx);
+                ay = __fadd_rn(ay, dy);
+                az = __fadd_rn(az, dz);
+            }
+            for (int q = 0; q < total; ++q) {
+                const int src = lst[q];
+                ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(A[3 * src], sx)));
+                ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(A[3 * src + 1], sy)));
+                az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(A[3 * src + 2], sz)));
+            }
+            if (!c1) {
+                ax = __fadd_rn(ax, dx);
+                ay = __fadd_rn(ay, dy);
+                az = __fadd_rn(az, dz);
+            }
+            float *G = c1 ? G1 : G2;
+            G[3 * j] = ax;
+            G[3 * j + 1] = ay;
+            G[3 * j + 2] = az;
+        }
+        __syncthreads();
+    }
+}
+
+// Workspace of the fused kernel (after pcm_chamfer_forward_loss's bytes, so one
+// zero-filled buffer serves both): the loss epoch word, an arrival counter per
+// batch element (left zeroed), a partial sum per workgroup, and two 8-byte
+// {epoch, sum} granules per batch element (sum of dist1, sum of dist2).
+struct GradWs {
+    unsigned *epoch, *bcount;
+    float *wpart;
+    unsigned long long *gran;
+};
+inline size_t grad_ws_bytes(int b, long long blocks) {
+    const size_t c = ((size_t)b * 4 + 127) / 128 * 128, p = ((size_t)blocks * 4 + 127) / 128 * 128;
+    return 128 + c + p + (size_t)b * 16;
+}
+inline GradWs grad_ws(void *base, int b, long long blocks) {
+    char *p = (char *)base;
+    GradWs w;
+    w.epoch = (unsigned *)p;
+    w.bcount = (unsigned *)(p + 128);
+    w.wpart = (float *)(p + 128 + ((size_t)b * 4 + 127) / 128 * 128);
+    w.gran = (unsigned long long *)((char *)w.wpart + ((size_t)blocks * 4 + 127) / 128 * 128);
+    return w;
+}
+
+// the grid's last workgroup: sweep the 2b granules until all carry this
+// call's epoch (bounded: NaN means on timeout), fixed-order sums, advance the
+// epoch (chamfer_loss.h poll_loss, with the granules per batch element)
+__device__ __forceinline__ void poll_grad_loss(int b, int n, int m, const GradWs &ws, float *__restrict__ mean_out) {
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    const unsigned epoch = ws.epoch[0] + 1u;
+    float s1 = 0.f, s2 = 0.f;
+    bool ok = true;
+    for (int base = 0; base < 2 * b && ok; base += 64) {
+        const int i = base + lane;
+        unsigned long long x = (unsigned long long)epoch << 32;
+        for (unsigned spins = 0;; ++spins) {
+            if (i < 2 * b) x = __hip_atomic_load(ws.gran + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__all((unsigned)(x >> 32) == epoch)) break;
+            if (spins >= kPollMaxSpins) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const float v = __uint_as_float((unsigned)x);
+        if (i < 2 * b) {
+            if (i & 1) s2 += v;
+            else s1 += v;
+        }
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+        const float m1 = ok ? s1 / ((float)b * (float)n) : __builtin_nanf("");
+        const float m2 = ok ? s2 / ((float)b * (float)m) : __builtin_nanf("");
+        mean_out[0] = m1;
+        mean_out[1] = m2;
+        mean_out[2] = m1 + m2;
+        ws.epoch[0] = epoch;
+    }
+}
+
+template <int W, int QPT, int C, int TILE>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
+    float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
+    float *__restrict__ mean_out, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
+    GradWs ws) {
+    constexpr int QW = 64 * QPT;
+    constexpr int NT = 64 * W;
+    constexpr int kFwd = FiltLds<W, QPT, TILE>::kBytes;
+    constexpr int kArena = kFwd > kGradBytes ? kFwd : kGradBytes;
+    __shared__ float sRed[16];
+    __shared__ int sFlag;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
+    unsigned char *arena = lds_arena<kArena>();
+    const int nprod = (int)gridDim.x - 1;
+    if ((int)blockIdx.x == nprod) {
+        PCM_STAMP2(5);
+        poll_grad_loss(b, n, m, ws, mean_out);
+        PCM_STAMP2(6);
+        return;
+    }
+    PCM_STAMP2(0);
+
+    // batch-major numbering: one batch element's workgroups share an XCD
+    const int per = nblk1 + nblk2;
+    const int bid = pcm_xcd_remap((int)blockIdx.x, nprod);
+    const int batch = bid / per;
+    const int r = bid - batch * per;
+    const bool first = r < nblk1;
+    const float *X1 = xyz1 + (size_t)batch * n * 3;
+    const float *X2 = xyz2 + (size_t)batch * m * 3;
+    const float my_d = filt_forward<float, W, QPT, C, TILE, true>(
+        first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, (first ? r : r - nblk1) * QW,
+        first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
+        first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena);
+    PCM_STAMP2(1);
+
+    // ---- workgroup partial (fixed order), write-through; drain; arrive
+    const float s = wave_sum(my_d);
+    if (lane == 0) sRed[wave] = s;
+    __syncthreads();
+    if (tid == 0) {
+        float t = 0.f;
+        for (int w = 0; w < W; ++w) t += sRed[w];
+        __hip_atomic_store(ws.wpart + bid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    __syncthreads();
+    if (tid == 0) {
+        const unsigned old =
+            __hip_atomic_fetch_add(ws.bcount + batch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        sFlag = (old == (unsigned)per - 1);
+    }
+    __syncthreads();
+    PCM_STAMP2(2);
+    if (!sFlag) return;
+
+    // ---- the batch element's last arriver: its loss sums (wave 0; the
+    // granule is the flag, nothing waits on it here) and its gradients
+    if (tid == 0) __hip_atomic_store(ws.bcount + batch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wave == 0) {
+        float v1 = 0.f, v2 = 0.f;
+        for (int i = lane; i < per; i += 64) {
+            const float v = ld_sc1(ws.wpart + (size_t)batch * per + i);
+            if (i < nblk1) v1 += v;
+            else v2 += v;
+        }
+        v1 = wave_sum(v1);
+        v2 = wave_sum(v2);
+        if (lane < 2) {
+            const unsigned long long tag = (unsigned long long)(ws.epoch[0] + 1u) << 32;
+            __hip_atomic_store(ws.gran + 2 * batch + lane, tag | __float_as_uint(lane ? v2 : v1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    element_grad<NT>(X1, X2, n, m, w1, w2, idx1 + (size_t)batch * n, idx2 + (size_t)batch * m,
+                     grad1 + (size_t)batch * n * 3, grad2 + (size_t)batch * m * 3, arena);
+    PCM_STAMP2(7);
+}
+
+}  // namespace
+
+#define PCM_FWD_FILT(W, Q, C, TILE)                                                                   \
+    PcmFwdVariant{chamfer_fwd_filt_kernel<float, W, Q, C, TILE, 0>, nullptr, nullptr,                \
+                  chamfer_fwd_filt_kernel<float, W, Q, C, TILE, 3>, W, Q, false}
+const PcmFwdVariant kPcmFiltVariants[] = {
+    PCM_FWD_FILT(8, 2, 16, 2048),   // base + 0
+    PCM_FWD_FILT(8, 4, 16, 2048),   // base + 1
+    PCM_FWD_FILT(16, 4, 16, 2048),  // base + 2
+    PCM_FWD_FILT(8, 4, 32, 2048),   // base + 3
+    PCM_FWD_FILT(4, 4, 16, 2048),   // base + 4
+    PCM_FWD_FILT(16, 2, 16, 2048),  // base + 5
+    PCM_FWD_FILT(8, 4, 16, 4096),   // base + 6
+    PCM_FWD_FILT(8, 8, 16, 2048),   // base + 7
+};
+const int kPcmNumFiltVariants = sizeof(kPcmFiltVariants) / sizeof(kPcmFiltVariants[0]);
+
+// ---- fused loss + gradient: variants (tools/tune_chamfer.py) and entry points
+namespace {
+typedef void (*grad_kernel_t)(const float *, const float *, int, int, int, float, float, float *, float *,
+                              int32_t *, int32_t *, float *, float *, float *, int, int, GradWs);
+struct GradVariant {
+    grad_kernel_t k;
+    int waves, qpt;
+};
+const GradVariant kGradVariants[] = {
+    {chamfer_loss_grad_kernel<8, 2, 16, 1024>, 8, 2},  // 0
+    {chamfer_loss_grad_kernel<8, 4, 16, 1024>, 8, 4},  // 1
+    {chamfer_loss_grad_kernel<4, 2, 16, 1024>, 4, 2},  // 2
+};
+constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
+
+long long grad_blocks(const GradVariant &v, int b, int n, int m, int &nblk1, int &nblk2) {
+    const int QW = 64 * v.qpt;
+    nblk1 = (n + QW - 1) / QW;
+    nblk2 = (m + QW - 1) / QW;
+    return (long long)b * (nblk1 + nblk2);
+}
+
+long long grad_blocks_max(int b, int n, int m) {
+    long long most = 0;
+    for (int i = 0; i < kNumGradVariants; ++i) {
+        int n1, n2;
+        const long long bl = grad_blocks(kGradVariants[i], b, n, m, n1, n2);
+        most = bl > most ? bl : most;
+    }
+    return most;
+}
+
+int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, int n, int m, float w1, float w2,
+                     float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out, float *grad1,
+                     float *grad2, void *workspace, size_t workspace_bytes, void *stream) {
+    if (b <= 0 || n <= 0 || m <= 0) return PCM_ERR_INVALID_ARG;
+    if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
+    if (variant < 0 || variant >= kNumGradVariants) return PCM_ERR_INVALID_ARG;
+    if (!xyz1 || !xyz2 || !dist1 || !dist2 || !idx1 || !idx2 || !mean_out || !grad1 || !grad2 || !workspace)
+        return PCM_ERR_INVALID_ARG;
+    const GradVariant &v = kGradVariants[variant];
+    int nblk1, nblk2;
+    const long long blocks = grad_blocks(v, b, n, m, nblk1, nblk2);
+    if (blocks > 0x7ffffffeLL) return PCM_ERR_UNSUPPORTED;
+    const size_t off = pcm_chamfer_loss_ws_offset(b, n, m);
+    if (workspace_bytes < off + grad_ws_bytes(b, grad_blocks_max(b, n, m))) return PCM_ERR_WORKSPACE;
+    const GradWs ws = grad_ws((char *)workspace + off, b, blocks);
+    // + the polling workgroup (the grid's last)
+    hipLaunchKernelGGL(v.k, dim3((unsigned)blocks + 1), dim3(64 * v.waves), 0, (hipStream_t)stream, xyz1, xyz2, b,
+                       n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out, grad1, grad2, nblk1, nblk2, ws);
+    return pcm_launch_status();
+}
+}  // namespace
+
+size_t pcm_chamfer_grad_ws_bytes(int b, int n, int m) {
+    if (b <= 0 || n <= 0 || m <= 0) return 0;
+    return grad_ws_bytes(b, grad_blocks_max(b, n, m));
+}
+
+extern "C" int pcm_chamfer_loss_grad(const float *xyz1, const float *xyz2, int b, int n, int m, float w1,
+                                     float w2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                                     float *mean_out, float *gradxyz1, float *gradxyz2, void *workspace,
+                                     size_t workspace_bytes, void *stream) {
+    return launch_loss_grad(0, xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out, gradxyz1,
+                            gradxyz2, workspace, workspace_bytes, stream);
+}
+
+extern "C" int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
+                                          float w1, float w2, float *dist1, float *dist2, int32_t *idx1,
+                                          int32_t *idx2, float *mean_out, float *gradxyz1, float *gradxyz2,
+                                          void *workspace, size_t workspace_bytes, void *stream) {
+    return launch_loss_grad(variant, xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out, gradxyz1,
+                            gradxyz2, workspace, workspace_bytes, stream);
+}
+
+extern "C" int pcm_tune_num_chamfer_loss_grad_variants(void) { return kNumGradVariants; }
+
+#ifdef PCM_STAMPS
+extern "C" int pcm_tune_read_stamps(unsigned long long *host, int nblocks) {
+    if (nblocks > kStampSlots) nblocks = kStampSlots;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pcm_stamps), (size_t)nblocks * 8 * 8, 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? nblocks : -1;
+}
+#endif
+
+#ifdef PCM_STAMPS
+// Core clock estimate (profiling build): every workgroup spins ~20 us of
+// dependent VALU work between two (s_memtime, s_memrealtime) pairs.
+__global__ void pcm_clock_kernel(unsigned long long *out, int iters) {
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    float v = (float)threadIdx.x;
+    for (int i = 0; i < iters; ++i) v = __builtin_fmaf(v, 0.999f, 0.5f);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        out[4 * blockIdx.x + 0] = t1 - t0;
+        out[4 * blockIdx.x + 1] = r1 - r0;
+        out[4 * blockIdx.x + 2] = __float_as_uint(v);
+    }
+}
+extern "C" int pcm_tune_clock(unsigned long long *dev_out, int blocks, int iters, void *stream) {
+    hipLaunchKernelGGL(pcm_clock_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, dev_out, iters);
+    return pcm_launch_status();
+}
+#endif

@@ -23,6 +23,15 @@ __device__ __forceinline__ pcm_f2 pcm_sqd2(pcm_f2 dx, pcm_f2 dy, pcm_f2 dz) {
     return __builtin_elementwise_fma(dz, dz, __builtin_elementwise_fma(dy, dy, dx * dx));
 }
 
+// (d, k) <- lexicographic min of (d, k) and (dv, kv), branch-free: bitwise
+// ops instead of || / && keep hipcc from turning the update into exec-mask
+// branches that serialise the surrounding loads
+__device__ __forceinline__ void pcm_lexmin(float &d, int &k, float dv, int kv) {
+    const bool take = (dv < d) | ((dv == d) & (kv < k));
+    d = take ? dv : d;
+    k = take ? kv : k;
+}
+
 __device__ __forceinline__ bool pcm_finite(float v) {
     return __builtin_isfinite(v);
 }

@@ -16,6 +16,12 @@ int pcm_tune_chamfer_backward(int variant, const float *xyz1, const float *xyz2,
 int pcm_tune_chamfer_forward_loss(int variant, int loss_mode, const float *xyz1, const float *xyz2, int b,
                                   int n, int m, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                   float *mean_out, void *workspace, size_t workspace_bytes, void *stream);
+int pcm_tune_num_chamfer_loss_grad_variants(void);
+int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, int n, int m, float w1,
+                               float w2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out,
+                               float *gradxyz1, float *gradxyz2, void *workspace, size_t workspace_bytes,
+                               void *stream);
+int pcm_tune_read_stamps(unsigned long long *host, int nblocks);  // profiling build only (make stamps)
 int pcm_tune_num_chamfer_f16_variants(void);
 int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
                                  float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, void *stream);

@@ -26,7 +26,12 @@ EXPORTED = (
     "pcm_chamfer_workspace_bytes", "pcm_chamfer_forward_loss",
     "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward",
     "pcm_chamfer_forward_f16", "pcm_chamfer_backward_f16",
+    "pcm_chamfer_loss_grad",
 )
+
+# largest cloud (points per batch element) pcm_chamfer_loss_grad runs as one
+# launch (csrc/chamfer_filt.hip kGradCap); larger clouds take forward + backward
+LOSS_GRAD_MAX_POINTS = 1024
 
 
 class PcmError(RuntimeError):
@@ -81,6 +86,13 @@ def load_library():
     L.pcm_emd_forward.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, vp, cs, vp]
     L.pcm_emd_backward.restype = ci
     L.pcm_emd_backward.argtypes = [vp, vp, ci, ci, vp, vp, vp, vp]
+    L.pcm_chamfer_loss_grad.restype = ci
+    L.pcm_chamfer_loss_grad.argtypes = [vp, vp, ci, ci, ci, cf, cf, vp, vp, vp, vp, vp, vp, vp, vp, cs, vp]
+    L.pcm_tune_chamfer_loss_grad.restype = ci
+    L.pcm_tune_chamfer_loss_grad.argtypes = [ci, vp, vp, ci, ci, ci, cf, cf, vp, vp, vp, vp, vp, vp, vp, vp, cs,
+                                             vp]
+    L.pcm_tune_num_chamfer_loss_grad_variants.restype = ci
+    L.pcm_tune_num_chamfer_loss_grad_variants.argtypes = []
     _lib = L
     return L
 
@@ -175,6 +187,39 @@ def chamfer_forward_loss(xyz1, xyz2, dist1, dist2, idx1, idx2, mean_out, workspa
             _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
             _ptr(mean_out), _ptr(workspace), workspace.numel(), _stream(dev)),
             "pcm_chamfer_forward_loss")
+
+
+def loss_grad_supported(xyz1, xyz2) -> bool:
+    """Whether pcm_chamfer_loss_grad takes these clouds in one launch."""
+    return (xyz1.dtype == torch.float32 and xyz2.dtype == torch.float32 and xyz1.shape[0] > 0
+            and 0 < xyz1.shape[1] <= LOSS_GRAD_MAX_POINTS and 0 < xyz2.shape[1] <= LOSS_GRAD_MAX_POINTS)
+
+
+def chamfer_loss_grad(xyz1, xyz2, w1, w2, dist1, dist2, idx1, idx2, mean_out, gradxyz1, gradxyz2,
+                      workspace=None, variant=None) -> None:
+    """pcm_chamfer_loss_grad: the forward (dist/idx), mean_out[0:3] = (mean(dist1),
+    mean(dist2), their sum), and the gradients of w1*sum(dist1) + w2*sum(dist2)
+    w.r.t. both clouds, in one launch (float32, n, m <= LOSS_GRAD_MAX_POINTS)."""
+    dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2, mean_out, gradxyz1, gradxyz2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    if mean_out.numel() < 3:
+        raise ValueError("mean_out needs 3 floats")
+    if workspace is None:
+        workspace = chamfer_workspace(dev, b, n, m)
+    L = load_library()
+    with torch.cuda.device(dev):
+        args = (_ptr(xyz1), _ptr(xyz2), b, n, m, float(w1), float(w2), _ptr(dist1), _ptr(dist2), _ptr(idx1),
+                _ptr(idx2), _ptr(mean_out), _ptr(gradxyz1), _ptr(gradxyz2), _ptr(workspace), workspace.numel(),
+                _stream(dev))
+        if variant is None:
+            _check(L.pcm_chamfer_loss_grad(*args), "pcm_chamfer_loss_grad")
+        else:
+            _check(L.pcm_tune_chamfer_loss_grad(int(variant), *args), "pcm_tune_chamfer_loss_grad")
+
+
+def tune_num_chamfer_loss_grad_variants() -> int:
+    return int(load_library().pcm_tune_num_chamfer_loss_grad_variants())
 
 
 def tune_chamfer_forward(variant, xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:

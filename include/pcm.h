@@ -86,6 +86,26 @@ int pcm_chamfer_forward_loss(const float *xyz1, const float *xyz2, int b, int n,
                              void *stream);
 
 /*
+ * Fused Chamfer loss + gradient (extension): the training step of
+ * loss/loss.py:31-37 (chamfer_3DDist forward + torch.mean(dist1) +
+ * torch.mean(dist2)) and its backward (chamfer3D.cu:155-195) in ONE launch:
+ *   - everything pcm_chamfer_forward does (dist1, dist2, idx1, idx2);
+ *   - mean_out[0] = mean(dist1), mean_out[1] = mean(dist2),
+ *     mean_out[2] = mean_out[0] + mean_out[1]        (device float[3]);
+ *   - gradxyz1/gradxyz2 = gradients of  w1*sum(dist1) + w2*sum(dist2),
+ *     bit-identical to pcm_chamfer_backward with graddist1 = w1 and
+ *     graddist2 = w2 everywhere (w1 = 1/(b*n), w2 = 1/(b*m) for the mean loss).
+ * Deterministic.  Needs b > 0, 0 < n, m <= 1024 (else PCM_ERR_UNSUPPORTED:
+ * use pcm_chamfer_forward_loss + pcm_chamfer_backward) and the zero-filled
+ * workspace of pcm_chamfer_workspace_bytes(b, n, m) (the same buffer serves
+ * pcm_chamfer_forward_loss; stream-ordered reuse only).
+ */
+int pcm_chamfer_loss_grad(const float *xyz1, const float *xyz2, int b, int n, int m, float w1, float w2,
+                          float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out,
+                          float *gradxyz1, float *gradxyz2, void *workspace, size_t workspace_bytes,
+                          void *stream);
+
+/*
  * Chamfer backward (chamfer3D.cu:155-195).  With g = 2*graddist:
  *   gradxyz1[j] = g1[j](xyz1[j]-xyz2[idx1[j]]) - sum_{k: idx2[k]=j} g2[k](xyz2[k]-xyz1[j])
  *   gradxyz2[k] = g2[k](xyz2[k]-xyz1[idx2[k]]) - sum_{j: idx1[j]=k} g1[j](xyz1[j]-xyz2[k])

@@ -366,3 +366,203 @@ def test_all_f16_variants_bit_identical(cuda, oracle):
         pcm_hip.tune_chamfer_forward_f16(v, x1, x2, d1, d2, i1, i2)
         torch.cuda.synchronize()
         _assert_fwd_equal((d1.cpu().numpy(), d2.cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()), ref)
+
+
+def _stress_clouds(kind, b=2, n=1200, m=900, seed=81):
+    g = torch.Generator().manual_seed(seed)
+    a = torch.rand(b, n, 3, generator=g)
+    c = torch.rand(b, m, 3, generator=g)
+    if kind == "grid":          # coordinates on a 1/8 grid: exact ties everywhere
+        a, c = torch.floor(a * 8) / 8, torch.floor(c * 8) / 8
+    elif kind == "near_ties":   # every target has a twin 1 ulp-ish away
+        c[:, m // 2:] = c[:, : m - m // 2] + 1e-7
+    elif kind == "offset":      # far from the origin: wide filter bound
+        a, c = a + 100.0, c + 100.0
+    elif kind == "tiny":        # very small extent
+        a, c = a * 1e-3, c * 1e-3
+    elif kind == "huge":        # squared norms near the fp32 limit
+        a, c = a * 1e18, c * 1e18
+    elif kind == "dup_queries":
+        a[:, 1::2] = a[:, 0::2][:, : n // 2]
+    return a, c
+
+
+@pytest.mark.parametrize("kind", ["grid", "near_ties", "offset", "tiny", "huge", "dup_queries"])
+def test_all_forward_variants_stress(cuda, oracle, kind):
+    # the filtered variants prove their chunk choice with an error bound and
+    # fall back to exact scans on near-ties: results must stay bit-identical
+    import pcm_hip
+    a, c = _stress_clouds(kind)
+    b, n, m = a.shape[0], a.shape[1], c.shape[1]
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    x1, x2 = a.to(cuda), c.to(cuda)
+    for v in range(pcm_hip.tune_num_chamfer_variants()):
+        d1 = torch.empty(b, n, device=cuda)
+        d2 = torch.empty(b, m, device=cuda)
+        i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+        i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+        pcm_hip.tune_chamfer_forward(v, x1, x2, d1, d2, i1, i2)
+        torch.cuda.synchronize()
+        _assert_fwd_equal((d1.cpu().numpy(), d2.cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()), ref)
+
+
+def test_all_forward_variants_fused_loss(cuda, oracle):
+    import pcm_hip
+    b, n, m = 4, 1500, 700
+    a, c = _clouds(91, b, n, m)
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    r = np.array([ref[0].astype(np.float64).mean(), ref[1].astype(np.float64).mean()])
+    x1, x2 = a.to(cuda), c.to(cuda)
+    ws = torch.zeros(pcm_hip.chamfer_workspace(cuda, b, n, m).numel(), dtype=torch.uint8, device=cuda)
+    for v in range(pcm_hip.tune_num_chamfer_variants()):
+        d1 = torch.empty(b, n, device=cuda)
+        d2 = torch.empty(b, m, device=cuda)
+        i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+        i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+        mo = torch.zeros(2, 2, device=cuda)
+        for k in range(2):
+            pcm_hip.tune_chamfer_forward_loss(v, 3, x1, x2, d1, d2, i1, i2, mo[k], ws)
+        torch.cuda.synchronize()
+        _assert_fwd_equal((d1.cpu().numpy(), d2.cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()), ref)
+        mo = mo.cpu()
+        assert torch.equal(mo[0], mo[1])
+        np.testing.assert_allclose(mo[0].numpy(), r, rtol=2e-6)
+
+
+def _loss_grad(cuda, a, c, variant=None, ws=None, reps=1):
+    import pcm_hip
+    b, n, m = a.shape[0], a.shape[1], c.shape[1]
+    x1, x2 = a.to(cuda), c.to(cuda)
+    out = dict(d1=torch.empty(b, n, device=cuda), d2=torch.empty(b, m, device=cuda),
+               i1=torch.empty(b, n, dtype=torch.int32, device=cuda),
+               i2=torch.empty(b, m, dtype=torch.int32, device=cuda),
+               g1=torch.full((b, n, 3), float("nan"), device=cuda),
+               g2=torch.full((b, m, 3), float("nan"), device=cuda))
+    means = []
+    w1, w2 = np.float32(1.0 / (b * n)), np.float32(1.0 / (b * m))
+    for _ in range(reps):
+        mo = torch.full((3,), float("nan"), device=cuda)
+        pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, out["d1"], out["d2"], out["i1"], out["i2"], mo,
+                                  out["g1"], out["g2"], workspace=ws, variant=variant)
+        means.append(mo)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in out.items()}, [x.cpu().numpy() for x in means], (w1, w2)
+
+
+@pytest.mark.parametrize("b,n,m,seed,dist", [
+    (32, 1024, 1024, 101, "uniform"),  # BASELINE config 2
+    (4, 256, 256, 102, "uniform"),     # BASELINE config 1
+    (3, 1000, 700, 103, "normal"),
+    (2, 1, 5, 104, "uniform"),
+    (5, 257, 1024, 105, "uniform"),
+    (1, 1024, 3, 106, "normal"),
+])
+def test_loss_grad_matches_oracle(cuda, oracle, b, n, m, seed, dist):
+    # one launch: forward + means + gradients of w1*sum(d1) + w2*sum(d2), identical
+    # to the oracle forward and the oracle backward fed graddist = w
+    import pcm_hip
+    a, c = _clouds(seed, b, n, m, dist)
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    r = np.array([ref[0].astype(np.float64).mean(), ref[1].astype(np.float64).mean()])
+    for v in range(pcm_hip.tune_num_chamfer_loss_grad_variants()):
+        o, means, (w1, w2) = _loss_grad(cuda, a, c, variant=v, reps=3)
+        _assert_fwd_equal((o["d1"], o["d2"], o["i1"], o["i2"]), ref)
+        gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), w1, np.float32),
+                                           np.full((b, m), w2, np.float32), ref[2], ref[3])
+        np.testing.assert_array_equal(o["g1"].view(np.int32), gr1.view(np.int32))
+        np.testing.assert_array_equal(o["g2"].view(np.int32), gr2.view(np.int32))
+        assert all(np.array_equal(means[0].view(np.int32), x.view(np.int32)) for x in means)
+        np.testing.assert_allclose(means[0][:2], r, rtol=2e-6)
+        assert means[0][2] == np.float32(means[0][0] + means[0][1])
+
+
+@pytest.mark.parametrize("kind", ["grid", "near_ties", "dup_queries", "offset"])
+def test_loss_grad_stress(cuda, oracle, kind):
+    a, c = _stress_clouds(kind, b=3, n=1000, m=900)
+    b, n, m = a.shape[0], a.shape[1], c.shape[1]
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    o, _, (w1, w2) = _loss_grad(cuda, a, c)
+    _assert_fwd_equal((o["d1"], o["d2"], o["i1"], o["i2"]), ref)
+    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), w1, np.float32),
+                                       np.full((b, m), w2, np.float32), ref[2], ref[3])
+    np.testing.assert_array_equal(o["g1"].view(np.int32), gr1.view(np.int32))
+    np.testing.assert_array_equal(o["g2"].view(np.int32), gr2.view(np.int32))
+
+
+def test_loss_grad_collapsed_cloud(cuda, oracle):
+    # every query of one direction hits the same target: one bucket of 1024
+    # sources (parallel ranking inside the bucket)
+    b, n, m = 2, 1024, 1024
+    a, c = _clouds(111, b, n, m)
+    c[:, :, :] = c[:, :1, :]
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    o, _, (w1, w2) = _loss_grad(cuda, a, c)
+    _assert_fwd_equal((o["d1"], o["d2"], o["i1"], o["i2"]), ref)
+    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), w1, np.float32),
+                                       np.full((b, m), w2, np.float32), ref[2], ref[3])
+    np.testing.assert_array_equal(o["g1"].view(np.int32), gr1.view(np.int32))
+    np.testing.assert_array_equal(o["g2"].view(np.int32), gr2.view(np.int32))
+
+
+def test_loss_grad_nonfinite(cuda, oracle):
+    a, c = _clouds(112, 2, 600, 500)
+    a[0, 17, 1] = float("nan")
+    c[1, 3, 0] = float("inf")
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    o, _, _ = _loss_grad(cuda, a, c)
+    np.testing.assert_array_equal(o["i1"], ref[2])
+    np.testing.assert_array_equal(o["i2"], ref[3])
+    np.testing.assert_array_equal(o["d1"], ref[0])
+    np.testing.assert_array_equal(o["d2"], ref[1])
+
+
+def test_loss_grad_graph_replay_and_shared_workspace(cuda, oracle):
+    # the fused kernel and the fused-loss forward share one workspace; counters
+    # re-arm across stream-ordered calls and graph replays
+    import pcm_hip
+    b, n, m = 32, 1024, 1024
+    a, c = _clouds(113, b, n, m)
+    x1, x2 = a.to(cuda), c.to(cuda)
+    ws = torch.zeros(pcm_hip.chamfer_workspace(cuda, b, n, m).numel(), dtype=torch.uint8, device=cuda)
+    d1, d2 = torch.empty(b, n, device=cuda), torch.empty(b, m, device=cuda)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+    g1, g2 = torch.empty(b, n, 3, device=cuda), torch.empty(b, m, 3, device=cuda)
+    mo = torch.zeros(6, 3, device=cuda)
+    w = 1.0 / (b * n)
+    pcm_hip.chamfer_loss_grad(x1, x2, w, w, d1, d2, i1, i2, mo[0], g1, g2, workspace=ws)
+    pcm_hip.chamfer_forward_loss(x1, x2, d1, d2, i1, i2, mo[1], workspace=ws)
+    pcm_hip.chamfer_loss_grad(x1, x2, w, w, d1, d2, i1, i2, mo[2], g1, g2, workspace=ws)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        pcm_hip.chamfer_loss_grad(x1, x2, w, w, d1, d2, i1, i2, mo[3], g1, g2, workspace=ws)
+    torch.cuda.current_stream().wait_stream(s)
+    gr = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(gr):
+        pcm_hip.chamfer_loss_grad(x1, x2, w, w, d1, d2, i1, i2, mo[4], g1, g2, workspace=ws)
+        pcm_hip.chamfer_loss_grad(x1, x2, w, w, d1, d2, i1, i2, mo[5], g1, g2, workspace=ws)
+    gr.replay()
+    gr.replay()
+    torch.cuda.synchronize()
+    mo = mo.cpu()
+    for k in (2, 3, 4, 5):
+        assert torch.equal(mo[0], mo[k])
+    np.testing.assert_allclose(mo[1, :2].numpy(), mo[0, :2].numpy(), rtol=2e-6)
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), w, np.float32),
+                                       np.full((b, m), w, np.float32), ref[2], ref[3])
+    np.testing.assert_array_equal(g1.cpu().numpy().view(np.int32), gr1.view(np.int32))
+    np.testing.assert_array_equal(g2.cpu().numpy().view(np.int32), gr2.view(np.int32))
+
+
+def test_loss_grad_rejects_large_clouds(cuda):
+    import pcm_hip
+    a = torch.rand(1, 1025, 3, device=cuda)
+    c = torch.rand(1, 8, 3, device=cuda)
+    assert not pcm_hip.loss_grad_supported(a, c)
+    with pytest.raises(pcm_hip.PcmError):
+        pcm_hip.chamfer_loss_grad(a, c, 1.0, 1.0, torch.empty(1, 1025, device=cuda), torch.empty(1, 8, device=cuda),
+                                  torch.empty(1, 1025, dtype=torch.int32, device=cuda),
+                                  torch.empty(1, 8, dtype=torch.int32, device=cuda), torch.empty(3, device=cuda),
+                                  torch.empty_like(a), torch.empty_like(c))

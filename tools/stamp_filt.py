@@ -1,0 +1,118 @@
+#!/usr/bin/env python3
+"""Phase breakdown of the filtered Chamfer forward from in-kernel stamps.
+
+Needs the profiling build (make -C 3d-pointcloudreconstruction_amd/csrc stamps),
+loaded through PCM_HIP_LIB.  Thread 0 of every workgroup records
+s_memrealtime (100 MHz) at: 0 start, 1 centre barrier, 2 first tile staged,
+3 scan done, 4 merge/proof done, 5 rescan done, 6 near-tie scans done,
+7 end.
+
+    python tools/stamp_filt.py VARIANT [VARIANT ...]
+    python tools/stamp_filt.py fused [VARIANT ...]     (pcm_chamfer_loss_grad)
+"""
+import ctypes
+import os
+import statistics
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+os.environ["PCM_HIP_LIB"] = os.path.join(REPO, "3d-pointcloudreconstruction_amd", "lib", "libpcm_hip_stamps.so")
+sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric"))
+import torch  # noqa: E402
+import pcm_hip  # noqa: E402
+
+NBASE = 10                                  # csrc/chamfer.hip kNumBaseFwdVariants
+FILT_QPT = [2, 4, 4, 4, 4, 2, 4, 8]         # csrc/chamfer_filt.hip kPcmFiltVariants
+TICK_US = 0.01                              # s_memrealtime: 100 MHz
+
+
+def run(v, b, n, m, dev):
+    g = torch.Generator().manual_seed(0)
+    x1 = torch.rand(b, n, 3, generator=g).to(dev)
+    x2 = torch.rand(b, m, 3, generator=g).to(dev)
+    d1, d2 = torch.empty(b, n, device=dev), torch.empty(b, m, device=dev)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=dev)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=dev)
+    for _ in range(5):
+        pcm_hip.tune_chamfer_forward(v, x1, x2, d1, d2, i1, i2)
+    torch.cuda.synchronize()
+    qw = 64 * FILT_QPT[v - NBASE]
+    nblk = b * ((n + qw - 1) // qw + (m + qw - 1) // qw)
+    L = pcm_hip.load_library()
+    L.pcm_tune_read_stamps.restype = ctypes.c_int
+    L.pcm_tune_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    buf = (ctypes.c_ulonglong * (nblk * 8))()
+    got = L.pcm_tune_read_stamps(buf, nblk)
+    rows = [[buf[i * 8 + k] for k in range(8)] for i in range(got)]
+    t0 = min(r[0] for r in rows)
+    ends = [r[7] for r in rows]
+    names = ["centre", "stage", "scan", "proof", "rescan", "ties"]
+    print(f"variant {v} B={b} N={n} M={m}: {got} workgroups, kernel span "
+          f"{(max(ends) - t0) * TICK_US:.2f} us, start spread {(max(r[0] for r in rows) - t0) * TICK_US:.2f} us")
+    for k, nm in enumerate(names):
+        dur = [(r[k + 1] - r[k]) * TICK_US for r in rows]
+        print(f"  {nm:7s} median {statistics.median(dur):7.2f} us  mean {statistics.mean(dur):7.2f}  "
+              f"max {max(dur):7.2f}")
+    tail = [(e - r[6]) * TICK_US for e, r in zip(ends, rows)]
+    tot = [(e - r[0]) * TICK_US for e, r in zip(ends, rows)]
+    print(f"  tail    median {statistics.median(tail):7.2f} us;  per-WG total median "
+          f"{statistics.median(tot):7.2f} max {max(tot):7.2f}")
+
+
+def run_fused(v, b, n, m, dev):
+    """pcm_chamfer_loss_grad variant v: stamps in the table's upper half
+    (0 start, 1 forward done, 2 arrival done; last arrivers: 3 loads landed,
+    4 buckets filled, 7 gradients stored)."""
+    g = torch.Generator().manual_seed(0)
+    x1 = torch.rand(b, n, 3, generator=g).to(dev)
+    x2 = torch.rand(b, m, 3, generator=g).to(dev)
+    d1, d2 = torch.empty(b, n, device=dev), torch.empty(b, m, device=dev)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=dev)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=dev)
+    g1, g2 = torch.empty(b, n, 3, device=dev), torch.empty(b, m, 3, device=dev)
+    mo = torch.empty(3, device=dev)
+    for _ in range(5):
+        pcm_hip.chamfer_loss_grad(x1, x2, 1.0 / (b * n), 1.0 / (b * m), d1, d2, i1, i2, mo, g1, g2, variant=v)
+    torch.cuda.synchronize()
+    qw = 64 * FUSED_QPT[v]
+    nblk = b * ((n + qw - 1) // qw + (m + qw - 1) // qw) + 1  # + the polling workgroup
+    L = pcm_hip.load_library()
+    L.pcm_tune_read_stamps.restype = ctypes.c_int
+    L.pcm_tune_read_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    half = 1 << 15
+    buf = (ctypes.c_ulonglong * ((half + nblk) * 8))()
+    L.pcm_tune_read_stamps(buf, half + nblk)
+    rows = [[buf[(half + i) * 8 + k] for k in range(8)] for i in range(nblk)]
+    poll = rows.pop()
+    t0 = min(r[0] for r in rows)
+    lasts = [r for r in rows if r[7] > r[2]]
+    end = max(max(r[2] for r in rows), max((r[7] for r in lasts), default=0))
+    print(f"fused variant {v} B={b} N={n} M={m}: {nblk} workgroups, span {(end - t0) * TICK_US:.2f} us, "
+          f"forwards done by {(max(r[1] for r in rows) - t0) * TICK_US:.2f} us, last arrivers {len(lasts)}")
+    for nm, k0, k1, rs in [("forward", 0, 1, rows), ("arrive", 1, 2, rows), ("loads", 2, 3, lasts),
+                           ("buckets", 3, 4, lasts), ("grads", 4, 7, lasts)]:
+        dur = [(r[k1] - r[k0]) * TICK_US for r in rs]
+        print(f"  {nm:7s} median {statistics.median(dur):7.2f} us  max {max(dur):7.2f}")
+    print(f"  poller: starts {(poll[5] - t0) * TICK_US:.2f} us, done {(poll[6] - t0) * TICK_US:.2f} us")
+    print(f"  last arrivers start {(min(r[2] for r in lasts) - t0) * TICK_US:.2f} .. "
+          f"{(max(r[2] for r in lasts) - t0) * TICK_US:.2f} us after the first start")
+
+
+FUSED_QPT = [2, 4, 2]                       # csrc/chamfer_filt.hip kGradVariants
+
+
+def main():
+    dev = torch.device("cuda:0")
+    if sys.argv[1:2] == ["fused"]:
+        for v in [int(a) for a in sys.argv[2:]] or [0]:
+            run_fused(v, 32, 1024, 1024, dev)
+        return
+    vs = [int(a) for a in sys.argv[1:]] or [NBASE, NBASE + 1]
+    for v in vs:
+        run(v, 32, 1024, 1024, dev)
+    for v in vs:
+        run(v, 8, 16384, 16384, dev)
+
+
+if __name__ == "__main__":
+    main()

@@ -97,6 +97,28 @@ def main():
             tm = statistics.median([time_graph_us(gm, reps) for _ in range(rounds)])
             torch.cuda.synchronize()
             print(f"  fused-loss mode {mode}: {tm:9.2f} us  mean=({mo2[0].item():.7g},{mo2[1].item():.7g})")
+        if pcm_hip.loss_grad_supported(x1, x2):
+            # fused loss + gradient (one launch) vs fused-loss forward + backward (two)
+            mo3 = torch.empty(3, device=dev)
+            w1, w2 = 1.0 / (b * n), 1.0 / (b * m)
+            gsep = graph_of(lambda: (pcm_hip.chamfer_forward_loss(x1, x2, d1, d2, i1, i2, mo, ws),
+                                     pcm_hip.chamfer_backward(x1, x2, g1, g2, i1, i2, gx1, gx2)), reps)
+            tsep = statistics.median([time_graph_us(gsep, reps) for _ in range(rounds)])
+            print(f"  step as two launches (fused-loss fwd + bwd): {tsep:9.2f} us")
+            for v in range(pcm_hip.tune_num_chamfer_loss_grad_variants()):
+                gv = graph_of(lambda v=v: pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo3, gx1, gx2,
+                                                                    ws, variant=v), reps)
+                tv = statistics.median([time_graph_us(gv, reps) for _ in range(rounds)])
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                e0.record()
+                for _ in range(reps):
+                    pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo3, gx1, gx2, ws, variant=v)
+                e1.record()
+                e1.synchronize()
+                te = e0.elapsed_time(e1) * 1000 / reps
+                print(f"  loss+grad fused variant {v}: {tv:9.2f} us (graph)  {te:9.2f} us (eager)  "
+                      f"{2 * b * n * m / tv / 1e6:8.3f} Tpairs/s  mean={mo3.tolist()}")
         # eager per-call cost through the Python API, for reference
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()

@@ -1094,8 +1094,12 @@ inline const FwdVariant &fwd_variant(int i) {
 // for ShapeNet-size clouds (B=32, N=M=1024: 12.7 us vs 13.5 us LDS-tile), 4
 // queries per lane once a batch has >= 4M pairs (B=8, N=M=16384: 453 us).
 constexpr int kDefaultLossMode = 3;  // tools/tune_chamfer.py (profiles/r01): mode 3 vs 2 vs 1
+// With chamfer_filt.hip's filtered form (profiles/r01/tune_chamfer_r01e.txt): at
+// B=8, N=M=16384 the filtered W=8 QPT=4 C=32 variant takes 344-356 us against
+// 457-471 us for the best exact-scan form; at B=32, N=M=1024 the two are level
+// (12.2 vs 12.4 us) and the SGPR form keeps the small sizes.
 inline int default_fwd_variant(int n, int m) {
-    return (long long)n * m >= (1LL << 22) ? 3 : 8;
+    return (long long)n * m >= (1LL << 22) ? kNumBaseFwdVariants + 3 : 8;
 }
 
 int fwd_grid(const FwdVariant &v, int b, int n, int m, int &nblk1, int &nblk2, long long &blocks) {
@@ -1267,27 +1271,31 @@ extern "C" int pcm_tune_chamfer_backward(int variant, const float *xyz1, const f
 // candidate in every wave (3 more VALU per candidate per wave).
 // ---------------------------------------------------------------------------
 namespace {
-typedef void (*fwd16_kernel_t)(const pcm_h *, const pcm_h *, int, int, int, float *, float *, int32_t *,
-                               int32_t *, int, int, float *, unsigned *, float *);
-struct Fwd16Variant {
-    fwd16_kernel_t k;
-    int waves, qpt;
-};
+typedef PcmFwd16Variant Fwd16Variant;
 const Fwd16Variant kFwd16Variants[] = {
     {chamfer_fwd_kernel<pcm_h, 8, 2, kChunk, kTile, false>, 8, 2},  // 0
     {chamfer_fwd_kernel<pcm_h, 8, 4, kChunk, kTile, false>, 8, 4},  // 1
 };
-constexpr int kNumFwd16Variants = sizeof(kFwd16Variants) / sizeof(kFwd16Variants[0]);
-inline int default_fwd16_variant(int n, int m) { return (long long)n * m >= (1LL << 22) ? 1 : 0; }
+constexpr int kNumBaseFwd16Variants = sizeof(kFwd16Variants) / sizeof(kFwd16Variants[0]);
+// ids >= kNumBaseFwd16Variants: the filtered form on fp16 clouds (chamfer_filt.hip)
+inline int num_fwd16_variants() { return kNumBaseFwd16Variants + kPcmNumFilt16Variants; }
+inline const Fwd16Variant &fwd16_variant(int i) {
+    return i < kNumBaseFwd16Variants ? kFwd16Variants[i] : kPcmFilt16Variants[i - kNumBaseFwd16Variants];
+}
+// tools/tune_chamfer.py on MI355X (profiles/r01): the filtered form wins once
+// a batch element has >= 4M pairs (B=8, N=M=16384); LDS-tile form below
+inline int default_fwd16_variant(int n, int m) {
+    return (long long)n * m >= (1LL << 22) ? kNumBaseFwd16Variants + 1 : 0;
+}
 
 int launch_fwd16(int variant, const pcm_h *xyz1, const pcm_h *xyz2, int b, int n, int m, float *dist1,
                  float *dist2, int32_t *idx1, int32_t *idx2, void *stream) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
-    if (variant < 0 || variant >= kNumFwd16Variants) return PCM_ERR_INVALID_ARG;
+    if (variant < 0 || variant >= num_fwd16_variants()) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2)))
         return PCM_ERR_INVALID_ARG;
-    const Fwd16Variant &v = kFwd16Variants[variant];
+    const Fwd16Variant &v = fwd16_variant(variant);
     const int QW = 64 * v.qpt;
     const int nblk1 = (m > 0) ? (n + QW - 1) / QW : 0;
     const int nblk2 = (n > 0) ? (m + QW - 1) / QW : 0;
@@ -1315,7 +1323,7 @@ extern "C" int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, c
                         stream);
 }
 
-extern "C" int pcm_tune_num_chamfer_f16_variants(void) { return kNumFwd16Variants; }
+extern "C" int pcm_tune_num_chamfer_f16_variants(void) { return num_fwd16_variants(); }
 
 extern "C" int pcm_chamfer_backward_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
                                         const float *graddist1, const float *graddist2,

@@ -433,10 +433,37 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         __syncthreads();
         PCM_STAMP(5);
 
-        // ---- near-ties: cooperative exact scans of the whole target cloud,
-        // kTB queries per pass (one pass over the candidates serves them all)
+        // ---- near-ties: exact scans of the whole target cloud.  Resident
+        // cloud: one wave per query (LDS reads, one wave reduction, no
+        // barriers).  Otherwise: the workgroup cooperates, kTB queries per pass
+        // (one pass over the global candidates serves them all).
         const int nl = sNList;
-        for (int e0 = 0; e0 < nl; e0 += kTB) {
+        if (resident) {
+            for (int e = wave; e < nl; e += W) {
+                const int s = sList[e];
+                float x = rx[0], y = ry[0], z = rz[0];
+#pragma unroll
+                for (int qq = 1; qq < QPT; ++qq)
+                    if ((s >> 6) == qq) { x = rx[qq]; y = ry[qq]; z = rz[qq]; }
+                x = __shfl(x, s & 63, 64);
+                y = __shfl(y, s & 63, 64);
+                z = __shfl(z, s & 63, 64);
+                float bd = PCM_INF;
+                int bk = 0x7fffffff;
+                for (int k = lane; k < nt; k += 64) {
+                    const int sk = slot(k);
+                    pcm_lexmin(bd, bk, pcm_sqd(sT[0][sk] - x, sT[1][sk] - y, sT[2][sk] - z), k);
+                }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) pcm_lexmin(bd, bk, __shfl_xor(bd, o, 64), __shfl_xor(bk, o, 64));
+                if (lane == 0) {
+                    sD[s] = bd;
+                    sK[s] = bk;
+                }
+            }
+            if (nl > 0) __syncthreads();
+        }
+        for (int e0 = 0; e0 < (resident ? 0 : nl); e0 += kTB) {
             float qx[kTB], qy[kTB], qz[kTB], bd[kTB];
             int bk[kTB];
 #pragma unroll
@@ -461,9 +488,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                     pcm_lexmin(bd[j], bk[j], d, k);
                 }
             };
-            if (resident) {
-                for (int k = tid; k < nt; k += NT) visit(k, sT[0][slot(k)], sT[1][slot(k)], sT[2][slot(k)]);
-            } else {
+            {
                 constexpr int U = 8;  // candidates per thread with loads in flight together
                 for (int k0 = tid; k0 < nt; k0 += U * NT) {
                     float tx[U], ty[U], tz[U];
@@ -619,21 +644,53 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 
 // Sum of the scatter terms -h (A[src] - s) over the <= kGradSlots sources of
 // one target (ids in tab, in arbitrary order) in ascending source index -- the
-// reference's fp32 accumulation made deterministic: selection in registers.
+// reference's fp32 accumulation made deterministic.  The ids are sorted with
+// Batcher's 19-comparator network in registers; the first four sources'
+// coordinates are gathered together (clamped, unconditional LDS reads), the
+// rare rest one by one.
 __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, float sx, float sy, float sz,
                                             float h, const float *A, const uint16_t *tab, int cnt) {
-    int e[kGradSlots];
+    static_assert(kGradSlots == 8, "sorting network for 8 ids");
+    int e[8];
 #pragma unroll
-    for (int u = 0; u < kGradSlots; ++u) e[u] = u < cnt ? (int)tab[u] : 0x7fffffff;
-    int last = -1;
-    for (int t = 0; t < cnt; ++t) {
-        int nxt = 0x7fffffff;
+    for (int u = 0; u < 8; ++u) {
+        const int t = tab[u];  // unconditional: slots past cnt hold stale ids
+        e[u] = u < cnt ? t : 0x7fffffff;
+    }
+    auto cas = [&](int i, int j) {
+        const int lo = min(e[i], e[j]), hi = max(e[i], e[j]);
+        e[i] = lo;
+        e[j] = hi;
+    };
+    cas(0, 1); cas(2, 3); cas(4, 5); cas(6, 7); cas(0, 2); cas(1, 3); cas(4, 6); cas(5, 7); cas(1, 2);
+    cas(5, 6); cas(0, 4); cas(3, 7); cas(1, 5); cas(2, 6); cas(1, 4); cas(3, 6); cas(2, 4); cas(3, 5);
+    cas(3, 4);
+    auto add = [&](float tx, float ty, float tz) {
+        ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(tx, sx)));
+        ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(ty, sy)));
+        az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(tz, sz)));
+    };
+    float gx[4], gy[4], gz[4];
 #pragma unroll
-        for (int u = 0; u < kGradSlots; ++u) nxt = (e[u] > last && e[u] < nxt) ? e[u] : nxt;
-        ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(A[3 * nxt], sx)));
-        ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(A[3 * nxt + 1], sy)));
-        az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(A[3 * nxt + 2], sz)));
-        last = nxt;
+    for (int u = 0; u < 4; ++u) {
+        const int src = u < cnt ? e[u] : 0;
+        gx[u] = A[3 * src];
+        gy[u] = A[3 * src + 1];
+        gz[u] = A[3 * src + 2];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const bool on = u < cnt;
+        const float nx = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(gx[u], sx)));
+        const float ny = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(gy[u], sy)));
+        const float nz = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(gz[u], sz)));
+        ax = on ? nx : ax;
+        ay = on ? ny : ay;
+        az = on ? nz : az;
+    }
+    for (int u = 4; u < cnt; ++u) {
+        const int src = e[u];
+        add(A[3 * src], A[3 * src + 1], A[3 * src + 2]);
     }
 }
 
@@ -669,8 +726,7 @@ __device__ __forceinline__ void element_grad(const float *__restrict__ X1, const
     uint16_t *tab1 = reinterpret_cast<uint16_t *>(cnt2 + kGradCap);  // [n][slots]
     uint16_t *tab2 = tab1 + kGradCap * kGradSlots;                    // [m][slots]
 
-    pcm_dma_to_lds(P1, X1, 12 * n, wave, NW);
-    pcm_dma_to_lds(P2, X2, 12 * m, wave, NW);
+    // (P1, P2: LDS-DMA'd by the caller before its arrival, already waited for)
     int i1r[kPerT], i2r[kPerT];  // argmins of this thread's points (written by other workgroups: sc1)
 #pragma unroll
     for (int r = 0; r < kPerT; ++r) {
@@ -681,7 +737,6 @@ __device__ __forceinline__ void element_grad(const float *__restrict__ X1, const
         if (i < m) cnt2[i] = 0;
     }
     if (tid == 0) sNOvf = 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // LDS-DMA of the clouds landed
     __syncthreads();
     PCM_STAMP2(3);
 #pragma unroll
@@ -911,7 +966,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         for (int w = 0; w < W; ++w) t += sRed[w];
         __hip_atomic_store(ws.wpart + bid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+    // Every workgroup stages its batch element's clouds for the gradient phase
+    // now (L2-hot; the forward is done with the arena): whichever arrives last
+    // then finds them in LDS, and the copies land during the arrival round trip.
+    pcm_dma_to_lds(arena, X1, 12 * n, wave, W);
+    pcm_dma_to_lds(arena + 12 * kGradCap, X2, 12 * m, wave, W);
+    // every storing wave drains its sc1 stores (and the LDS-DMA lands)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) {
         const unsigned old =
@@ -962,6 +1023,13 @@ const PcmFwdVariant kPcmFiltVariants[] = {
 };
 const int kPcmNumFiltVariants = sizeof(kPcmFiltVariants) / sizeof(kPcmFiltVariants[0]);
 
+// fp16 clouds: coordinates widened on load (exact), then the same computation
+const PcmFwd16Variant kPcmFilt16Variants[] = {
+    {chamfer_fwd_filt_kernel<pcm_h, 8, 2, 16, 2048, 0>, 8, 2},  // f16 base + 0
+    {chamfer_fwd_filt_kernel<pcm_h, 8, 4, 32, 2048, 0>, 8, 4},  // f16 base + 1
+};
+const int kPcmNumFilt16Variants = sizeof(kPcmFilt16Variants) / sizeof(kPcmFilt16Variants[0]);
+
 // ---- fused loss + gradient: variants (tools/tune_chamfer.py) and entry points
 namespace {
 typedef void (*grad_kernel_t)(const float *, const float *, int, int, int, float, float, float *, float *,
@@ -976,6 +1044,9 @@ const GradVariant kGradVariants[] = {
     {chamfer_loss_grad_kernel<4, 2, 16, 1024>, 4, 2},  // 2
 };
 constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
+// tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,
+// W=8 QPT=2 19.3 us, W=4 QPT=2 21.4 us
+constexpr int kDefaultGradVariant = 1;
 
 long long grad_blocks(const GradVariant &v, int b, int n, int m, int &nblk1, int &nblk2) {
     const int QW = 64 * v.qpt;
@@ -1025,8 +1096,8 @@ extern "C" int pcm_chamfer_loss_grad(const float *xyz1, const float *xyz2, int b
                                      float w2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                      float *mean_out, float *gradxyz1, float *gradxyz2, void *workspace,
                                      size_t workspace_bytes, void *stream) {
-    return launch_loss_grad(0, xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out, gradxyz1,
-                            gradxyz2, workspace, workspace_bytes, stream);
+    return launch_loss_grad(kDefaultGradVariant, xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out,
+                            gradxyz1, gradxyz2, workspace, workspace_bytes, stream);
 }
 
 extern "C" int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,

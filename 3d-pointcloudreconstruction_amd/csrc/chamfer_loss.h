@@ -162,6 +162,16 @@ struct PcmFwdVariant {
 extern const PcmFwdVariant kPcmFiltVariants[];
 extern const int kPcmNumFiltVariants;
 
+// fp16-cloud forward kernels (same signature on binary16 clouds)
+typedef void (*pcm_fwd16_kernel_t)(const _Float16 *, const _Float16 *, int, int, int, float *, float *, int32_t *,
+                                   int32_t *, int, int, float *, unsigned *, float *);
+struct PcmFwd16Variant {
+    pcm_fwd16_kernel_t k;
+    int waves, qpt;
+};
+extern const PcmFwd16Variant kPcmFilt16Variants[];
+extern const int kPcmNumFilt16Variants;
+
 // One zero-filled workspace serves pcm_chamfer_forward_loss (its bytes first,
 // chamfer.hip) and pcm_chamfer_loss_grad (the bytes after that offset,
 // chamfer_filt.hip).

@@ -5,10 +5,13 @@
 
 One step = one pass of the hot path over one synthetic batch, exactly as a
 training step of train.py:162-176 drives it: Chamfer3D forward (both
-directions, B=32, N=M=1024 per GPU -- BASELINE config 2), the loss partial sums
+directions, B=32, N=M=1024 per GPU -- BASELINE config 2), the loss
 mean(dist1)+mean(dist2) (loss/loss.py:36), the cross-rank RCCL all-reduce of
 that scalar when N>1, and the Chamfer3D backward with graddist = 1/(B*N) (the
 gradient torch's mean feeds it).  Inputs are resident in HBM before timing.
+The step runs as ONE launch of pcm_chamfer_loss_grad (forward, loss and both
+clouds' gradients; csrc/chamfer_filt.hip); --two-launch runs it as the fused-
+loss forward + the backward kernel instead (both are reported).
 By default GRAPH_STEPS consecutive steps are captured in one hipGraph and
 replayed (HIP graphs instead of a tracing compiler: a step is two ~10 us
 kernels, so per-step host launches would leave the GPU idle); --eager launches
@@ -48,6 +51,7 @@ GRAPH_STEPS = 10                   # steps captured per hipGraph replay
 # up in for roofline.traffic (tools/pmc_passes.sh + tools/pmc_summarize.py)
 FWD_KERNEL = "chamfer_fwd_sgpr_kernel<8, 2, 16, 3>"
 BWD_KERNEL = "chamfer_bwd_staged_kernel"
+FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024>"
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "pmc_summary.json")
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
@@ -59,6 +63,9 @@ FLOP_PER_PAIR = 8
 # dist1/dist2 (f32) + idx1/idx2 (i32)  
 FWD_BYTES = 2 * B * N * 12 + 4 * B * N * 4
 BWD_BYTES = 2 * B * N * 12 + 2 * B * N * 4 + 2 * B * N * 4 + 2 * B * N * 12
+# the one-launch loss + gradient: read both clouds, write dist + idx (both
+# directions) and both gradients (the constant graddist is a kernel argument)
+FUSED_BYTES = 2 * B * N * 12 + 4 * B * N * 4 + 2 * B * N * 12
 
 
 def parse():
@@ -67,6 +74,8 @@ def parse():
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    p.add_argument("--two-launch", action="store_true",
+                   help="step = fused-loss forward + backward kernel (not the one-launch loss+gradient)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-emd", action="store_true", help="skip the EMD leg")
     p.add_argument("--no-dense", action="store_true", help="skip the dense fp16 (config 5) leg")
@@ -82,7 +91,7 @@ class ChamferStep:
     cross-rank all-reduce can take the losses of a whole graph of steps at once
     (one bucketed collective instead of one 8-byte collective per step)."""
 
-    def __init__(self, dev, world, seed, slots):
+    def __init__(self, dev, world, seed, slots, fused=True):
         g = torch.Generator(device="cpu").manual_seed(seed)
         self.xyz1 = torch.rand(B, N, 3, generator=g).to(dev)
         self.xyz2 = torch.rand(B, M, 3, generator=g).to(dev)
@@ -95,12 +104,19 @@ class ChamferStep:
         self.g2 = torch.full((B, M), 1.0 / (world * B * M), device=dev)
         self.gx1 = torch.empty(B, N, 3, device=dev)
         self.gx2 = torch.empty(B, M, 3, device=dev)
-        self.loss = torch.zeros(slots, 2, device=dev)
+        self.w1, self.w2 = 1.0 / (world * B * N), 1.0 / (world * B * M)
+        self.loss = torch.zeros(slots, 3, device=dev)
         self.ws = pcm_hip.chamfer_workspace(dev, B, N, M)
         self.world = world
+        self.fused = fused and pcm_hip.loss_grad_supported(self.xyz1, self.xyz2)
 
     def __call__(self, slot=0):
-        # forward + deterministic in-kernel mean(dist1), mean(dist2)
+        if self.fused:
+            # one launch: forward, deterministic mean(dist1), mean(dist2), and both gradients
+            pcm_hip.chamfer_loss_grad(self.xyz1, self.xyz2, self.w1, self.w2, self.d1, self.d2, self.i1,
+                                      self.i2, self.loss[slot], self.gx1, self.gx2, self.ws)
+            return
+        # forward + deterministic in-kernel mean(dist1), mean(dist2); then the backward
         pcm_hip.chamfer_forward_loss(self.xyz1, self.xyz2, self.d1, self.d2, self.i1, self.i2,
                                      self.loss[slot], self.ws)
         pcm_hip.chamfer_backward(self.xyz1, self.xyz2, self.g1, self.g2, self.i1, self.i2,
@@ -259,7 +275,7 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     per = 1 if args.eager else max(1, min(GRAPH_STEPS, args.steps))
-    step = ChamferStep(dev, world, seed=1234 + rank, slots=per)
+    step = ChamferStep(dev, world, seed=1234 + rank, slots=per, fused=not args.two_launch)
 
     def run_eager(k):
         for _ in range(k):
@@ -309,6 +325,12 @@ def main():
                                                             step.i1, step.i2, step.gx1, step.gx2),
                            200, dev)
     fwd_tflops = pairs_per_step * FLOP_PER_PAIR / (fwd_us * 1e-6) / 1e12
+    if step.fused:
+        dom_kernel, dom_bytes = FUSED_KERNEL, FUSED_BYTES
+        dom_us = kernel_avg_us(lambda: step(0), 200, dev)
+    else:
+        dom_kernel, dom_bytes, dom_us = FWD_KERNEL, FWD_BYTES, fwd_us
+    dom_tflops = pairs_per_step * FLOP_PER_PAIR / (dom_us * 1e-6) / 1e12
     out = {
         "metric": "Chamfer3D fwd+bwd point-pairs/sec @ B=32 N=M=1024; EMD iters/sec",
         "value": value,
@@ -326,21 +348,24 @@ def main():
                    "batch_per_gpu": B, "n_points": N, "m_points": M,
                    "global_batch": world * B, "parallelism": f"dp{world} (batch-sharded)",
                    "launch": mode},
-        "roofline": {"bound": "valu", "kernel": FWD_KERNEL,
-                     "achieved": fwd_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": fwd_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": pmc_bytes(FWD_KERNEL),
+        "roofline": {"bound": "valu", "kernel": dom_kernel,
+                     "achieved": dom_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": dom_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": pmc_bytes(dom_kernel),
                      "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE*2+WRITE_SIZE, "
                                      "profiles/r01/pmc_summary.json)",
-                     "kernel_us": fwd_us,
+                     "kernel_us": dom_us,
                      "note": "FLOPs = 8 per point pair (algorithmic); VALU-bound, see DESIGN.md"},
-        "roofline_hbm": {"bound": "hbm", "kernel": FWD_KERNEL,
-                         "achieved": FWD_BYTES / (fwd_us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS,
+        "roofline_hbm": {"bound": "hbm", "kernel": dom_kernel,
+                         "achieved": dom_bytes / (dom_us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s",
-                         "frac": FWD_BYTES / (fwd_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                         "algorithmic_bytes": FWD_BYTES, "traffic": pmc_bytes(FWD_KERNEL),
-                         "bwd_kernel_us": bwd_us,
-                         "bwd_achieved_gbs": BWD_BYTES / (bwd_us * 1e-6) / 1e9,
-                         "bwd_algorithmic_bytes": BWD_BYTES, "bwd_traffic": pmc_bytes(BWD_KERNEL)},
+                         "frac": dom_bytes / (dom_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                         "algorithmic_bytes": dom_bytes, "traffic": pmc_bytes(dom_kernel)},
+        "two_launch": {"fwd_loss_kernel": FWD_KERNEL, "fwd_loss_us": fwd_us,
+                       "fwd_tflops": fwd_tflops, "fwd_traffic": pmc_bytes(FWD_KERNEL),
+                       "bwd_kernel": BWD_KERNEL, "bwd_us": bwd_us,
+                       "bwd_achieved_gbs": BWD_BYTES / (bwd_us * 1e-6) / 1e9,
+                       "bwd_algorithmic_bytes": BWD_BYTES, "bwd_traffic": pmc_bytes(BWD_KERNEL),
+                       "step_us": fwd_us + bwd_us},
     }
     if not args.no_emd:
         out["emd"] = emd_leg(dev)

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Fixed kernel sequence for rocprofv3 counter passes (BASELINE configs 2 and 3):
-20x Chamfer fused-loss forward, 20x Chamfer backward (B=32, N=M=1024), 3x EMD
-forward (B=16, N=1024, 50 iters, eps 0.005).  Inputs resident before the loop."""
+20x Chamfer fused-loss forward, 20x Chamfer backward, 20x one-launch loss +
+gradient (B=32, N=M=1024), 3x EMD forward (B=16, N=1024, 50 iters, eps 0.005),
+2x the filtered forward at B=8, N=M=16384.  Inputs resident before the loop."""
 import os
 import sys
 
@@ -35,8 +36,19 @@ def main():
         pcm_hip.chamfer_forward_loss(x1, x2, d1, d2, i1, i2, mo, ws)
     for _ in range(20):
         pcm_hip.chamfer_backward(x1, x2, g1, g2, i1, i2, gx1, gx2)
+    mo3 = torch.empty(3, device=dev)
+    for _ in range(20):
+        pcm_hip.chamfer_loss_grad(x1, x2, 1.0 / (B * N), 1.0 / (B * N), d1, d2, i1, i2, mo3, gx1, gx2, ws)
     for _ in range(3):
         pcm_hip.emd_forward(e1, e2, 0.005, 50, ed, ea)
+    b5, n5 = 8, 16384
+    y1 = torch.rand(b5, n5, 3, generator=g).to(dev)
+    y2 = torch.rand(b5, n5, 3, generator=g).to(dev)
+    f1, f2 = torch.empty(b5, n5, device=dev), torch.empty(b5, n5, device=dev)
+    j1 = torch.empty(b5, n5, dtype=torch.int32, device=dev)
+    j2 = torch.empty(b5, n5, dtype=torch.int32, device=dev)
+    for _ in range(2):
+        pcm_hip.chamfer_forward(y1, y2, f1, f2, j1, j2)
     torch.cuda.synchronize()
     print("done")
 

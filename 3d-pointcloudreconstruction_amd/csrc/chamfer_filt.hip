@@ -268,6 +268,9 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                 const pcm_f4 X4 = X4n, Y4 = Y4n, Z4 = Z4n, W4 = W4n;
                 if (g + 1 < G) fetch(c, g + 1);
                 else fetch(cn, 0);
+                // the next group's four reads stay ahead of this group's math
+                // (hipcc otherwise sinks them to their use and waits on each)
+                __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int qq = 0; qq < QPT; ++qq) {
                     const pcm_f2 a01 = __builtin_elementwise_fma(
@@ -647,14 +650,18 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 // reference's fp32 accumulation made deterministic.  The ids are sorted with
 // Batcher's 19-comparator network in registers; the first four sources'
 // coordinates are gathered together (clamped, unconditional LDS reads), the
-// rare rest one by one.
+// rare rest one by one.  (Measured and rejected: both clouds' targets of a
+// round interleaved in straight-line code -- 2.6 -> 3.0 us per batch element.)
 __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, float sx, float sy, float sz,
                                             float h, const float *A, const uint16_t *tab, int cnt) {
     static_assert(kGradSlots == 8, "sorting network for 8 ids");
     int e[8];
+    // the whole 16-byte row in one ds_read_b128; slots past cnt hold stale ids
+    const uint4 row = *reinterpret_cast<const uint4 *>(tab);
+    const unsigned w[4] = {row.x, row.y, row.z, row.w};
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-        const int t = tab[u];  // unconditional: slots past cnt hold stale ids
+        const int t = (int)((w[u >> 1] >> (16 * (u & 1))) & 0xffffu);
         e[u] = u < cnt ? t : 0x7fffffff;
     }
     auto cas = [&](int i, int j) {

@@ -21,7 +21,7 @@ _METRIC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 for _p in (os.path.join(_METRIC, "emd"), os.path.join(_METRIC, "chamfer3D")):
     if _p not in sys.path:
         sys.path.append(_p)
-from dist_chamfer_3D import chamfer_3DDist  # noqa: E402
+from dist_chamfer_3D import chamfer_3DDist, chamfer_3DLoss  # noqa: E402,F401
 import emd_module as emd_func  # noqa: E402
 
 
@@ -37,10 +37,12 @@ class Loss(nn.Module):
         return torch.sqrt(emd_1).mean(1).mean()
 
     def get_chamfer_loss(self, pred, gt):
-        """pred and gt are B x N x 3; mean(dist1) + mean(dist2) (squared L2)."""
-        cham_loss = chamfer_3DDist().cuda()
-        dist1, dist2, idx1, idx2 = cham_loss(pred, gt)
-        return torch.mean(dist1) + torch.mean(dist2)
+        """pred and gt are B x N x 3; mean(dist1) + mean(dist2) (squared L2).
+
+        One kernel launch computes the loss and its gradient for float32 clouds
+        of <= 1024 points (chamfer_3DLoss); otherwise the reference sequence
+        chamfer_3DDist + two torch.mean."""
+        return chamfer_3DLoss()(pred, gt)
 
 
 if __name__ == "__main__":

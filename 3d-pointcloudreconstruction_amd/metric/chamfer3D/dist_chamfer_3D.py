@@ -9,6 +9,12 @@ Extension: float16 clouds are accepted as well (BASELINE config 5); distances
 stay float32 and gradients come back in float16 (the fp32 gradient of the
 widened clouds, rounded once).
 
+Extension: ``chamfer_3DLossFunction`` / ``chamfer_3DLoss`` return the training
+loss mean(dist1) + mean(dist2) of loss/loss.py:36 directly and compute its
+gradient in the SAME launch as the forward (pcm_chamfer_loss_grad, float32
+clouds of <= 1024 points); backward only scales the saved gradient by the
+upstream scalar.  Other clouds take the forward + torch means + backward path.
+
 Differences, all on the "stricter" side:
   * outputs are allocated directly on the device (the reference built them on
     the CPU and copied, dist_chamfer_3D.py:40-49, 63-67);
@@ -65,6 +71,52 @@ class chamfer_3DFunction(Function):
         gradxyz2 = torch.empty_like(xyz2)
         pcm_hip.chamfer_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
         return gradxyz1, gradxyz2
+
+
+class chamfer_3DLossFunction(Function):
+    """mean(dist1) + mean(dist2) and its gradient from one kernel launch."""
+
+    @staticmethod
+    def forward(ctx, xyz1, xyz2):
+        batchsize, n, dim = xyz1.size()
+        assert dim == 3, "Wrong last dimension for the chamfer distance 's input! Check with .size()"
+        _, m, dim = xyz2.size()
+        assert dim == 3, "Wrong last dimension for the chamfer distance 's input! Check with .size()"
+        assert xyz2.size(0) == batchsize, "batch sizes of the two clouds differ"
+        xyz1 = xyz1.contiguous()
+        xyz2 = xyz2.contiguous()
+        if not pcm_hip.loss_grad_supported(xyz1, xyz2):
+            raise ValueError("chamfer_3DLossFunction takes float32 clouds of 1..%d points; use "
+                             "chamfer_3DDist + torch.mean" % pcm_hip.LOSS_GRAD_MAX_POINTS)
+        device = xyz1.device
+        dist1 = torch.empty(batchsize, n, device=device)
+        dist2 = torch.empty(batchsize, m, device=device)
+        idx1 = torch.empty(batchsize, n, dtype=torch.int32, device=device)
+        idx2 = torch.empty(batchsize, m, dtype=torch.int32, device=device)
+        means = torch.empty(3, device=device)
+        gradxyz1 = torch.empty_like(xyz1)
+        gradxyz2 = torch.empty_like(xyz2)
+        # gradient of torch.mean: 1/numel per element (the weight torch's mean backward feeds)
+        pcm_hip.chamfer_loss_grad(xyz1, xyz2, 1.0 / (batchsize * n), 1.0 / (batchsize * m), dist1, dist2,
+                                  idx1, idx2, means, gradxyz1, gradxyz2)
+        ctx.save_for_backward(gradxyz1, gradxyz2)
+        return means[2]
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        gradxyz1, gradxyz2 = ctx.saved_tensors
+        return gradxyz1 * grad_loss, gradxyz2 * grad_loss
+
+
+class chamfer_3DLoss(nn.Module):
+    """loss/loss.py:34-36 in one launch (see chamfer_3DLossFunction); falls back
+    to chamfer_3DDist + torch.mean where the one-launch kernel does not apply."""
+
+    def forward(self, input1, input2):
+        if pcm_hip.loss_grad_supported(input1, input2) and input1.is_cuda:
+            return chamfer_3DLossFunction.apply(input1, input2)
+        dist1, dist2, _, _ = chamfer_3DDist()(input1, input2)
+        return torch.mean(dist1) + torch.mean(dist2)
 
 
 class chamfer_3DDist(nn.Module):

@@ -50,3 +50,11 @@ def test_modules_have_reference_names():
         assert hasattr(dist_chamfer_3D, name)
     for name in ("emdFunction", "emdModule"):
         assert hasattr(emd_module, name)
+
+
+def test_chamfer_loss_module_rejects_cpu_tensors():
+    import dist_chamfer_3D
+    with pytest.raises(RuntimeError, match="HIP device"):
+        dist_chamfer_3D.chamfer_3DLoss()(torch.rand(2, 8, 3), torch.rand(2, 9, 3))
+    with pytest.raises(ValueError):
+        dist_chamfer_3D.chamfer_3DLossFunction.apply(torch.rand(2, 8, 3).double(), torch.rand(2, 9, 3).double())

@@ -566,3 +566,42 @@ def test_loss_grad_rejects_large_clouds(cuda):
                                   torch.empty(1, 1025, dtype=torch.int32, device=cuda),
                                   torch.empty(1, 8, dtype=torch.int32, device=cuda), torch.empty(3, device=cuda),
                                   torch.empty_like(a), torch.empty_like(c))
+
+
+@pytest.mark.parametrize("b,n,m", [(32, 1024, 1024), (3, 700, 1000), (2, 2048, 100)])
+def test_loss_module_matches_reference_sequence(cuda, b, n, m):
+    # Loss.get_chamfer_loss (one launch where it applies) against the
+    # reference sequence chamfer_3DDist + torch.mean + autograd
+    import dist_chamfer_3D
+    import loss as loss_mod
+    a, c = _clouds(121, b, n, m)
+    x1 = a.to(cuda).requires_grad_(True)
+    x2 = c.to(cuda).requires_grad_(True)
+    L = loss_mod.Loss().get_chamfer_loss(x1, x2)
+    (L * 1.0).backward()
+    y1 = a.to(cuda).requires_grad_(True)
+    y2 = c.to(cuda).requires_grad_(True)
+    d1, d2, _, _ = dist_chamfer_3D.chamfer_3DDist()(y1, y2)
+    R = torch.mean(d1) + torch.mean(d2)
+    R.backward()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(L.item(), R.item(), rtol=2e-6)
+    # same per-point gradient formula and order: bit-identical
+    assert torch.equal(x1.grad, y1.grad)
+    assert torch.equal(x2.grad, y2.grad)
+
+
+def test_loss_function_scales_upstream_gradient(cuda):
+    import dist_chamfer_3D
+    a, c = _clouds(122, 4, 512, 512)
+    x1 = a.to(cuda).requires_grad_(True)
+    x2 = c.to(cuda).requires_grad_(True)
+    L = dist_chamfer_3D.chamfer_3DLossFunction.apply(x1, x2)
+    (3.0 * L).backward()
+    y1 = a.to(cuda).requires_grad_(True)
+    y2 = c.to(cuda).requires_grad_(True)
+    d1, d2, _, _ = dist_chamfer_3D.chamfer_3DDist()(y1, y2)
+    (3.0 * (torch.mean(d1) + torch.mean(d2))).backward()
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(x1.grad.cpu().numpy(), y1.grad.cpu().numpy(), rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(x2.grad.cpu().numpy(), y2.grad.cpu().numpy(), rtol=1e-6, atol=1e-9)

@@ -1,0 +1,620 @@
+// icp.hip -- ICP alignment for the evaluation caller.
+//
+// Reference: utils/icp.py (numpy + sklearn) called once per sample by
+// testnet.py:62-64 / test_pix.py with tolerance=1e-10, max_iterations=1024:
+//   nearest_neighbor    icp.py:49-65   sklearn NearestNeighbors(1), float64
+//   best_fit_transform  icp.py:4-46    centroids, H = AA^T BB, SVD, R = V U^T,
+//                                      reflection fix, t = cB - R cA
+//   icp                 icp.py:68-118  NN -> best fit -> src = T src until
+//                                      |prev - mean(dist)| < tolerance
+//
+// MI355X design: a prep kernel writes B's screening rows once; then one
+// 1024-thread workgroup owns one (A, B) pair and runs the whole loop in one
+// launch -- the source cloud stays in LDS (float64) across iterations, so
+// there is no per-iteration launch or host round trip.  Per iteration:
+//   1. nearest neighbour of every source point: a float32 screen over rows
+//      (-2t, |t|^2) of B streamed through SGPRs (3 FMAs + half a min3 per
+//      pair; chunk minima with their second best), then an exact float64
+//      decision.  The float32 value of a pair differs
+//      from the exact one by at most E = 2^-21 (|q| + R)^2 (coordinates
+//      centred on B's centroid, R = max |t|; the rounding analysis is in
+//      DESIGN.md §3.6).  If second > best + 2E the
+//      float32 winner IS the float64 winner; otherwise every candidate within
+//      best + 2E is re-scored in float64 (lowest index on exact ties).  The
+//      returned distance is sqrt((dx*dx + dy*dy) + dz*dz) in float64 -- the
+//      expression sklearn's Euclidean rdist evaluates;
+//   2. fixed-order float64 block reductions: centroids and mean distance,
+//      then the 3x3 cross-covariance of the centred pairs;
+//   3. thread 0: 3x3 SVD by one-sided Jacobi, R = V U^T with the reflection
+//      fix, T; convergence test exactly as icp.py:111-114;
+//   4. src = T src (homogeneous, float64, in LDS).
+// The final transform is best_fit_transform(A, src) (icp.py:117).
+#include "pcm_common.h"
+
+namespace {
+
+constexpr int kIcpThreads = 1024;
+constexpr int kIcpWaves = kIcpThreads / 64;
+constexpr int kIcpMaxN = 4096;                 // 36 B of LDS per point (src x,y,z,w float64 + idx)
+constexpr int kNnThreads = 256;                // one query per thread
+constexpr int kPrepThreads = 256;
+constexpr float kNnErr = 4.76837158203125e-07f;  // 2^-21
+
+// ---- float64 helpers --------------------------------------------------------
+
+// sklearn's Euclidean rdist: d = 0; d += tmp*tmp per coordinate (no fma;
+// the Makefile builds with -ffp-contract=off)
+template <typename P>
+__device__ __forceinline__ double sqd64(double sx, double sy, double sz, P t) {
+    const double dx = sx - t[0], dy = sy - t[1], dz = sz - t[2];
+    return (dx * dx + dy * dy) + dz * dz;
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Fixed-order workgroup sum of NV doubles per thread; every thread then reads
+// the totals from out[0..NV).  Two barriers; red/out may be reused by the next
+// call.
+template <int NV, int W>
+__device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[W], double *out) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+        const double s = wave_sum_d(v[i]);
+        if (lane == 0) red[i][wave] = s;
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        double s = 0.0;
+        for (int w = 0; w < W; ++w) s += red[threadIdx.x][w];
+        out[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
+template <int W>
+__device__ __forceinline__ float block_max(float v, float *red) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    if (lane == 0) red[wave] = v;
+    __syncthreads();
+    float r = red[0];
+    for (int w = 1; w < W; ++w) r = fmaxf(r, red[w]);
+    __syncthreads();
+    return r;
+}
+
+// ---- Kabsch (best_fit_transform, icp.py:22-46) ------------------------------
+
+__device__ __forceinline__ double dot3(const double *a, const double *b) {
+    return (a[0] * b[0] + a[1] * b[1]) + a[2] * b[2];
+}
+
+__device__ __forceinline__ void cross3(const double *a, const double *b, double *c) {
+    c[0] = a[1] * b[2] - a[2] * b[1];
+    c[1] = a[2] * b[0] - a[0] * b[2];
+    c[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+__device__ __forceinline__ void normalize3(double *a) {
+    const double s = sqrt(dot3(a, a));
+    if (s > 0.0) { a[0] /= s; a[1] /= s; a[2] /= s; }
+}
+
+// H (row-major, H[i][j] = sum_k AA[k][i] BB[k][j]) -> T = [R t] (3x4, row-major)
+// with R = V U^T the proper rotation of H = U S V^T (the reflection fix of
+// icp.py:34-36 keeps det R = +1: the smallest singular pair enters with the
+// sign that makes det R = +1), t = cb - R ca.
+__device__ void kabsch(const double *Hin, const double *ca, const double *cb, double *T) {
+    double h[3][3], v[3][3];
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) { h[i][j] = Hin[3 * i + j]; v[i][j] = (i == j) ? 1.0 : 0.0; }
+    // one-sided Jacobi: rotate column pairs of h until orthogonal (h V = U S)
+    for (int sweep = 0; sweep < 40; ++sweep) {
+        bool rotated = false;
+        for (int pq = 0; pq < 3; ++pq) {
+            const int p = pq == 2 ? 1 : 0, q = pq == 0 ? 1 : 2;
+            double alpha = 0.0, beta = 0.0, gamma = 0.0;
+            for (int i = 0; i < 3; ++i) {
+                alpha += h[i][p] * h[i][p];
+                beta += h[i][q] * h[i][q];
+                gamma += h[i][p] * h[i][q];
+            }
+            if (gamma == 0.0 || fabs(gamma) <= 1e-16 * sqrt(alpha * beta)) continue;
+            rotated = true;
+            const double zeta = (beta - alpha) / (2.0 * gamma);
+            const double t = copysign(1.0, zeta) / (fabs(zeta) + hypot(1.0, zeta));
+            const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
+            for (int i = 0; i < 3; ++i) {
+                const double hp = h[i][p], hq = h[i][q];
+                h[i][p] = c * hp - s * hq;
+                h[i][q] = s * hp + c * hq;
+                const double vp = v[i][p], vq = v[i][q];
+                v[i][p] = c * vp - s * vq;
+                v[i][q] = s * vp + c * vq;
+            }
+        }
+        if (!rotated) break;
+    }
+    // singular values = column norms; order descending (LAPACK's order)
+    // (compare-swap network on whole columns: static indices only, so the
+    // arrays stay in registers)
+    double sig[3];
+    for (int j = 0; j < 3; ++j) sig[j] = sqrt(h[0][j] * h[0][j] + h[1][j] * h[1][j] + h[2][j] * h[2][j]);
+    auto cswap = [&](int p, int q) {
+        if (sig[p] < sig[q]) {
+            const double s = sig[p]; sig[p] = sig[q]; sig[q] = s;
+            for (int i = 0; i < 3; ++i) {
+                const double x = h[i][p]; h[i][p] = h[i][q]; h[i][q] = x;
+                const double y = v[i][p]; v[i][p] = v[i][q]; v[i][q] = y;
+            }
+        }
+    };
+    cswap(0, 1);
+    cswap(1, 2);
+    cswap(0, 1);
+    double u1[3], u2[3], u3[3], v1[3], v2[3], v3[3];
+    for (int i = 0; i < 3; ++i) {
+        u1[i] = h[i][0]; u2[i] = h[i][1];
+        v1[i] = v[i][0]; v2[i] = v[i][1]; v3[i] = v[i][2];
+    }
+    double R[3][3];
+    if (sig[0] == 0.0) {  // H == 0: numpy's SVD gives U = V = I, R = I
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) R[i][j] = (i == j) ? 1.0 : 0.0;
+    } else {
+        normalize3(u1);
+        const double pr = dot3(u2, u1);
+        for (int i = 0; i < 3; ++i) u2[i] -= pr * u1[i];
+        if (dot3(u2, u2) <= 1e-30 * sig[0] * sig[0]) {  // rank 1: any unit vector orthogonal to u1
+            const double e[3] = {fabs(u1[0]) < 0.6 ? 1.0 : 0.0, fabs(u1[0]) < 0.6 ? 0.0 : 1.0, 0.0};
+            cross3(u1, e, u2);
+        }
+        normalize3(u2);
+        cross3(u1, u2, u3);  // det U = +1
+        double vx[3];
+        cross3(v2, v3, vx);
+        const double sgn = dot3(v1, vx) < 0.0 ? -1.0 : 1.0;  // det V of the sorted columns
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) R[i][j] = (v1[i] * u1[j] + v2[i] * u2[j]) + sgn * v3[i] * u3[j];
+    }
+    for (int i = 0; i < 3; ++i) {
+        T[4 * i + 0] = R[i][0];
+        T[4 * i + 1] = R[i][1];
+        T[4 * i + 2] = R[i][2];
+        T[4 * i + 3] = cb[i] - ((R[i][0] * ca[0] + R[i][1] * ca[1]) + R[i][2] * ca[2]);
+    }
+}
+
+// ---- nearest neighbour: float32 screen + exact float64 decision ------------
+//
+// Rows: per destination cloud, rows[j] = (-2 t'_j, |t'_j|^2) with
+// t' = fl32(dst_j - c) (c = the cloud's centroid), padded to a multiple of kChunk
+// with (0, 0, 0, +inf).  d'(q, j) = |t'|^2 - 2 t'.q' ranks j like |q' - t'|^2.
+// The rows are written by nn_prep_kernel and only read afterwards, so the scan
+// reads them through the constant address space: every wave walks the same
+// rows, the addresses are wave-uniform, and hipcc streams them with s_load into
+// SGPRs that feed the FMAs directly (no LDS traffic; one v_min3 per two rows).
+
+typedef const __attribute__((address_space(4))) pcm_f4 pcm_cf4;
+
+constexpr int kChunk = 32;
+
+struct NnHdr {      // per destination cloud, written by nn_prep_kernel
+    double c[3];    // centroid
+    float R;        // max |t'|
+    int pad;
+};
+
+__host__ __device__ inline int nn_mpad(int m) { return (m + kChunk - 1) / kChunk * kChunk; }
+
+__device__ __forceinline__ float row_d(const pcm_f4 t, float qx, float qy, float qz) {
+    return __builtin_fmaf(t.x, qx, __builtin_fmaf(t.y, qy, __builtin_fmaf(t.z, qz, t.w)));
+}
+
+// Screen of one query against all mpad rows.  Returns d1 = min d', k1 = the
+// lowest index attaining it, d2 = min over j != k1 of d'.  Chunk minima are
+// tracked with their second best (med3), then the winning chunk is rescanned
+// per candidate.
+__device__ __forceinline__ void nn_screen(pcm_cf4 *rows, const pcm_f4 *__restrict__ rows_v, int mpad, float qx,
+                                          float qy, float qz, float &d1, float &d2, int &k1) {
+    float b1 = PCM_INF, b2 = PCM_INF;
+    int c1 = 0;
+    const int nch = mpad / kChunk;
+    for (int c = 0; c < nch; ++c) {
+        pcm_cf4 *tk = rows + c * kChunk;
+        float mn = PCM_INF;
+#pragma unroll
+        for (int k = 0; k < kChunk; k += 2) {
+            const float da = row_d(tk[k], qx, qy, qz);
+            const float db = row_d(tk[k + 1], qx, qy, qz);
+            mn = __builtin_fminf(__builtin_fminf(mn, da), db);
+        }
+        b2 = __builtin_amdgcn_fmed3f(b1, b2, mn);  // second smallest chunk minimum (b1 <= b2)
+        const bool lt = mn < b1;
+        b1 = lt ? mn : b1;
+        c1 = lt ? c : c1;
+    }
+    // rescan the winning chunk (per-lane chunk: vector loads, L1/L2 resident)
+    const pcm_f4 *tk = rows_v + c1 * kChunk;
+    float e1 = PCM_INF, e2 = PCM_INF;
+    int j1 = 0;
+#pragma unroll 8
+    for (int k = 0; k < kChunk; ++k) {
+        const float d = row_d(tk[k], qx, qy, qz);
+        e2 = __builtin_amdgcn_fmed3f(e1, e2, d);
+        const bool lt = d < e1;
+        e1 = lt ? d : e1;
+        j1 = lt ? k : j1;
+    }
+    d1 = e1;
+    k1 = c1 * kChunk + j1;
+    d2 = __builtin_fminf(e2, b2);
+}
+
+// Exact float64 decision for one query s (float64) given its screen.  The
+// screened value of a pair differs from the exact |s - t|^2 - |q'|^2 by at most
+// E = 2^-21 (|q'| + R)^2, so only rows with d' <= d1 + 2E can
+// be the exact nearest; when d2 is above that, k1 is it.  Otherwise every
+// candidate within d1 + 2E is re-scored in float64 (lowest index on exact
+// ties): one more pass over the rows, taken by the whole wave when any lane
+// needs it, with the rows and the float64 destination points streamed through
+// SGPRs (the loop index is wave-uniform).  Returns the index; e2 = the squared
+// distance in sklearn's expression.
+typedef const __attribute__((address_space(4))) double pcm_cd;
+
+__device__ __forceinline__ int nn_decide(double sx, double sy, double sz, float qx, float qy, float qz, float d1,
+                                         float d2, int k1, pcm_cf4 *rows, int mpad, const double *__restrict__ dst,
+                                         double &e2) {
+    // local bound: any row that could beat k1 lies within sqrt(D1) of q
+    // (D1 = exact squared distance to k1), so |t| <= |q| + sqrt(D1) for every
+    // row that matters
+    const double e1 = sqd64(sx, sy, sz, dst + 3 * (size_t)k1);
+    const float qn = sqrtf(__builtin_fmaf(qz, qz, __builtin_fmaf(qy, qy, qx * qx)));
+    const float rr = 2.f * qn + sqrtf((float)e1) + 1e-30f;
+    const float E = kNnErr * rr * rr;
+    const float lim = d1 + 2.f * E;
+#ifdef PCM_NN_NOFALLBACK  // A/B timing build only (tools/tune_icp.py)
+    const bool fb = false;
+#else
+    const bool fb = !(d2 > lim);
+#endif
+    int bk = k1;
+    if (__any(fb)) {
+        // chunk by chunk as in the screen (unrolled s_load stream); only
+        // chunks whose minimum is within lim are re-scored row by row
+        pcm_cd *dc = (pcm_cd *)(uintptr_t)dst;
+        double best = __builtin_huge_val();
+        const int nch = mpad / kChunk;
+        for (int c = 0; c < nch; ++c) {
+            pcm_cf4 *tk = rows + c * kChunk;
+            float mn = PCM_INF;
+#pragma unroll
+            for (int k = 0; k < kChunk; k += 2) {
+                const float da = row_d(tk[k], qx, qy, qz);
+                const float db = row_d(tk[k + 1], qx, qy, qz);
+                mn = __builtin_fminf(__builtin_fminf(mn, da), db);
+            }
+            if (fb & (mn <= lim)) {
+                for (int k = 0; k < kChunk; ++k) {
+                    const int j = c * kChunk + k;
+                    if (row_d(tk[k], qx, qy, qz) <= lim) {  // padding rows give +inf
+                        const double e = sqd64(sx, sy, sz, dc + 3 * (size_t)j);
+                        if (e < best) { best = e; bk = j; }
+                    }
+                }
+            }
+        }
+    }
+    e2 = bk == k1 ? e1 : sqd64(sx, sy, sz, dst + 3 * (size_t)bk);
+    return bk;
+}
+
+template <int W>
+__device__ __forceinline__ void centroid3(const double *__restrict__ p, int n, double (*red)[W], double *out,
+                                          double *c) {
+    double s[3] = {0.0, 0.0, 0.0};
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        s[0] += p[3 * (size_t)j];
+        s[1] += p[3 * (size_t)j + 1];
+        s[2] += p[3 * (size_t)j + 2];
+    }
+    block_sum<3, W>(s, red, out);
+    c[0] = out[0] / n; c[1] = out[1] / n; c[2] = out[2] / n;
+}
+
+// One workgroup per destination cloud: centroid, rows, R.
+__global__ __launch_bounds__(kPrepThreads) void nn_prep_kernel(const double *__restrict__ dst, int m,
+                                                               NnHdr *__restrict__ hdr, pcm_f4 *__restrict__ rows) {
+    constexpr int W = kPrepThreads / 64;
+    __shared__ double red[3][W];
+    __shared__ double tot[3];
+    __shared__ float redf[W];
+    const int bi = blockIdx.x;
+    const double *d = dst + (size_t)bi * m * 3;
+    const int mpad = nn_mpad(m);
+    pcm_f4 *r = rows + (size_t)bi * mpad;
+    double c[3];
+    centroid3<W>(d, m, red, tot, c);
+    float rmax = 0.f;
+    for (int j = threadIdx.x; j < mpad; j += kPrepThreads) {
+        pcm_f4 t;
+        if (j < m) {
+            const float tx = (float)(d[3 * (size_t)j] - c[0]);
+            const float ty = (float)(d[3 * (size_t)j + 1] - c[1]);
+            const float tz = (float)(d[3 * (size_t)j + 2] - c[2]);
+            const float w = __builtin_fmaf(tz, tz, __builtin_fmaf(ty, ty, tx * tx));
+            t.x = -2.f * tx; t.y = -2.f * ty; t.z = -2.f * tz; t.w = w;
+            rmax = fmaxf(rmax, sqrtf(w));
+        } else {
+            t.x = 0.f; t.y = 0.f; t.z = 0.f; t.w = PCM_INF;
+        }
+        r[j] = t;
+    }
+    const float R = block_max<W>(rmax, redf);
+    if (threadIdx.x == 0) {
+        hdr[bi].c[0] = c[0]; hdr[bi].c[1] = c[1]; hdr[bi].c[2] = c[2];
+        hdr[bi].R = R;
+        hdr[bi].pad = 0;
+    }
+}
+
+// ---- ICP kernel: one workgroup per (A, B) pair -----------------------------
+
+__global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restrict__ A, const double *__restrict__ B,
+                                                          int n, const double *__restrict__ init_pose, int max_it,
+                                                          double tol, const NnHdr *__restrict__ hdr,
+                                                          const pcm_f4 *__restrict__ rows_all,
+                                                          double *__restrict__ T_out, double *__restrict__ dist_out,
+                                                          int32_t *__restrict__ iters_out) {
+    extern __shared__ __align__(16) unsigned char smem[];
+    double *sx = reinterpret_cast<double *>(smem);
+    double *sy = sx + n, *sz = sy + n, *sw = sz + n;
+    int *sidx = reinterpret_cast<int *>(sw + n);
+    __shared__ double red[12][kIcpWaves];
+    __shared__ double tot[12];
+    __shared__ double sT[12];
+    __shared__ int sDone;
+
+    const int bi = blockIdx.x, tid = threadIdx.x;
+    const double *a = A + (size_t)bi * n * 3;
+    const double *bb = B + (size_t)bi * n * 3;
+    const double *P = init_pose ? init_pose + (size_t)bi * 16 : nullptr;
+    const int mpad = nn_mpad(n);
+    const pcm_f4 *rows_v = rows_all + (size_t)bi * mpad;
+    pcm_cf4 *rows = (pcm_cf4 *)(uintptr_t)rows_v;
+    const double c[3] = {hdr[bi].c[0], hdr[bi].c[1], hdr[bi].c[2]};
+
+    // src = init_pose @ [A^T; 1] (icp.py:89-96), kept homogeneous
+    for (int j = tid; j < n; j += kIcpThreads) {
+        const double x = a[3 * (size_t)j], y = a[3 * (size_t)j + 1], z = a[3 * (size_t)j + 2];
+        if (P) {
+            sx[j] = ((P[0] * x + P[1] * y) + P[2] * z) + P[3];
+            sy[j] = ((P[4] * x + P[5] * y) + P[6] * z) + P[7];
+            sz[j] = ((P[8] * x + P[9] * y) + P[10] * z) + P[11];
+            sw[j] = ((P[12] * x + P[13] * y) + P[14] * z) + P[15];
+        } else {
+            sx[j] = x; sy[j] = y; sz[j] = z; sw[j] = 1.0;
+        }
+    }
+
+    double prev = 0.0;
+    int it = 0;
+    for (;; ++it) {
+        // 1. nearest neighbours (each thread owns points tid, tid + kIcpThreads, ...)
+        double s7[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int base = 0; base < n; base += kIcpThreads) {
+            const int q = min(base + tid, n - 1);
+            const float qx = (float)(sx[q] - c[0]);
+            const float qy = (float)(sy[q] - c[1]);
+            const float qz = (float)(sz[q] - c[2]);
+            float d1, d2;
+            int k1;
+            nn_screen(rows, rows_v, mpad, qx, qy, qz, d1, d2, k1);
+            if (base + tid < n) {
+                double e2;
+                const int k = nn_decide(sx[q], sy[q], sz[q], qx, qy, qz, d1, d2, k1, rows, mpad, bb, e2);
+                const double dist = sqrt(e2);
+                sidx[q] = k;
+                dist_out[(size_t)bi * n + q] = dist;
+                s7[0] += sx[q]; s7[1] += sy[q]; s7[2] += sz[q];
+                s7[3] += bb[3 * (size_t)k]; s7[4] += bb[3 * (size_t)k + 1]; s7[5] += bb[3 * (size_t)k + 2];
+                s7[6] += dist;
+            }
+        }
+        block_sum<7, kIcpWaves>(s7, red, tot);
+        const double ca[3] = {tot[0] / n, tot[1] / n, tot[2] / n};
+        const double cb[3] = {tot[3] / n, tot[4] / n, tot[5] / n};
+        const double mean = tot[6] / n;
+        // 2. cross-covariance of the centred pairs (icp.py:23-29)
+        double h[9] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        for (int j = tid; j < n; j += kIcpThreads) {
+            const int k = sidx[j];
+            const double ax = sx[j] - ca[0], ay = sy[j] - ca[1], az = sz[j] - ca[2];
+            const double bx = bb[3 * (size_t)k] - cb[0], by = bb[3 * (size_t)k + 1] - cb[1],
+                         bz = bb[3 * (size_t)k + 2] - cb[2];
+            h[0] += ax * bx; h[1] += ax * by; h[2] += ax * bz;
+            h[3] += ay * bx; h[4] += ay * by; h[5] += ay * bz;
+            h[6] += az * bx; h[7] += az * by; h[8] += az * bz;
+        }
+        block_sum<9, kIcpWaves>(h, red, tot);
+        // 3. SVD / transform / convergence (icp.py:105-114)
+        if (tid == 0) {
+#ifdef PCM_ICP_NOKABSCH  // A/B timing build only (tools/tune_icp.py)
+            for (int i = 0; i < 12; ++i) sT[i] = (i % 5 == 0) ? 1.0 : 0.0;
+#else
+            kabsch(tot, ca, cb, sT);
+#endif
+            sDone = (fabs(prev - mean) < tol) || (it + 1 >= max_it);
+        }
+        __syncthreads();
+        // 4. src = T src
+        for (int j = tid; j < n; j += kIcpThreads) {
+            const double x = sx[j], y = sy[j], z = sz[j], w = sw[j];
+            sx[j] = ((sT[0] * x + sT[1] * y) + sT[2] * z) + sT[3] * w;
+            sy[j] = ((sT[4] * x + sT[5] * y) + sT[6] * z) + sT[7] * w;
+            sz[j] = ((sT[8] * x + sT[9] * y) + sT[10] * z) + sT[11] * w;
+        }
+        prev = mean;
+        if (sDone) break;  // uniform: written before the barrier above, rewritten only after two more
+    }
+    __syncthreads();
+    // final: best_fit_transform(A, src) (icp.py:117)
+    double s6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int j = tid; j < n; j += kIcpThreads) {
+        s6[0] += a[3 * (size_t)j]; s6[1] += a[3 * (size_t)j + 1]; s6[2] += a[3 * (size_t)j + 2];
+        s6[3] += sx[j]; s6[4] += sy[j]; s6[5] += sz[j];
+    }
+    block_sum<6, kIcpWaves>(s6, red, tot);
+    const double ca[3] = {tot[0] / n, tot[1] / n, tot[2] / n};
+    const double cs[3] = {tot[3] / n, tot[4] / n, tot[5] / n};
+    double h[9] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int j = tid; j < n; j += kIcpThreads) {
+        const double ax = a[3 * (size_t)j] - ca[0], ay = a[3 * (size_t)j + 1] - ca[1], az = a[3 * (size_t)j + 2] - ca[2];
+        const double bx = sx[j] - cs[0], by = sy[j] - cs[1], bz = sz[j] - cs[2];
+        h[0] += ax * bx; h[1] += ax * by; h[2] += ax * bz;
+        h[3] += ay * bx; h[4] += ay * by; h[5] += ay * bz;
+        h[6] += az * bx; h[7] += az * by; h[8] += az * bz;
+    }
+    block_sum<9, kIcpWaves>(h, red, tot);
+    if (tid == 0) {
+        double T[12];
+        kabsch(tot, ca, cs, T);
+        double *o = T_out + (size_t)bi * 16;
+        for (int i = 0; i < 12; ++i) o[i] = T[i];
+        o[12] = 0.0; o[13] = 0.0; o[14] = 0.0; o[15] = 1.0;
+        iters_out[bi] = it;
+    }
+}
+
+// ---- standalone nearest neighbour and best fit -----------------------------
+
+__global__ __launch_bounds__(kNnThreads) void nn_kernel(const double *__restrict__ src, const double *__restrict__ dst,
+                                                        int n, int m, const NnHdr *__restrict__ hdr,
+                                                        const pcm_f4 *__restrict__ rows_all,
+                                                        double *__restrict__ dist, int32_t *__restrict__ idx) {
+    const int bi = blockIdx.y;
+    const int q0 = blockIdx.x * kNnThreads + threadIdx.x;
+    const int q = min(q0, n - 1);
+    const double *s = src + (size_t)bi * n * 3;
+    const double *d = dst + (size_t)bi * m * 3;
+    const int mpad = nn_mpad(m);
+    const pcm_f4 *rows_v = rows_all + (size_t)bi * mpad;
+    pcm_cf4 *rows = (pcm_cf4 *)(uintptr_t)rows_v;
+    const double c0 = hdr[bi].c[0], c1 = hdr[bi].c[1], c2 = hdr[bi].c[2];
+    const double sx = s[3 * (size_t)q], sy = s[3 * (size_t)q + 1], sz = s[3 * (size_t)q + 2];
+    const float qx = (float)(sx - c0), qy = (float)(sy - c1), qz = (float)(sz - c2);
+    float d1, d2;
+    int k1;
+    nn_screen(rows, rows_v, mpad, qx, qy, qz, d1, d2, k1);
+    if (q0 < n) {
+        double e2;
+        const int k = nn_decide(sx, sy, sz, qx, qy, qz, d1, d2, k1, rows, mpad, d, e2);
+        dist[(size_t)bi * n + q0] = sqrt(e2);
+        idx[(size_t)bi * n + q0] = k;
+    }
+}
+
+__global__ __launch_bounds__(kPrepThreads) void best_fit_kernel(const double *__restrict__ A,
+                                                                const double *__restrict__ B, int n,
+                                                                double *__restrict__ T_out) {
+    constexpr int W = kPrepThreads / 64;
+    __shared__ double red[9][W];
+    __shared__ double tot[9];
+    const int bi = blockIdx.x;
+    const double *a = A + (size_t)bi * n * 3;
+    const double *b = B + (size_t)bi * n * 3;
+    double ca[3], cb[3];
+    centroid3<W>(a, n, red, tot, ca);
+    centroid3<W>(b, n, red, tot, cb);
+    double h[9] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    for (int j = threadIdx.x; j < n; j += kPrepThreads) {
+        const double ax = a[3 * (size_t)j] - ca[0], ay = a[3 * (size_t)j + 1] - ca[1], az = a[3 * (size_t)j + 2] - ca[2];
+        const double bx = b[3 * (size_t)j] - cb[0], by = b[3 * (size_t)j + 1] - cb[1], bz = b[3 * (size_t)j + 2] - cb[2];
+        h[0] += ax * bx; h[1] += ax * by; h[2] += ax * bz;
+        h[3] += ay * bx; h[4] += ay * by; h[5] += ay * bz;
+        h[6] += az * bx; h[7] += az * by; h[8] += az * bz;
+    }
+    block_sum<9, W>(h, red, tot);
+    if (threadIdx.x == 0) {
+        double T[12];
+        kabsch(tot, ca, cb, T);
+        double *o = T_out + (size_t)bi * 16;
+        for (int i = 0; i < 12; ++i) o[i] = T[i];
+        o[12] = 0.0; o[13] = 0.0; o[14] = 0.0; o[15] = 1.0;
+    }
+}
+
+size_t nn_ws_bytes(int b, int m) {
+    return (size_t)b * sizeof(NnHdr) + (size_t)b * nn_mpad(m) * sizeof(pcm_f4);
+}
+
+int launch_prep(const double *dst, int b, int m, void *workspace, hipStream_t s, const NnHdr **hdr,
+                const pcm_f4 **rows) {
+    NnHdr *h = reinterpret_cast<NnHdr *>(workspace);
+    pcm_f4 *r = reinterpret_cast<pcm_f4 *>(h + b);
+    hipLaunchKernelGGL(nn_prep_kernel, dim3(b), dim3(kPrepThreads), 0, s, dst, m, h, r);
+    *hdr = h;
+    *rows = r;
+    return pcm_launch_status();
+}
+
+}  // namespace
+
+extern "C" size_t pcm_icp_workspace_bytes(int b, int m) {
+    if (b <= 0 || m <= 0) return 0;
+    return nn_ws_bytes(b, m);
+}
+
+extern "C" int pcm_icp(const double *A, const double *B, int b, int n, const double *init_pose, int max_iterations,
+                       double tolerance, double *T_out, double *distances, int32_t *iterations, void *workspace,
+                       size_t workspace_bytes, void *stream) {
+    if (b < 0 || n < 0 || max_iterations < 1) return PCM_ERR_INVALID_ARG;
+    if (b == 0) return PCM_OK;
+    if (n == 0 || !A || !B || !T_out || !distances || !iterations) return PCM_ERR_INVALID_ARG;
+    if (n > kIcpMaxN || b > 65535) return PCM_ERR_UNSUPPORTED;
+    if (!workspace || workspace_bytes < nn_ws_bytes(b, n)) return PCM_ERR_WORKSPACE;
+    hipStream_t s = (hipStream_t)stream;
+    const NnHdr *hdr;
+    const pcm_f4 *rows;
+    if (launch_prep(B, b, n, workspace, s, &hdr, &rows) != PCM_OK) return PCM_ERR_LAUNCH;
+    const size_t lds = (size_t)n * (32 + 4);
+    if (lds > 64 * 1024 &&
+        hipFuncSetAttribute((const void *)icp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
+            hipSuccess)
+        return PCM_ERR_LAUNCH;
+    hipLaunchKernelGGL(icp_kernel, dim3(b), dim3(kIcpThreads), lds, s, A, B, n, init_pose, max_iterations,
+                       tolerance, hdr, rows, T_out, distances, iterations);
+    return pcm_launch_status();
+}
+
+extern "C" int pcm_nearest_neighbor(const double *src, const double *dst, int b, int n, int m, double *distances,
+                                    int32_t *indices, void *workspace, size_t workspace_bytes, void *stream) {
+    if (b < 0 || n < 0 || m < 0) return PCM_ERR_INVALID_ARG;
+    if (b == 0 || n == 0) return PCM_OK;
+    if (m == 0 || !src || !dst || !distances || !indices) return PCM_ERR_INVALID_ARG;
+    if (b > 65535) return PCM_ERR_UNSUPPORTED;
+    if (!workspace || workspace_bytes < nn_ws_bytes(b, m)) return PCM_ERR_WORKSPACE;
+    hipStream_t s = (hipStream_t)stream;
+    const NnHdr *hdr;
+    const pcm_f4 *rows;
+    if (launch_prep(dst, b, m, workspace, s, &hdr, &rows) != PCM_OK) return PCM_ERR_LAUNCH;
+    const unsigned gx = (unsigned)((n + kNnThreads - 1) / kNnThreads);
+    hipLaunchKernelGGL(nn_kernel, dim3(gx, b), dim3(kNnThreads), 0, s, src, dst, n, m, hdr, rows, distances,
+                       indices);
+    return pcm_launch_status();
+}
+
+extern "C" int pcm_best_fit_transform(const double *A, const double *B, int b, int n, double *T_out, void *stream) {
+    if (b < 0 || n < 0) return PCM_ERR_INVALID_ARG;
+    if (b == 0) return PCM_OK;
+    if (n == 0 || !A || !B || !T_out) return PCM_ERR_INVALID_ARG;
+    if (b > 65535) return PCM_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(best_fit_kernel, dim3(b), dim3(kPrepThreads), 0, (hipStream_t)stream, A, B, n, T_out);
+    return pcm_launch_status();
+}

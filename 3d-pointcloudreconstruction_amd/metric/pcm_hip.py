@@ -27,7 +27,11 @@ EXPORTED = (
     "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward",
     "pcm_chamfer_forward_f16", "pcm_chamfer_backward_f16",
     "pcm_chamfer_loss_grad",
+    "pcm_icp_workspace_bytes", "pcm_icp", "pcm_nearest_neighbor", "pcm_best_fit_transform",
 )
+
+# largest cloud pcm_icp holds in LDS (csrc/icp.hip kIcpMaxN)
+ICP_MAX_POINTS = 4096
 
 # largest cloud (points per batch element) pcm_chamfer_loss_grad runs as one
 # launch (csrc/chamfer_filt.hip kGradCap); larger clouds take forward + backward
@@ -93,6 +97,15 @@ def load_library():
                                              vp]
     L.pcm_tune_num_chamfer_loss_grad_variants.restype = ci
     L.pcm_tune_num_chamfer_loss_grad_variants.argtypes = []
+    cd = ctypes.c_double
+    L.pcm_icp.restype = ci
+    L.pcm_icp.argtypes = [vp, vp, ci, ci, vp, ci, cd, vp, vp, vp, vp, cs, vp]
+    L.pcm_icp_workspace_bytes.restype = cs
+    L.pcm_icp_workspace_bytes.argtypes = [ci, ci]
+    L.pcm_nearest_neighbor.restype = ci
+    L.pcm_nearest_neighbor.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, cs, vp]
+    L.pcm_best_fit_transform.restype = ci
+    L.pcm_best_fit_transform.argtypes = [vp, vp, ci, ci, vp, vp]
     _lib = L
     return L
 
@@ -328,3 +341,50 @@ def tune_emd_forward_stats(xyz1, xyz2, eps: float, iters: int, dist, assignment,
         _check(load_library().pcm_tune_emd_forward_stats(
             _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
             _ptr(ws), ws_bytes, _ptr(stats), _stream(dev)), "pcm_tune_emd_forward_stats")
+
+
+def _nn_workspace(dev, b: int, m: int):
+    """Cached workspace for the screening rows (content on entry irrelevant)."""
+    need = max(int(load_library().pcm_icp_workspace_bytes(b, m)), 1)
+    key = ("nn", dev, need)
+    ws = _ws_cache.get(key)
+    if ws is None:
+        ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        _ws_cache[key] = ws
+    return ws
+
+
+def icp(A, B, init_pose, max_iterations: int, tolerance: float, T_out, distances, iterations,
+        workspace=None) -> None:
+    """pcm_icp on float64 device tensors A, B [b,n,3], init_pose None or [b,4,4];
+    outputs T_out [b,4,4] float64, distances [b,n] float64, iterations [b] int32."""
+    dev = _require_device(A, B, T_out, distances, iterations)
+    b, n, _ = A.shape
+    if workspace is None:
+        workspace = _nn_workspace(dev, b, n)
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_icp(
+            _ptr(A), _ptr(B), b, n, _ptr(init_pose), int(max_iterations), float(tolerance), _ptr(T_out),
+            _ptr(distances), _ptr(iterations), _ptr(workspace), workspace.numel(), _stream(dev)), "pcm_icp")
+
+
+def nearest_neighbor(src, dst, distances, indices, workspace=None) -> None:
+    """pcm_nearest_neighbor on float64 device tensors src [b,n,3], dst [b,m,3]."""
+    dev = _require_device(src, dst, distances, indices)
+    b, n, _ = src.shape
+    m = dst.shape[1]
+    if workspace is None:
+        workspace = _nn_workspace(dev, b, m)
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_nearest_neighbor(
+            _ptr(src), _ptr(dst), b, n, m, _ptr(distances), _ptr(indices), _ptr(workspace), workspace.numel(),
+            _stream(dev)), "pcm_nearest_neighbor")
+
+
+def best_fit_transform(A, B, T_out) -> None:
+    """pcm_best_fit_transform on float64 device tensors A, B [b,n,3] -> T_out [b,4,4]."""
+    dev = _require_device(A, B, T_out)
+    b, n, _ = A.shape
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_best_fit_transform(_ptr(A), _ptr(B), b, n, _ptr(T_out), _stream(dev)),
+               "pcm_best_fit_transform")

@@ -79,6 +79,7 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--no-emd", action="store_true", help="skip the EMD leg")
     p.add_argument("--no-dense", action="store_true", help="skip the dense fp16 (config 5) leg")
+    p.add_argument("--no-icp", action="store_true", help="skip the ICP (evaluation alignment) leg")
     p.add_argument("--dist-backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
                         "several ranks on one GPU)")
@@ -219,6 +220,49 @@ def dense_f16_leg(dev, reps=10):
     return {"config": f"B={b} N=M={n} fp16 clouds, fp32 arithmetic", "fwd_us": f_us, "bwd_us": b_us,
             "pairs_per_s": pairs / ((f_us + b_us) * 1e-6),
             "fwd_tflops": pairs * FLOP_PER_PAIR / (f_us * 1e-6) / 1e12}
+
+
+ICP_B, ICP_N, ICP_PASSES = 32, 1024, 50
+
+
+def icp_leg(dev, with_cpu, reps=3):
+    """ICP alignment of B=32 prediction/ground-truth pairs of
+    1024 points (testnet.py:62-64), whole loop in one launch; tolerance < 0 so
+    every pair runs exactly ICP_PASSES passes (the reference default stops
+    on convergence).  CPU side: the reference's algorithm (sklearn kd-tree NN,
+    numpy SVD) restated in oracle/icp_oracle.py, on 2 pairs."""
+    import numpy as np
+    g = torch.Generator(device="cpu").manual_seed(7)
+    A = (torch.randn(ICP_B, ICP_N, 3, generator=g, dtype=torch.float64) * 0.3).to(dev)
+    B = A + 0.01 * torch.randn(ICP_B, ICP_N, 3, generator=g, dtype=torch.float64).to(dev)
+    T = torch.empty(ICP_B, 4, 4, dtype=torch.float64, device=dev)
+    d = torch.empty(ICP_B, ICP_N, dtype=torch.float64, device=dev)
+    it = torch.empty(ICP_B, dtype=torch.int32, device=dev)
+
+    def run():
+        pcm_hip.icp(A, B, None, ICP_PASSES, -1.0, T, d, it)
+
+    us = kernel_avg_us(run, reps, dev, graph=False)
+    passes = ICP_B * ICP_PASSES
+    pairs = passes * ICP_N * ICP_N
+    out = {"config": f"B={ICP_B} pairs, N={ICP_N}, {ICP_PASSES} passes each (tolerance < 0), float64 decisions",
+           "kernel": "icp_kernel", "ms_per_launch": us / 1000.0,
+           "passes_per_s": passes / (us * 1e-6), "nn_pairs_per_s": pairs / (us * 1e-6),
+           "screen_tflops": pairs * FLOP_PER_PAIR / (us * 1e-6) / 1e12}
+    if with_cpu:
+        sys.path.insert(0, os.path.join(REPO, "oracle"))
+        import icp_oracle  # CPU baseline leg only
+        An, Bn = A[:2].cpu().numpy(), B[:2].cpu().numpy()
+        t0 = time.perf_counter()
+        for k in range(2):
+            icp_oracle.icp(An[k], Bn[k], max_iterations=ICP_PASSES, tolerance=-1.0,
+                           nn=icp_oracle.nearest_neighbor_sklearn)
+        el = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": 2 * ICP_PASSES / el, "unit": "passes/s", "cores": 1, "kind": "port",
+                               "sample": f"2 pairs x {ICP_PASSES} passes, utils/icp.py algorithm with sklearn "
+                                         f"kd-tree NN (oracle/icp_oracle.py), {el:.2f} s"}
+        out["speedup_vs_cpu"] = out["passes_per_s"] / out["cpu_baseline"]["value"]
+    return out
 
 
 def pmc_bytes(kernel):
@@ -371,6 +415,8 @@ def main():
         out["emd"] = emd_leg(dev)
     if not args.no_dense:
         out["dense_fp16"] = dense_f16_leg(dev)
+    if not args.no_icp:
+        out["icp"] = icp_leg(dev, with_cpu=rank == 0 and world == 1 and not args.no_cpu)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

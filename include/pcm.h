@@ -12,6 +12,10 @@
  *                                                  metric/emd/emd_cuda.cu:228-282)
  *   pcm_emd_backward      <- emd.backward         (metric/emd/emd.cpp:19-23,
  *                                                  metric/emd/emd_cuda.cu:302-316)
+ *   pcm_icp, pcm_nearest_neighbor, pcm_best_fit_transform
+ *                         <- icp / nearest_neighbor / best_fit_transform
+ *                            (utils/icp.py:68-118, :49-65, :4-46; numpy + sklearn
+ *                            on the host in the reference, testnet.py:62-64)
  *
  * Conventions:
  *   - all pointers are DEVICE pointers to contiguous row-major arrays:
@@ -163,6 +167,50 @@ int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int n, float ep
 int pcm_emd_backward(const float *xyz1, const float *xyz2, int b, int n,
                      const float *graddist, const int32_t *assignment,
                      float *gradxyz1, void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* ICP alignment (evaluation caller)           */
+/* ---------------------------------------------------------------------- */
+
+/*
+ * Batched icp (utils/icp.py:68-118) for b independent pairs, as testnet.py:63
+ * calls it per sample: A [b,n,3] (source) and B [b,n,3] (destination), float64
+ * (the reference copies its inputs into float64 arrays, icp.py:89-92).
+ * init_pose: NULL or [b,4,4] float64 row-major (icp.py:95-96).  Per pair:
+ *   repeat: nearest neighbour of every src point in B (float64 Euclidean,
+ *           lowest index on exact ties), best-fit rigid transform, src = T src,
+ *   until |prev - mean(distances)| < tolerance or max_iterations passes;
+ *   T_out [b,4,4] = best_fit_transform(A, src) (row-major, float64),
+ *   distances [b,n] = the last pass's Euclidean NN distances (float64),
+ *   iterations [b] = the reference's returned loop index i.
+ * A prep launch writes B's float32 screening rows into `workspace`
+ * (pcm_icp_workspace_bytes(b, n) bytes, content on entry irrelevant); then the
+ * whole loop runs in one launch (one workgroup per pair).  Needs
+ * max_iterations >= 1 (the reference fails otherwise), 0 < n <= 4096
+ * (else PCM_ERR_UNSUPPORTED).  Non-finite inputs give unspecified values (the
+ * reference's sklearn rejects them; the Python wrapper does the same).
+ */
+size_t pcm_icp_workspace_bytes(int b, int m);
+int pcm_icp(const double *A, const double *B, int b, int n, const double *init_pose, int max_iterations,
+            double tolerance, double *T_out, double *distances, int32_t *iterations, void *workspace,
+            size_t workspace_bytes, void *stream);
+
+/*
+ * nearest_neighbor (utils/icp.py:49-65, sklearn NearestNeighbors(n_neighbors=1)):
+ * for each src[b,i] (n points) the nearest dst[b,k] (m points), float64:
+ *   distances[b,i] = sqrt((dx*dx + dy*dy) + dz*dz), indices[b,i] = k (int32,
+ *   lowest index on exact ties).  `workspace`: pcm_icp_workspace_bytes(b, m)
+ *   bytes (content on entry irrelevant).  Any m >= 1.
+ */
+int pcm_nearest_neighbor(const double *src, const double *dst, int b, int n, int m, double *distances,
+                         int32_t *indices, void *workspace, size_t workspace_bytes, void *stream);
+
+/*
+ * best_fit_transform (utils/icp.py:4-46) for b pairs of corresponding clouds
+ * A, B [b,n,3] float64: T_out [b,4,4] maps A onto B (proper rotation, the
+ * reflection case fixed as icp.py:34-36 does).
+ */
+int pcm_best_fit_transform(const double *A, const double *B, int b, int n, double *T_out, void *stream);
 
 #ifdef __cplusplus
 }

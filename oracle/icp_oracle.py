@@ -73,8 +73,20 @@ def nearest_neighbor(src, dst, block: int = 2048):
     return dist, idx
 
 
-def icp(A, B, init_pose=None, max_iterations=20, tolerance=0.001):
-    """utils/icp.py:68-118.  Returns (T, distances, i)."""
+def nearest_neighbor_sklearn(src, dst):
+    """utils/icp.py:49-65 verbatim in algorithm: sklearn's kd-tree (the CPU
+    baseline's timing of the reference's own NN search)."""
+    from sklearn.neighbors import NearestNeighbors
+    neigh = NearestNeighbors(n_neighbors=1)
+    neigh.fit(dst)
+    distances, indices = neigh.kneighbors(src, return_distance=True)
+    return distances.ravel(), indices.ravel()
+
+
+def icp(A, B, init_pose=None, max_iterations=20, tolerance=0.001, nn=None):
+    """utils/icp.py:68-118.  Returns (T, distances, i).  nn: the NN search
+    (default: the float64 brute force)."""
+    nn = nn or nearest_neighbor
     assert A.shape == B.shape
     m = A.shape[1]
     src = np.ones((m + 1, A.shape[0]))
@@ -85,7 +97,7 @@ def icp(A, B, init_pose=None, max_iterations=20, tolerance=0.001):
         src = init_pose @ src
     prev_error = 0
     for i in range(max_iterations):
-        distances, indices = nearest_neighbor(src[:m, :].T, dst[:m, :].T)
+        distances, indices = nn(src[:m, :].T, dst[:m, :].T)
         T, _, _ = best_fit_transform(src[:m, :].T, dst[:m, indices].T)
         src = T @ src
         mean_error = np.mean(distances)

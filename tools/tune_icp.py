@@ -1,0 +1,49 @@
+#!/usr/bin/env python3
+"""Time pcm_icp / pcm_nearest_neighbor across cloud sizes (per-pass cost split
+into the n^2 scan and the per-pass constant: reductions + 3x3 SVD)."""
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3d-pointcloudreconstruction_amd", "metric"))
+import pcm_hip  # noqa: E402
+
+
+def time_us(fn, reps=3):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        fn()
+    e1.record()
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1000.0 / reps
+
+
+def main():
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device="cpu").manual_seed(7)
+    b = int(os.environ.get("ICP_B", "32"))
+    for n in (64, 256, 1024, 2048):
+        A = (torch.randn(b, n, 3, generator=g, dtype=torch.float64) * 0.3).to(dev)
+        B = A + 0.01 * torch.randn(b, n, 3, generator=g, dtype=torch.float64).to(dev)
+        T = torch.empty(b, 4, 4, dtype=torch.float64, device=dev)
+        d = torch.empty(b, n, dtype=torch.float64, device=dev)
+        it = torch.empty(b, dtype=torch.int32, device=dev)
+        res = []
+        for passes in (1, 11):
+            res.append(time_us(lambda: pcm_hip.icp(A, B, None, passes, -1.0, T, d, it)))
+        per_pass = (res[1] - res[0]) / 10
+        nn_d = torch.empty(b, n, dtype=torch.float64, device=dev)
+        nn_i = torch.empty(b, n, dtype=torch.int32, device=dev)
+        nn_us = time_us(lambda: pcm_hip.nearest_neighbor(A, B, nn_d, nn_i), reps=10)
+        print(f"n={n:5d} b={b}: icp 1 pass {res[0]:8.1f} us, per extra pass {per_pass:8.1f} us "
+              f"({n * n / per_pass / 1e3:.2f} Gpair/s per pair-WG); nearest_neighbor {nn_us:7.1f} us", flush=True)
+
+
+if __name__ == "__main__":
+    main()

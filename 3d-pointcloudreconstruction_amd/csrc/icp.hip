@@ -50,22 +50,41 @@ __device__ __forceinline__ double sqd64(double sx, double sy, double sz, P t) {
     return (dx * dx + dy * dy) + dz * dz;
 }
 
-__device__ __forceinline__ double wave_sum_d(double v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// Fixed-order workgroup sum of NV doubles per thread (v is consumed); every
+// thread then reads the totals from out[0..NV).  Two barriers; red/out may be
+// reused by the next call.
+// 64-lane sum into lane 63 by DPP moves (no LDS round trips): quad swaps,
+// row_shr 4 / 8, row_bcast 15 / 31 -- a fixed pattern, so deterministic.  A
+// double moves as two 32-bit halves with the same control.
+template <int CTRL>
+__device__ __forceinline__ double dpp_move(double v) {
+    const unsigned long long b = __builtin_bit_cast(unsigned long long, v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(unsigned)b, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(unsigned)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __builtin_bit_cast(double, ((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
 
-// Fixed-order workgroup sum of NV doubles per thread; every thread then reads
-// the totals from out[0..NV).  Two barriers; red/out may be reused by the next
-// call.
+// Fixed-order workgroup sum of NV doubles per thread (v is consumed); every
+// thread then reads the totals from out[0..NV).  Two barriers; red/out may be
+// reused by the next call.
 template <int NV, int W>
 __device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[W], double *out) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) {
-        const double s = wave_sum_d(v[i]);
-        if (lane == 0) red[i][wave] = s;
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0xb1>(v[i]);   // quad_perm [1,0,3,2]
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0x4e>(v[i]);   // quad_perm [2,3,0,1]
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0x114>(v[i]);  // row_shr:4
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0x118>(v[i]);  // row_shr:8
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0x142>(v[i]);  // row_bcast:15
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0x143>(v[i]);  // row_bcast:31
+    if (lane == 63) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) red[i][wave] = v[i];
     }
     __syncthreads();
     if (threadIdx.x < NV) {
@@ -110,12 +129,21 @@ __device__ __forceinline__ void normalize3(double *a) {
 // with R = V U^T the proper rotation of H = U S V^T (the reflection fix of
 // icp.py:34-36 keeps det R = +1: the smallest singular pair enters with the
 // sign that makes det R = +1), t = cb - R ca.
-__device__ void kabsch(const double *Hin, const double *ca, const double *cb, double *T) {
+// vwarm (optional, in/out): an orthogonal start for V -- the previous ICP
+// pass's V, which nearly diagonalises this pass's H, so the Jacobi sweeps
+// converge in one or two instead of four or five.
+__device__ void kabsch(const double *Hin, const double *ca, const double *cb, double *T, double *vwarm = nullptr) {
     double h[3][3], v[3][3];
     for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) { h[i][j] = Hin[3 * i + j]; v[i][j] = (i == j) ? 1.0 : 0.0; }
+        for (int j = 0; j < 3; ++j) v[i][j] = vwarm ? vwarm[3 * i + j] : (i == j) ? 1.0 : 0.0;
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j)
+            h[i][j] = (Hin[3 * i] * v[0][j] + Hin[3 * i + 1] * v[1][j]) + Hin[3 * i + 2] * v[2][j];
     // one-sided Jacobi: rotate column pairs of h until orthogonal (h V = U S)
-    for (int sweep = 0; sweep < 40; ++sweep) {
+    // (columns count as orthogonal at |gamma| <= 1e-15 sqrt(alpha beta), ~4.5
+    // ulp: a tighter test is below what rounding lets a rotation reach and
+    // would spin to the sweep cap)
+    for (int sweep = 0; sweep < 16; ++sweep) {
         bool rotated = false;
         for (int pq = 0; pq < 3; ++pq) {
             const int p = pq == 2 ? 1 : 0, q = pq == 0 ? 1 : 2;
@@ -125,10 +153,11 @@ __device__ void kabsch(const double *Hin, const double *ca, const double *cb, do
                 beta += h[i][q] * h[i][q];
                 gamma += h[i][p] * h[i][q];
             }
-            if (gamma == 0.0 || fabs(gamma) <= 1e-16 * sqrt(alpha * beta)) continue;
+            if (!(fabs(gamma) > 1e-15 * sqrt(alpha * beta))) continue;
             rotated = true;
             const double zeta = (beta - alpha) / (2.0 * gamma);
-            const double t = copysign(1.0, zeta) / (fabs(zeta) + hypot(1.0, zeta));
+            const double az = fabs(zeta);
+            const double t = az > 1e150 ? 0.5 / zeta : copysign(1.0, zeta) / (az + sqrt(1.0 + zeta * zeta));
             const double c = 1.0 / sqrt(1.0 + t * t), s = c * t;
             for (int i = 0; i < 3; ++i) {
                 const double hp = h[i][p], hq = h[i][q];
@@ -163,6 +192,9 @@ __device__ void kabsch(const double *Hin, const double *ca, const double *cb, do
         u1[i] = h[i][0]; u2[i] = h[i][1];
         v1[i] = v[i][0]; v2[i] = v[i][1]; v3[i] = v[i][2];
     }
+    if (vwarm)
+        for (int i = 0; i < 3; ++i)
+            for (int j = 0; j < 3; ++j) vwarm[3 * i + j] = v[i][j];
     double R[3][3];
     if (sig[0] == 0.0) {  // H == 0: numpy's SVD gives U = V = I, R = I
         for (int i = 0; i < 3; ++i)
@@ -366,6 +398,15 @@ __global__ __launch_bounds__(kPrepThreads) void nn_prep_kernel(const double *__r
 
 // ---- ICP kernel: one workgroup per (A, B) pair -----------------------------
 
+#ifdef PCM_STAMPS  // profiling build: per-phase time of workgroup 0 (tools/tune_icp.py)
+__device__ unsigned long long g_icp_stamps[8];
+#define ICP_T(v) unsigned long long v = (blockIdx.x == 0 && threadIdx.x == 0) ? __builtin_amdgcn_s_memrealtime() : 0
+#define ICP_ACC(i, a, b) if (blockIdx.x == 0 && threadIdx.x == 0) acc[i] += (b) - (a)
+#else
+#define ICP_T(v)
+#define ICP_ACC(i, a, b)
+#endif
+
 __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restrict__ A, const double *__restrict__ B,
                                                           int n, const double *__restrict__ init_pose, int max_it,
                                                           double tol, const NnHdr *__restrict__ hdr,
@@ -375,9 +416,8 @@ __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restri
     extern __shared__ __align__(16) unsigned char smem[];
     double *sx = reinterpret_cast<double *>(smem);
     double *sy = sx + n, *sz = sy + n, *sw = sz + n;
-    int *sidx = reinterpret_cast<int *>(sw + n);
-    __shared__ double red[12][kIcpWaves];
-    __shared__ double tot[12];
+    __shared__ double red[16][kIcpWaves];
+    __shared__ double tot[16];
     __shared__ double sT[12];
     __shared__ int sDone;
 
@@ -405,9 +445,21 @@ __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restri
 
     double prev = 0.0;
     int it = 0;
+    double vw[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};  // thread 0's warm start
+#ifdef PCM_STAMPS
+    unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+#endif
     for (;; ++it) {
-        // 1. nearest neighbours (each thread owns points tid, tid + kIcpThreads, ...)
-        double s7[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+        ICP_T(t0);
+        // 1. nearest neighbours (each thread owns points tid, tid + kIcpThreads, ...),
+        //    and in the same sweep the sums for best_fit_transform (icp.py:23-29):
+        //    S = sum of (a - c)(b - c)^T about B's centroid c, so that
+        //    H = S - n (ca - c)(cb - c)^T is the centred cross-covariance
+        //    without a second pass (c is within the clouds' extent, so the
+        //    correction is small and nothing cancels catastrophically)
+        double s16[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s16[i] = 0.0;
         for (int base = 0; base < n; base += kIcpThreads) {
             const int q = min(base + tid, n - 1);
             const float qx = (float)(sx[q] - c[0]);
@@ -420,39 +472,38 @@ __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restri
                 double e2;
                 const int k = nn_decide(sx[q], sy[q], sz[q], qx, qy, qz, d1, d2, k1, rows, mpad, bb, e2);
                 const double dist = sqrt(e2);
-                sidx[q] = k;
                 dist_out[(size_t)bi * n + q] = dist;
-                s7[0] += sx[q]; s7[1] += sy[q]; s7[2] += sz[q];
-                s7[3] += bb[3 * (size_t)k]; s7[4] += bb[3 * (size_t)k + 1]; s7[5] += bb[3 * (size_t)k + 2];
-                s7[6] += dist;
+                const double ax = sx[q], ay = sy[q], az = sz[q];
+                const double bx = bb[3 * (size_t)k], by = bb[3 * (size_t)k + 1], bz = bb[3 * (size_t)k + 2];
+                s16[0] += ax; s16[1] += ay; s16[2] += az;
+                s16[3] += bx; s16[4] += by; s16[5] += bz;
+                s16[6] += dist;
+                const double ux = ax - c[0], uy = ay - c[1], uz = az - c[2];
+                const double vx = bx - c[0], vy = by - c[1], vz = bz - c[2];
+                s16[7] += ux * vx; s16[8] += ux * vy; s16[9] += ux * vz;
+                s16[10] += uy * vx; s16[11] += uy * vy; s16[12] += uy * vz;
+                s16[13] += uz * vx; s16[14] += uz * vy; s16[15] += uz * vz;
             }
         }
-        block_sum<7, kIcpWaves>(s7, red, tot);
+        ICP_T(t1);
+        block_sum<16, kIcpWaves>(s16, red, tot);
+        ICP_T(t2);
         const double ca[3] = {tot[0] / n, tot[1] / n, tot[2] / n};
         const double cb[3] = {tot[3] / n, tot[4] / n, tot[5] / n};
         const double mean = tot[6] / n;
-        // 2. cross-covariance of the centred pairs (icp.py:23-29)
-        double h[9] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-        for (int j = tid; j < n; j += kIcpThreads) {
-            const int k = sidx[j];
-            const double ax = sx[j] - ca[0], ay = sy[j] - ca[1], az = sz[j] - ca[2];
-            const double bx = bb[3 * (size_t)k] - cb[0], by = bb[3 * (size_t)k + 1] - cb[1],
-                         bz = bb[3 * (size_t)k + 2] - cb[2];
-            h[0] += ax * bx; h[1] += ax * by; h[2] += ax * bz;
-            h[3] += ay * bx; h[4] += ay * by; h[5] += ay * bz;
-            h[6] += az * bx; h[7] += az * by; h[8] += az * bz;
-        }
-        block_sum<9, kIcpWaves>(h, red, tot);
+        ICP_T(t3);
         // 3. SVD / transform / convergence (icp.py:105-114)
         if (tid == 0) {
-#ifdef PCM_ICP_NOKABSCH  // A/B timing build only (tools/tune_icp.py)
-            for (int i = 0; i < 12; ++i) sT[i] = (i % 5 == 0) ? 1.0 : 0.0;
-#else
-            kabsch(tot, ca, cb, sT);
-#endif
+            const double ea[3] = {ca[0] - c[0], ca[1] - c[1], ca[2] - c[2]};
+            const double eb[3] = {cb[0] - c[0], cb[1] - c[1], cb[2] - c[2]};
+            double H[9];
+            for (int i = 0; i < 3; ++i)
+                for (int j = 0; j < 3; ++j) H[3 * i + j] = tot[7 + 3 * i + j] - n * (ea[i] * eb[j]);
+            kabsch(H, ca, cb, sT, vw);
             sDone = (fabs(prev - mean) < tol) || (it + 1 >= max_it);
         }
         __syncthreads();
+        ICP_T(t4);
         // 4. src = T src
         for (int j = tid; j < n; j += kIcpThreads) {
             const double x = sx[j], y = sy[j], z = sz[j], w = sw[j];
@@ -461,8 +512,18 @@ __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restri
             sz[j] = ((sT[8] * x + sT[9] * y) + sT[10] * z) + sT[11] * w;
         }
         prev = mean;
+        ICP_T(t5);
+        ICP_ACC(0, t0, t1);
+        ICP_ACC(1, t1, t2);
+        ICP_ACC(2, t2, t3);  // (empty since the covariance moved into the sweep)
+        ICP_ACC(3, t3, t4);
+        ICP_ACC(4, t4, t5);
         if (sDone) break;  // uniform: written before the barrier above, rewritten only after two more
     }
+#ifdef PCM_STAMPS
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int i = 0; i < 5; ++i) g_icp_stamps[i] = acc[i];
+#endif
     __syncthreads();
     // final: best_fit_transform(A, src) (icp.py:117)
     double s6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
@@ -609,6 +670,14 @@ extern "C" int pcm_nearest_neighbor(const double *src, const double *dst, int b,
                        indices);
     return pcm_launch_status();
 }
+
+#ifdef PCM_STAMPS
+extern "C" int pcm_tune_read_icp_stamps(unsigned long long *host, int n) {
+    if (n > 8) n = 8;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_icp_stamps), n * sizeof(unsigned long long)) == hipSuccess
+               ? PCM_OK : PCM_ERR_LAUNCH;
+}
+#endif
 
 extern "C" int pcm_best_fit_transform(const double *A, const double *B, int b, int n, double *T_out, void *stream) {
     if (b < 0 || n < 0) return PCM_ERR_INVALID_ARG;

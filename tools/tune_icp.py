@@ -1,13 +1,18 @@
 #!/usr/bin/env python3
 """Time pcm_icp / pcm_nearest_neighbor across cloud sizes (per-pass cost split
-into the n^2 scan and the per-pass constant: reductions + 3x3 SVD)."""
+into the n^2 scan and the per-pass constant: reductions + 3x3 SVD).
+
+ICP_STAMPS=1: use the profiling build (make -C 3d-pointcloudreconstruction_amd/csrc
+stamps) and print workgroup 0's time per phase of one pass."""
+import ctypes
 import os
 import sys
-import time
 
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if os.environ.get("ICP_STAMPS"):
+    os.environ["PCM_HIP_LIB"] = os.path.join(ROOT, "3d-pointcloudreconstruction_amd", "lib", "libpcm_hip_stamps.so")
 sys.path.insert(0, os.path.join(ROOT, "3d-pointcloudreconstruction_amd", "metric"))
 import pcm_hip  # noqa: E402
 
@@ -41,6 +46,15 @@ def main():
         nn_d = torch.empty(b, n, dtype=torch.float64, device=dev)
         nn_i = torch.empty(b, n, dtype=torch.int32, device=dev)
         nn_us = time_us(lambda: pcm_hip.nearest_neighbor(A, B, nn_d, nn_i), reps=10)
+        if os.environ.get("ICP_STAMPS"):
+            pcm_hip.icp(A, B, None, 11, -1.0, T, d, it)
+            torch.cuda.synchronize()
+            L = pcm_hip.load_library()
+            buf = (ctypes.c_ulonglong * 8)()
+            L.pcm_tune_read_icp_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
+            L.pcm_tune_read_icp_stamps(ctypes.cast(buf, ctypes.c_void_p), 8)
+            names = ["screen+decide", "sum7", "H+sum9", "kabsch+barrier", "update"]
+            print("   per pass (us): " + ", ".join(f"{nm} {buf[i] / 100.0 / 11:.2f}" for i, nm in enumerate(names)))
         print(f"n={n:5d} b={b}: icp 1 pass {res[0]:8.1f} us, per extra pass {per_pass:8.1f} us "
               f"({n * n / per_pass / 1e3:.2f} Gpair/s per pair-WG); nearest_neighbor {nn_us:7.1f} us", flush=True)
 

@@ -10,6 +10,8 @@ extern "C" const char *pcm_strerror(int status) {
     case PCM_ERR_LAUNCH: return "HIP launch/runtime error";
     case PCM_ERR_WORKSPACE: return "workspace missing or too small";
     case PCM_ERR_UNSUPPORTED: return "size not supported by this build";
+    case PCM_ERR_IO: return "file missing, unreadable or truncated";
+    case PCM_ERR_FORMAT: return "not an (npoints, 3) float .npy array";
     default: return "unknown pcm status";
     }
 }

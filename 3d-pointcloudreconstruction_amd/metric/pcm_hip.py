@@ -28,6 +28,7 @@ EXPORTED = (
     "pcm_chamfer_forward_f16", "pcm_chamfer_backward_f16",
     "pcm_chamfer_loss_grad",
     "pcm_icp_workspace_bytes", "pcm_icp", "pcm_nearest_neighbor", "pcm_best_fit_transform",
+    "pcm_npy_cloud_points", "pcm_npy_load_clouds",
 )
 
 # largest cloud pcm_icp holds in LDS (csrc/icp.hip kIcpMaxN)

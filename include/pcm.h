@@ -47,7 +47,9 @@ typedef enum pcm_status {
     PCM_ERR_INVALID_ARG = -1,   /* bad shape / size / null pointer (reference: -1)  */
     PCM_ERR_LAUNCH = -2,        /* HIP launch or runtime error (reference: 0)      */
     PCM_ERR_WORKSPACE = -3,     /* workspace missing or too small                  */
-    PCM_ERR_UNSUPPORTED = -4    /* size outside what this build supports          */
+    PCM_ERR_UNSUPPORTED = -4,   /* size outside what this build supports          */
+    PCM_ERR_IO = -5,            /* file missing, unreadable or truncated           */
+    PCM_ERR_FORMAT = -6         /* not an (npoints, 3) float .npy array            */
 } pcm_status;
 
 /* Library / ABI version: major*10000 + minor*100 + patch. */
@@ -211,6 +213,27 @@ int pcm_nearest_neighbor(const double *src, const double *dst, int b, int n, int
  * reflection case fixed as icp.py:34-36 does).
  */
 int pcm_best_fit_transform(const double *A, const double *B, int b, int n, double *T_out, void *stream);
+
+/* ---------------------------------------------------------------------- */
+/* Ground-truth cloud ingestion (host only)    */
+/* ---------------------------------------------------------------------- */
+
+/*
+ * The reference loads each sample's ground truth with
+ * np.load(data_dir_pcl + model + '/pointcloud_<numpoints>.npy')
+ * (utils/datasets_old.py:37-38) and copies the collated batch to the GPU.
+ * These read .npy files (format 1.0-3.0; '<f4' '>f4' '<f8' '>f8'; C or
+ * Fortran order; shape (npoints, 3)) on the HOST:
+ *   pcm_npy_cloud_points: *npoints = the file's row count;
+ *   pcm_npy_load_clouds:  out[count, npoints, 3] float32 (host memory, e.g. a
+ *     pinned staging buffer) = np.load(paths[i]).astype(float32), read by
+ *     nthreads threads.  On failure returns PCM_ERR_IO / PCM_ERR_FORMAT /
+ *     PCM_ERR_INVALID_ARG for the lowest failing index, stored in
+ *     *failed_index (-1 on success); other slots may be partly written.
+ */
+int pcm_npy_cloud_points(const char *path, int *npoints);
+int pcm_npy_load_clouds(const char *const *paths, int count, int npoints, float *out, int nthreads,
+                        int *failed_index);
 
 #ifdef __cplusplus
 }

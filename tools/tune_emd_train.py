@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""EMD diagnostics at the TRAINING call (loss/loss.py:23: eps=0.05, iters=3000)
+on the clouds a seeded random-init generator predicts (train/fenet.py) and on
+uniform clouds: how many auction iterations run before every point is
+assigned, bids / full scans, per-phase wall time of batch 0, graph time."""
+import argparse
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric"))
+sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "train"))
+import pcm_hip  # noqa: E402
+
+
+def run(name, x1, x2, eps, iters):
+    b, n, _ = x1.shape
+    dev = x1.device
+    d = torch.empty(b, n, device=dev)
+    a = torch.empty(b, n, dtype=torch.int32, device=dev)
+    st = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=dev)
+    pcm_hip.tune_emd_forward_stats(x1, x2, eps, iters, d, a, st)
+    torch.cuda.synchronize()
+    st = st.cpu()
+    ph = st[2 * iters:2 * iters + 6].tolist()
+    wall = st[3 * iters + 16:3 * iters + 16 + b].tolist()
+    per = st[:2 * iters].view(iters, 2)
+    active = int((per[:, 0] > 0).sum())
+    names = ["compact", "bid-from-cache", "full-scans", "claim", "assign", "reset"]
+    print(f"[{name}] B={b} N={n} eps={eps} iters={iters}: iterations with bidders {active}; "
+          f"bids {int(per[:, 0].sum())}, full scans {int(per[:, 1].sum())}")
+    marks = [0, 1, 2, 5, 10, 20, 50, 100, 200, 500, 1000, 2000, iters - 1]
+    print("  unassigned (sum over batch) at iter:", " ".join(f"{i}:{int(per[i, 0])}" for i in marks if i < iters))
+    print("  batch-0 phase wall (us):", ", ".join(f"{nm}={v / 100.0:.1f}" for nm, v in zip(names, ph)))
+    print("  auction wall per batch element (us): min %.1f max %.1f" % (min(wall) / 100.0, max(wall) / 100.0))
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    pcm_hip.emd_forward(x1, x2, eps, iters, d, a)
+    e0.record()
+    for _ in range(5):
+        pcm_hip.emd_forward(x1, x2, eps, iters, d, a)
+    e1.record()
+    e1.synchronize()
+    print(f"  forward: {e0.elapsed_time(e1) * 1000 / 5:.1f} us/call")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--b", type=int, default=16)
+    ap.add_argument("--eps", type=float, default=0.05)
+    ap.add_argument("--iters", type=int, default=3000)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    import fenet
+    import train_step as T
+    gen = fenet.seeded_init(fenet.Generator(1024), 0).to(dev).train()
+    images, points = T.synthetic_batch(args.b, 1024, dev, seed=0)
+    with torch.no_grad():
+        pred = gen(images)[2].transpose(2, 1).contiguous()
+    run("generator prediction vs uniform GT", pred, points, args.eps, args.iters)
+    g = torch.Generator().manual_seed(3)
+    u1 = torch.rand(args.b, 1024, 3, generator=g).to(dev)
+    u2 = torch.rand(args.b, 1024, 3, generator=g).to(dev)
+    run("uniform vs uniform", u1, u2, args.eps, args.iters)
+    run("uniform vs uniform, config 3", u1, u2, 0.005, 50)
+
+
+if __name__ == "__main__":
+    main()

@@ -35,15 +35,20 @@ def main():
     ap.add_argument("--emd-iters", type=int, default=3000)
     ap.add_argument("--emd-eps", type=float, default=0.05)
     ap.add_argument("--bucket-mb", type=float, default=100.0)
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="nccl (= RCCL); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
     torch.backends.cudnn.benchmark = True  # train.py:85
 
     step = T.TrainStep(device=dev, emd_eps=args.emd_eps, emd_iters=args.emd_iters,
@@ -113,7 +118,8 @@ def main():
             "config": {"workload": "train.py step: generator fwd, Chamfer+EMD loss, backward, Adam",
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world, "epoch": args.epoch,
                        "emd_eps": args.emd_eps, "emd_iters": args.emd_iters, "params": 177276968,
-                       "parallelism": f"ddp{world}", "bucket_cap_mb": args.bucket_mb},
+                       "parallelism": f"ddp{world}" + ("" if args.dist_backend == "nccl" else f" ({args.dist_backend})"),
+                       "bucket_cap_mb": args.bucket_mb},
             "phases_ms": phases, "loss_path_ms": loss_ms, "loss_path_share": loss_ms / ms,
             "last_losses": {"total": vals[0], "chamfer": vals[1], "emd": vals[2]},
         }))

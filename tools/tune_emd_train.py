@@ -31,7 +31,7 @@ def run(name, x1, x2, eps, iters):
     names = ["compact", "bid-from-cache", "full-scans", "claim", "assign", "reset"]
     print(f"[{name}] B={b} N={n} eps={eps} iters={iters}: iterations with bidders {active}; "
           f"bids {int(per[:, 0].sum())}, full scans {int(per[:, 1].sum())}")
-    marks = [0, 1, 2, 5, 10, 20, 50, 100, 200, 500, 1000, 2000, iters - 1]
+    marks = [0, 1, 2, 5, 10, 20, 50, 100, 200, 500, 1000, 2000, 5000, iters - 1]
     print("  unassigned (sum over batch) at iter:", " ".join(f"{i}:{int(per[i, 0])}" for i in marks if i < iters))
     print("  batch-0 phase wall (us):", ", ".join(f"{nm}={v / 100.0:.1f}" for nm, v in zip(names, ph)))
     print("  auction wall per batch element (us): min %.1f max %.1f" % (min(wall) / 100.0, max(wall) / 100.0))
@@ -64,6 +64,11 @@ def main():
     u2 = torch.rand(args.b, 1024, 3, generator=g).to(dev)
     run("uniform vs uniform", u1, u2, args.eps, args.iters)
     run("uniform vs uniform, config 3", u1, u2, 0.005, 50)
+    run("uniform vs uniform, README test-time setting", u1, u2, 0.002, 10000)
+    g = torch.Generator().manual_seed(4)
+    w1 = torch.rand(20, 2048, 3, generator=g).to(dev)
+    w2 = torch.rand(20, 2048, 3, generator=g).to(dev)
+    run("metric/emd/test.py: B=20 N=2048", w1, w2, 0.05, 3000)
 
 
 if __name__ == "__main__":

@@ -44,7 +44,10 @@
 
 namespace {
 
-constexpr int kL = 32;             // cache slots per point (unused slots hold -1)
+#ifndef PCM_EMD_KL
+#define PCM_EMD_KL 32
+#endif
+constexpr int kL = PCM_EMD_KL;     // cache slots per point (unused slots hold -1); <= 64
 constexpr int kSelectSteps = 8;    // bisection steps when > kL entries clear K3
 typedef int16_t cid_t;             // cached object id (n <= kEmdMaxN = 4096), -1 = unused
 constexpr int kSeedThreads = 256;  // one wave per point, 4 points per workgroup
@@ -581,6 +584,9 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
         if (stats && tid == 0 && blockIdx.x == 0)  // per-iteration cache-bid time of batch 0
             stats[2 * iters + 16 + it] = (int)(__builtin_amdgcn_s_memrealtime() - tprev);
         PCM_EMD_PHASE(1);
+#ifdef PCM_EMD_DIAG_B2
+        const unsigned long long tB2 = tprev;  // diagnostics build: per-iteration full-scan phase time
+#endif
         // ---- B2: full scans (one wave per missed point), cache rebuilt
         const int nm = sNm;
         if (stats && tid == 0) {  // diagnostics: [iter] -> (unassigned, full scans), summed over batches
@@ -618,6 +624,9 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
         }
         __syncthreads();
         PCM_EMD_PHASE(2);
+#ifdef PCM_EMD_DIAG_B2
+        if (stats && tid == 0 && blockIdx.x == 0) stats[2 * iters + 16 + it] = (int)(tprev - tB2);
+#endif
 
         // ---- C: claim -- lowest bidder inside the reference's 1e-6 window
         for (int u = tid; u < nu; u += kEmdThreads) {

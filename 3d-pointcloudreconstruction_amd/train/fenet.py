@@ -19,7 +19,9 @@ RepVGG-A2 checkpoint the reference loads at :352 is absent from the image):
   * coarse-to-fine decoder (:244-330): MLP 2000 -> 1024 -> 512 -> 256; 128
     centres from 256; 2 offsets per centre from a 128x128 map; 4 offsets per
     second-level point from a 512x256 map through two 1x1 convs; outputs the
-    three levels as [B, 3, 128], [B, 3, 256], [B, 3, 1024].
+    three levels as [B, 3, 128], [B, 3, 256], [B, 3, 1024].  The reference hard-codes 1024
+    output points (:257, :318) whatever ``num_points`` says; here ``num_points`` (a multiple of
+    256) sets the last level, and the default 1024 is the reference's network.
 
 Plain PyTorch: the convolutions and GEMMs go to MIOpen / hipBLASLt; the
 training hot path this repository accelerates is the loss (Chamfer + EMD),

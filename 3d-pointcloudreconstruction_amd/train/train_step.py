@@ -70,11 +70,15 @@ class TrainStep:
 
     def __init__(self, gen: torch.nn.Module | None = None, *, device=None, loss_fn=None, lr: float = 5e-4,
                  lambda_cd: float = 100.0, lambda_emd: float = 100.0, emd_eps: float = 0.05,
-                 emd_iters: int = 3000, bucket_cap_mb: float = 100.0, seed: int = 0):
+                 emd_iters: int = 3000, bucket_cap_mb: float = 100.0, seed: int = 0,
+                 channels_last: bool = False):
         self.device = torch.device(device) if device is not None else (
             torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu"))
         gen = gen if gen is not None else seeded_init(Generator(1024), seed)
         gen = gen.to(self.device).train()
+        self.channels_last = channels_last
+        if channels_last:  # NHWC activations for the encoder's convolutions (same fp32 math)
+            gen = gen.to(memory_format=torch.channels_last)
         self.world = dist.get_world_size() if (dist.is_available() and dist.is_initialized()) else 1
         if self.world > 1:
             ids = [self.device.index] if self.device.type == "cuda" else None
@@ -103,6 +107,8 @@ class TrainStep:
         w = loss_weights(epoch, self.lambda_cd, self.lambda_emd)
         if w is None:
             raise ValueError(f"epoch {epoch}: the reference trains epochs 1..50 only (train.py:170-171)")
+        if self.channels_last:
+            images = images.contiguous(memory_format=torch.channels_last)
         _, _, fake = self.gen(images)
         pred = fake.transpose(2, 1)
         cd = self.loss_fn.get_chamfer_loss(pred, points)

@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--emd-iters", type=int, default=3000)
     ap.add_argument("--emd-eps", type=float, default=0.05)
     ap.add_argument("--bucket-mb", type=float, default=100.0)
+    ap.add_argument("--channels-last", action="store_true", help="NHWC activations for the encoder")
     ap.add_argument("--dist-backend", default="nccl",
                     help="nccl (= RCCL); gloo only to rehearse several ranks on one GPU")
     args = ap.parse_args()
@@ -52,7 +53,8 @@ def main():
     torch.backends.cudnn.benchmark = True  # train.py:85
 
     step = T.TrainStep(device=dev, emd_eps=args.emd_eps, emd_iters=args.emd_iters,
-                       bucket_cap_mb=args.bucket_mb, seed=0)
+                       bucket_cap_mb=args.bucket_mb, seed=0,
+                       channels_last=args.channels_last)
     step.set_epoch(args.epoch)
     images, points = T.synthetic_batch(args.batch, 1024, dev, seed=rank)
 
@@ -63,7 +65,7 @@ def main():
     # phase split of one step (events on the current stream; no host sync inside)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
     ev[0].record()
-    _, _, fake = step.gen(images)
+    _, _, fake = step.gen(images.contiguous(memory_format=torch.channels_last) if args.channels_last else images)
     ev[1].record()
     pred = fake.transpose(2, 1)
     w = T.loss_weights(args.epoch, step.lambda_cd, step.lambda_emd)
@@ -119,7 +121,8 @@ def main():
                        "batch_per_gpu": args.batch, "global_batch": args.batch * world, "epoch": args.epoch,
                        "emd_eps": args.emd_eps, "emd_iters": args.emd_iters, "params": 177276968,
                        "parallelism": f"ddp{world}" + ("" if args.dist_backend == "nccl" else f" ({args.dist_backend})"),
-                       "bucket_cap_mb": args.bucket_mb},
+                       "bucket_cap_mb": args.bucket_mb,
+                       "channels_last": args.channels_last},
             "phases_ms": phases, "loss_path_ms": loss_ms, "loss_path_share": loss_ms / ms,
             "last_losses": {"total": vals[0], "chamfer": vals[1], "emd": vals[2]},
         }))

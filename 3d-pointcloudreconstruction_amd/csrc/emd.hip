@@ -2,32 +2,49 @@
 //
 // Replaces the reference's 7-launches-per-iteration host loop
 // (metric/emd/emd_cuda.cu:256-269: clear, calc_unass_cnt, calc_unass_cnt_sum,
-// calc_unass_idx, Bid, GetMax, Assign) by two launches for any `iters`:
+// calc_unass_idx, Bid, GetMax, Assign) by two launches for any `iters` and any
+// n % 1024 == 0 (the reference's contract, emd_cuda.cu:236-249):
 //
-//  1. emd_seed_kernel (all CUs, one wave per point): iteration 0's bids.  With
-//     every price 0 the bid value v = (float)((3.0 - (double)sqrtf(d)) - 0.0)
-//     is a monotone non-increasing function of the squared distance d, so the
-//     nearest candidates by d are the top of the value list.  Each lane keeps
-//     its top-3 keys (v_med3 insertion); the cache is every lane top-2 entry
-//     above K* = max over lanes of the 3rd keys (ballot compaction, <= kL = 32
-//     entries), and every uncached object has v <= T = v(-K*).  If the cached
-//     second-best value exceeds T nothing outside the cache can enter the top
-//     two, so the bid is exact; otherwise the point is flagged for a full scan.
-//     A cache entry is (object id, s = sqrtf(d)): s does not depend on prices.
+//  1. emd_seed_kernel (all CUs, one wave per point, target cloud staged in
+//     LDS per workgroup): iteration 0's bids.  With every price 0 the bid value
+//     v = (float)((3.0 - (double)sqrtf(d)) - 0.0) is a monotone non-increasing
+//     function of the squared distance d, so the nearest candidates by d are
+//     the top of the value list.  Each lane keeps its top-3 keys; the cache is
+//     every lane top-2 entry above K* = max over lanes of the 3rd keys (ballot
+//     compaction, <= kL entries), and every uncached object has v <= T = v(-K*).
+//     If the cached second-best value exceeds T nothing outside the cache can
+//     enter the top two, so the bid is exact; otherwise the point is flagged
+//     for a full scan.  A cache entry is (object id, s = sqrtf(d)) packed in 8
+//     bytes: s does not depend on prices.
 //
-//  2. emd_auction_kernel (one persistent workgroup per batch element): every
-//     auction iteration in-kernel with the whole auction state (assignment,
-//     owner, price, max increment, claim) and both clouds in LDS, and
-//     workgroup barriers only.  An unassigned point re-bids from its cache at
-//     CURRENT prices (two double subtractions per entry; 16, 8 or 4 lanes per
-//     point by bidder count, reduced with DPP row shifts): prices only rise,
-//     so uncached values are still <= T and the same proof applies.  Points whose cache cannot prove the top two are
-//     re-scanned by one wave each: selection on an fp32 approximation of the
-//     values with a proven error bound, exact evaluation of the chosen
-//     entries, cache rebuilt (exact scan as fallback).  (Measured and
-//     rejected: a lock-free LDS queue letting waves start full scans before
-//     every cache bid is placed, 408 -> 421 us; fewer lanes per point for
-//     large bidder sets, 421 -> 436 us.)
+//  2. emd_auction_kernel: one persistent MASTER workgroup per batch element
+//     runs every auction iteration in-kernel with workgroup barriers only.  Its
+//     state (assignment, owner, price, max increment, claim key, bids, the two
+//     bidder lists, the miss list) lives in LDS for n <= 2048 and in the
+//     workspace (L2) for larger n.  An unassigned point re-bids from its cache
+//     at CURRENT prices (two double subtractions per entry, G lanes per point,
+//     DPP row reductions): prices only rise, so uncached values stay <= T and
+//     the same proof applies.  Points whose cache cannot prove the top two get
+//     a full scan: selection on an fp32 approximation with a proven error
+//     bound, exact values of the chosen entries, cache rebuilt (exact scan as
+//     fallback).  A few misses are split over 2 or 4 waves each.
+//
+//     HELPER workgroups (the rest of the grid, up to 31 per batch element, on
+//     the master's XCD where the dispatcher allows) take the full scans of
+//     heavy iterations: the master publishes the miss list and a price
+//     snapshot, helpers and the master itself claim items with a CAS on a
+//     per-item ticket that the master armed for this job (so a late helper can
+//     never take an item of a newer job), write the rebuilt cache and the bid
+//     write-through (sc1) and raise a per-item done word; the master polls
+//     those words, then places the bids.  The master never waits for an item
+//     nobody claimed -- it claims what is left itself -- so the result and the
+//     termination never depend on how many helpers are resident.
+//     (MI355X_MICROARCH.md, inter-workgroup visibility, row 1: sc1 stores,
+//     s_waitcnt vmcnt(0), sc1 flag; sc1 polls and sc1 loads.)
+//
+// Per iteration: bids -> barrier -> [full scans -> barrier] -> claim ->
+// barrier -> assign (+ next bidder list) -> barrier.  Claims carry the
+// iteration in their key ((~it) << 32 | j with atomicMin), so no reset pass.
 //
 // The cache only skips evaluations that provably cannot change the bid, so
 // the results are identical to scanning every object every iteration (the
@@ -44,16 +61,46 @@
 
 namespace {
 
-#ifndef PCM_EMD_KL
-#define PCM_EMD_KL 32
-#endif
-constexpr int kL = PCM_EMD_KL;     // cache slots per point (unused slots hold -1); <= 64
-constexpr int kSelectSteps = 8;    // bisection steps when > kL entries clear K3
-typedef int16_t cid_t;             // cached object id (n <= kEmdMaxN = 4096), -1 = unused
-constexpr int kSeedThreads = 256;  // one wave per point, 4 points per workgroup
-constexpr int kEmdThreads = 1024;  // auction workgroup (16 waves)
-constexpr int kEmdMaxN = 4096;     // LDS-resident auction state: 9 x 4 B x n
-constexpr int kEmdStageMaxN = 2048;  // + 24 B x n copies of both clouds up to here
+constexpr int kL = 32;               // cache slots per point (unused slots: id -1)
+constexpr int kSelectSteps = 8;      // bisection steps when > kL entries clear K3
+constexpr int kSeedThreads = 256;    // 4 waves
+constexpr int kSeedPtsPerWave = 4;   // 16 points per seed workgroup
+constexpr int kSeedPts = kSeedThreads / 64 * kSeedPtsPerWave;
+constexpr int kEmdThreads = 1024;    // auction workgroup (16 waves)
+constexpr int kWaves = kEmdThreads / 64;
+constexpr int kLdsStateMaxN = 2048;  // master state in LDS up to here (44 B x n)
+constexpr int kStageMaxN = 8192;     // target cloud copied to LDS up to here (12 B x n)
+constexpr int kHelperMaxN = 32768;   // helpers keep a price snapshot in LDS (4 B x n)
+constexpr int kMaxHelpers = 31;
+constexpr int kBoardWords = 32;      // per batch element: gen, quit, jn, err (128-B line each group)
+constexpr int kSpinLimit = 1 << 22;  // bounded polls (sticky error word on timeout)
+constexpr int kDefaultOffloadMin = 24;  // misses above which an iteration is offloaded
+
+typedef unsigned long long centry;   // low 32 bits: object id (-1 unused), high 32: s bits
+typedef unsigned long long ckey;     // claim key: (~it) << 32 | point
+
+__device__ __forceinline__ centry cpack(int id, float s) {
+    return (unsigned)id | ((centry)__float_as_uint(s) << 32);
+}
+
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T *p) {
+    return __hip_atomic_load(const_cast<T *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void st_sc1(T *p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <bool kSc1>
+__device__ __forceinline__ void st_entry(centry *p, centry v) {
+    if constexpr (kSc1) st_sc1(p, v); else *p = v;
+}
+template <bool kSc1>
+__device__ __forceinline__ void st_float(float *p, float v) {
+    if constexpr (kSc1) st_sc1(p, v); else *p = v;
+}
 
 __device__ __forceinline__ int f2key(float f) {
     const int i = __float_as_int(f);
@@ -169,22 +216,14 @@ __device__ __forceinline__ float wave_max(float v) {
 // ===========================================================================
 // Candidate scan + cache selection by ONE wave (64 lanes) for one point.
 //
-// A cache entry is (object id, s = sqrtf(d)): s does not depend on prices, so
-// re-evaluating a cached object later costs the two double subtractions of
-// emd_cuda.cu:146 and nothing else.
-//
 // Selection (no sorting, no extraction rounds): with key = "larger is better,
 // lower object index on ties", each lane keeps its top-2 (key, k, d) and its
 // 3rd-best key.  Cache = every lane-top-2 entry strictly above K3 = max over
-// lanes of the 3rd-best keys (~30 on random clouds): every other object lies
-// at or below K3 -- it is either outside its lane's top-2 (<= that lane's 3rd
-// <= K3) or a top-2 entry not above K3.  If more than kL qualify (common:
-// ~30 is the typical count), the threshold is raised by bisection between K3
-// and the largest key until at most kL lane-top-2 entries lie above it; the
-// bound then stays exact for every uncached key.  (The earlier fallback -- the
-// lane-top-1 entries above K2 = max of the 2nd keys -- loses the global
-// second best whenever it shares a lane with the best, which sent ~4% of the
-// auction's full scans to the exact re-scan.)  Ballots, popcounts, mbcnt.
+// lanes of the 3rd-best keys: every other object lies at or below K3 -- it is
+// either outside its lane's top-2 (<= that lane's 3rd <= K3) or a top-2 entry
+// not above K3.  If more than kL qualify, the threshold is raised by
+// bisection between K3 and the largest key until at most kL lane-top-2
+// entries lie above it; the bound then stays exact for every uncached key.
 // ===========================================================================
 struct LaneTop {
     float a1, a2, a3;  // the lane's three largest keys (multiset order)
@@ -197,12 +236,11 @@ __device__ __forceinline__ void lane_top_init(LaneTop &t) {
 }
 // Insertion into a sorted triple with v_med3: a1' = max(a1, key),
 // a2' = med3(a1, a2, key), a3' = med3(a2, a3, key).  Ids follow with strict
-// '>' while k ascends, so equal keys keep the lower index.  (fmed3 takes its
-// operands as they are: no NaN-canonicalising v_max per loop-carried value.)
-// The id selects are spelled out as v_cmp/v_cndmask in one asm block:
-// written as ternaries, hipcc turns them into exec-mask branches inside the
-// scan loop.  gfx950 needs two wait states between a VALU SGPR write and a
-// v_cndmask reading it as the lane mask (s_nop 1).
+// '>' while k ascends, so equal keys keep the lower index.  The id selects
+// are spelled out as v_cmp/v_cndmask in one asm block: written as ternaries,
+// hipcc turns them into exec-mask branches inside the scan loop.  gfx950
+// needs two wait states between a VALU SGPR write and a v_cndmask reading it
+// as the lane mask (s_nop 1).
 __device__ __forceinline__ void lane_top_push(LaneTop &t, float key, int k) {
     unsigned long long c1, c2;
     int tmp;
@@ -218,6 +256,13 @@ __device__ __forceinline__ void lane_top_push(LaneTop &t, float key, int k) {
     t.a2 = __builtin_amdgcn_fmed3f(t.a1, t.a2, key);
     t.a1 = __builtin_amdgcn_fmed3f(t.a1, key, 3.4028235e38f);  // max (keys are finite)
 }
+// Merge of another lane top over a LATER (higher-index) object range into t:
+// the result is the lane top of the union scanned in ascending order.
+__device__ __forceinline__ void lane_top_merge(LaneTop &t, float o1, int r1, float o2, int r2, float o3) {
+    lane_top_push(t, o1, r1);
+    lane_top_push(t, o2, r2);
+    t.a3 = __builtin_amdgcn_fmed3f(t.a2, t.a3, o3);  // o3 <= o2 <= a2 already
+}
 
 // squared distance of a lane's entry (recomputed in the pinned order, so it
 // is bit-identical to the value the scan used)
@@ -225,12 +270,13 @@ __device__ __forceinline__ float entry_d(float x1, float y1, float z1, const flo
     return (unsigned)q < (unsigned)n ? sqd_to(x1, y1, z1, Qc + 3 * (size_t)q) : 0.f;
 }
 
-// picks the cache entries; writes the ids and s = sqrtf(d) of the chosen
-// entries into cidx/cs (unused slots: id -1).  Returns K* (every uncached
-// key <= K*) or +inf when nothing could be cached.  s1/s2: this lane's
-// entries chosen; d1/d2: their squared distances.
-__device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float d2, cid_t *__restrict__ cidx,
-                                              float *__restrict__ cs, bool &s1, bool &s2) {
+// picks the cache entries; writes (id, s = sqrtf(d)) of the chosen entries
+// into cache[0..kL) (unused slots: id -1).  Returns K* (every uncached key
+// <= K*) or +inf when nothing could be cached.  s1/s2: this lane's entries
+// chosen; d1/d2: their squared distances.
+template <bool kSc1>
+__device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float d2, centry *__restrict__ cache,
+                                              bool &s1, bool &s2) {
     const int lane = threadIdx.x & 63;
     float Kstar = wave_max(t.a3);
     s1 = t.a1 > Kstar;
@@ -255,17 +301,9 @@ __device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float 
         cnt = __popcll(m1) + __popcll(m2);
     }
     const unsigned long long below = (1ull << lane) - 1ull;
-    if (lane < kL && lane >= cnt) cidx[lane] = -1;  // unused slots
-    if (s1) {
-        const int p = __popcll(m1 & below);
-        cidx[p] = (cid_t)t.q1;
-        if (cs) cs[p] = __builtin_sqrtf(d1);
-    }
-    if (s2) {
-        const int p = __popcll(m1) + __popcll(m2 & below);
-        cidx[p] = (cid_t)t.q2;
-        if (cs) cs[p] = __builtin_sqrtf(d2);
-    }
+    if (lane < kL && lane >= cnt) st_entry<kSc1>(cache + lane, cpack(-1, 0.f));  // unused slots
+    if (s1) st_entry<kSc1>(cache + __popcll(m1 & below), cpack(t.q1, __builtin_sqrtf(d1)));
+    if (s2) st_entry<kSc1>(cache + __popcll(m1) + __popcll(m2 & below), cpack(t.q2, __builtin_sqrtf(d2)));
     return Kstar;
 }
 
@@ -292,8 +330,7 @@ __device__ __forceinline__ void wave_top2(float v1, int k1, float v2, int k2, fl
 // non-increasing in d).  T = v(-K*) bounds every uncached value.  The bid is
 // exact whenever b2 > T (caller checks).
 __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const float *Qc, int n,
-                                          cid_t *__restrict__ cidx, float *__restrict__ cs,
-                                          float &b1, int &kb, float &b2, float &T) {
+                                          centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T) {
     const int lane = threadIdx.x & 63;
     LaneTop t;
     lane_top_init(t);
@@ -306,7 +343,7 @@ __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const fl
     }
     bool s1, s2;
     const float d1 = -t.a1, d2 = -t.a2;  // negation is exact
-    const float Kstar = select_cache(t, d1, d2, cidx, cs, s1, s2);
+    const float Kstar = select_cache<false>(t, d1, d2, cache, s1, s2);
     T = Kstar == PCM_INF ? PCM_INF : value_of(-Kstar, 0.f);
     wave_top2(s1 ? value_of(d1, 0.f) : -PCM_INF, s1 ? t.q1 : 0x7fffffff,
               s2 ? value_of(d2, 0.f) : -PCM_INF, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
@@ -314,10 +351,8 @@ __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const fl
 
 // ---- auction full scan, exact: key = the exact bid value.  Always exact
 // bid (the lanes' top-2 hold the global top-2); T = K*.
-__device__ __noinline__ void scan_exact(float x1, float y1, float z1, const float *Qc,
-                                        const float *sPrice, int n, cid_t *__restrict__ cidx,
-                                        float *__restrict__ cs, float &b1, int &kb, float &b2,
-                                        float &T) {
+__device__ __noinline__ void scan_exact(float x1, float y1, float z1, const float *Qc, const float *price, int n,
+                                        centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T) {
     const int lane = threadIdx.x & 63;
     LaneTop t;
     lane_top_init(t);
@@ -326,13 +361,13 @@ __device__ __noinline__ void scan_exact(float x1, float y1, float z1, const floa
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int k = k0 + 64 * r;
-            key[r] = value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), sPrice[k]);
+            key[r] = value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), price[k]);
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) lane_top_push(t, key[r], k0 + 64 * r);
     }
     bool s1, s2;
-    T = select_cache(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cidx, cs, s1, s2);
+    T = select_cache<true>(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cache, s1, s2);
     wave_top2(t.a1, t.q1, t.a2, t.q2, b1, kb, b2);
 }
 
@@ -345,117 +380,168 @@ __device__ __noinline__ void scan_exact(float x1, float y1, float z1, const floa
 //   v <= T = K*' + 4u(6 + |K*'|)      (>= 1.7x margin on both terms)
 // independently of the object.  Exact values are computed for the cached
 // entries only; if their second best does not exceed T the exact scan runs
-// instead (~4% of scans).  Returns false when that fallback is needed.
-// approximate keys of objects [kbeg, kend) (a multiple of 256 long) into t
+// instead.  Keys of objects [kbeg, kend) (a multiple of 256 long) into t.
 __device__ __forceinline__ void scan_fast_keys(LaneTop &t, float x1, float y1, float z1, const float *Qc,
-                                               const float *sPrice, int kbeg, int kend) {
+                                               const float *price, int kbeg, int kend) {
     const int lane = threadIdx.x & 63;
     for (int k0 = kbeg + lane; k0 < kend; k0 += 4 * 64) {
         float key[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int k = k0 + 64 * r;
-            key[r] = (3.f - __builtin_amdgcn_sqrtf(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k))) - sPrice[k];
+            key[r] = (3.f - __builtin_amdgcn_sqrtf(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k))) - price[k];
         }
 #pragma unroll
         for (int r = 0; r < 4; ++r) lane_top_push(t, key[r], k0 + 64 * r);
     }
 }
 
-// selection, bound and exact bid from the lanes' approximate-key tops
-__device__ __forceinline__ bool scan_fast_finish(const LaneTop &t, float x1, float y1, float z1,
-                                                 const float *Qc, const float *sPrice, int n,
-                                                 cid_t *__restrict__ cidx, float *__restrict__ cs, float &b1,
+// selection, bound and exact bid from the lanes' approximate-key tops;
+// returns false when the exact scan is needed
+__device__ __forceinline__ bool scan_fast_finish(const LaneTop &t, float x1, float y1, float z1, const float *Qc,
+                                                 const float *price, int n, centry *__restrict__ cache, float &b1,
                                                  int &kb, float &b2, float &T) {
     bool s1, s2;
     const float d1 = entry_d(x1, y1, z1, Qc, n, t.q1), d2 = entry_d(x1, y1, z1, Qc, n, t.q2);
-    const float Kp = select_cache(t, d1, d2, cidx, cs, s1, s2);
+    const float Kp = select_cache<true>(t, d1, d2, cache, s1, s2);
     T = Kp + 4.f * 1.1920929e-7f * (6.f + fabsf(Kp));  // +inf stays +inf
-    // exact values of this lane's cached entries
-    const float v1 = s1 ? value_of(d1, sPrice[t.q1]) : -PCM_INF;
-    const float v2 = s2 ? value_of(d2, sPrice[t.q2]) : -PCM_INF;
+    const float v1 = s1 ? value_of(d1, price[t.q1]) : -PCM_INF;
+    const float v2 = s2 ? value_of(d2, price[t.q2]) : -PCM_INF;
     wave_top2(v1, s1 ? t.q1 : 0x7fffffff, v2, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
     return b2 > T;
 }
 
-__device__ __forceinline__ bool scan_fast(float x1, float y1, float z1, const float *Qc,
-                                          const float *sPrice, int n, cid_t *__restrict__ cidx,
-                                          float *__restrict__ cs, float &b1, int &kb, float &b2,
-                                          float &T) {
+// one wave: the full bid of point (x1, y1, z1) with a rebuilt cache
+__device__ __forceinline__ void scan_full(float x1, float y1, float z1, const float *Qc, const float *price, int n,
+                                          centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T) {
     LaneTop t;
     lane_top_init(t);
-    scan_fast_keys(t, x1, y1, z1, Qc, sPrice, 0, n);
-    return scan_fast_finish(t, x1, y1, z1, Qc, sPrice, n, cidx, cs, b1, kb, b2, T);
+    scan_fast_keys(t, x1, y1, z1, Qc, price, 0, n);
+    if (!scan_fast_finish(t, x1, y1, z1, Qc, price, n, cache, b1, kb, b2, T))
+        scan_exact(x1, y1, z1, Qc, price, n, cache, b1, kb, b2, T);
 }
 
 // ===========================================================================
-// 1. seed kernel: iteration-0 bids + caches, one wave per point
+// Workspace
 // ===========================================================================
-__global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(
-    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps,
-    cid_t *__restrict__ cache_idx, float *__restrict__ cache_s, float *__restrict__ cache_T,
-    int32_t *__restrict__ bid0, float *__restrict__ inc0) {
-    const int pt = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x) * (kSeedThreads / 64) + (threadIdx.x >> 6);
-    const int batch = pt / n;
-    const int j = pt - batch * n;
-    const float *P = xyz1 + (size_t)batch * n * 3;
-    const float *Qc = xyz2 + (size_t)batch * n * 3;
-    float b1, b2, T;
-    int kb;
-    scan_seed(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, n, cache_idx + (size_t)pt * kL,
-              cache_s + (size_t)pt * kL, b1, kb, b2, T);
-    if ((threadIdx.x & 63) == 0) {
-        cache_T[pt] = T;
-        const bool proven = b2 > T && (unsigned)kb < (unsigned)n;
-        bid0[pt] = proven ? kb : -2;  // -2: needs a full scan in the auction kernel
-        inc0[pt] = b1 - b2 + eps;
+struct EmdWs {
+    centry *cache;   // [b*n*kL]
+    float *CT;       // [b*n] cache bound
+    int32_t *bid0;   // [b*n] iteration-0 bid (-2: full scan needed)
+    float *inc0;     // [b*n]
+    int32_t *board;  // [b*kBoardWords]: gen, quit, jn, err (one 128-B line each)
+    int32_t *ml;     // [b*n] job: miss list
+    int32_t *iclaim; // [b*n] job: per-item ticket (-g armed, g claimed)
+    int32_t *idone;  // [b*n] job: per-item done generation
+    int32_t *rbid;   // [b*n] job results
+    float *rinc;     // [b*n]
+    float *pp;       // [b*n] job: price snapshot
+    // master state in global memory (n > kLdsStateMaxN), per batch element n words each
+    int32_t *g_ass, *g_inv, *g_max, *g_bid, *g_u0, *g_u1, *g_miss;
+    float *g_price, *g_inc;
+    ckey *g_claim;
+};
+constexpr int kBoardGen = 0, kBoardQuit = 8, kBoardJn = 16, kBoardErr = 24;
+
+// ===========================================================================
+// 1. seed kernel: iteration-0 bids + caches, one wave per point, 16 points
+//    per workgroup, the target cloud staged in LDS (kStage)
+// ===========================================================================
+template <bool kStage>
+__global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__restrict__ xyz1,
+                                                                const float *__restrict__ xyz2, int n, float eps,
+                                                                EmdWs ws) {
+    extern __shared__ __attribute__((aligned(16))) float sQs[];
+    const int wgs_per_batch = n / kSeedPts;
+    const int blk = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int batch = blk / wgs_per_batch;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const float *Pg = xyz1 + (size_t)batch * n * 3;
+    const float *Qg = xyz2 + (size_t)batch * n * 3;
+    if constexpr (kStage) {
+        pcm_dma_to_lds(sQs, Qg, 12 * n, wave, kSeedThreads / 64);
+        vm_drain();
+        __syncthreads();
+    }
+    const float *Qc = kStage ? (const float *)sQs : Qg;
+    const int j0 = (blk - batch * wgs_per_batch) * kSeedPts + wave * kSeedPtsPerWave;
+    for (int p = 0; p < kSeedPtsPerWave; ++p) {
+        const int j = j0 + p;
+        const size_t pt = (size_t)batch * n + j;
+        float b1, b2, T;
+        int kb;
+        scan_seed(Pg[3 * j], Pg[3 * j + 1], Pg[3 * j + 2], Qc, n, ws.cache + pt * kL, b1, kb, b2, T);
+        if (lane == 0) {
+            ws.CT[pt] = T;
+            const bool proven = b2 > T && (unsigned)kb < (unsigned)n;
+            ws.bid0[pt] = proven ? kb : -2;  // -2: needs a full scan in the auction kernel
+            ws.inc0[pt] = b1 - b2 + eps;
+            ws.iclaim[pt] = 0;  // job tickets and done words of this launch start at 0
+            ws.idone[pt] = 0;
+            if (j == 0) {
+                ws.board[(size_t)batch * kBoardWords + kBoardGen] = 0;
+                ws.board[(size_t)batch * kBoardWords + kBoardQuit] = 0;
+                ws.board[(size_t)batch * kBoardWords + kBoardJn] = 0;
+                ws.board[(size_t)batch * kBoardWords + kBoardErr] = 0;
+            }
+        }
     }
 }
 
 // ===========================================================================
+// 2. auction kernel
+// ===========================================================================
+
+// Master state: LDS arrays (kG = false) or the workspace (kG = true).  Words
+// updated by atomics are re-read with L1-bypassing sc1 loads in the global
+// form (a plain load could hit a stale L1 line).
+template <bool kG>
+struct AState {
+    int *ass, *inv, *mx, *bid, *U[2], *miss;
+    float *price, *inc;
+    ckey *claim;
+    __device__ __forceinline__ int ld_max(int k) const {
+        if constexpr (kG) return ld_sc1(mx + k); else return mx[k];
+    }
+    __device__ __forceinline__ ckey ld_claim(int k) const {
+        if constexpr (kG) return ld_sc1(claim + k); else return claim[k];
+    }
+};
+
 // Cache bids: G lanes per bidder, kL/G cached (id, s) entries per lane at
 // current prices, a row_shr reduction over the G lanes (G divides the 16-lane
 // DPP row); the group's last lane places the bid or lists a full scan.
-// ===========================================================================
-#ifndef PCM_EMD_FORCE_G
 __device__ __forceinline__ int cache_bid_lanes(int nu) {
     // measured per bidder count on MI355X (tools/tune_emd.py, profiles/r01):
     // few bidders are latency-bound (more lanes per bidder), many are
     // VALU-bound (fewer lanes, fewer reduction steps per bidder)
     return nu <= 64 ? 16 : (nu <= 256 ? 8 : 4);
 }
-#else
-__device__ __forceinline__ int cache_bid_lanes(int) { return PCM_EMD_FORCE_G; }
-#endif
 
-template <int G>
-__device__ __forceinline__ void cache_bids(int nu, float eps, const int *sU, const cid_t *C, const float *CS,
-                                           const float *CT, const float *sPrice, int *sBid, float *sInc, int *sMax,
-                                           int *sMiss, int *sNm) {
-    static_assert(G == 1 || G == 2 || G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
-    static_assert(kL % G == 0, "entries split evenly");
+template <int G, bool kG>
+__device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, const centry *C, const float *CT,
+                                           const AState<kG> &st, int *sNm) {
+    static_assert(G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
     constexpr int E = kL / G;
     const int gi = threadIdx.x / G, gl = threadIdx.x % G;
     for (int u0 = 0; u0 < nu; u0 += kEmdThreads / G) {
         const int u = u0 + gi;
         const bool act = u < nu;
-        const int j = act ? sU[u] : 0;
-        const float tj = CT[j];
-        int ke[E];
-        float se[E];
+        const int j = act ? Ucur[u] : 0;
+        const float tj = ld_sc1(CT + j);
+        centry ce[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) ke[e] = C[(size_t)j * kL + gl + G * e];  // -1: unused slot
-#pragma unroll
-        for (int e = 0; e < E; ++e) se[e] = CS[(size_t)j * kL + gl + G * e];
+        for (int e = 0; e < E; ++e) ce[e] = ld_sc1(C + (size_t)j * kL + gl + G * e);  // helpers write them
         float b1 = -PCM_INF, b2 = -PCM_INF;
         int kb = 0x7fffffff;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             // branch-free: an unused slot (k = -1) evaluates object 0 and is
             // then forced to (-inf, INT_MAX)
-            const int k = ke[e];
+            const int k = (int)(unsigned)ce[e];
+            const float s = __uint_as_float((unsigned)(ce[e] >> 32));
             const int neg = k >> 31;
-            const float v0 = value_from_s(se[e], sPrice[k & ~neg]);
+            const float v0 = value_from_s(s, st.price[k & ~neg]);
             const float v = __int_as_float((__float_as_int(v0) & ~neg) | (int)(0xff800000u & (unsigned)neg));
             top2_push(b1, kb, b2, v, k & 0x7fffffff);
         }
@@ -465,225 +551,376 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *sU, con
         if constexpr (G >= 16) dpp_top2_step<kDppRowShr8, 0xf>(b1, kb, b2);
         if (act && gl == G - 1) {
             if (b2 > tj) {
-                sBid[j] = kb;
-                sInc[j] = b1 - b2 + eps;
-                atomicMax(&sMax[kb], f2key(b1 - b2 + eps));
+                st.bid[j] = kb;
+                st.inc[j] = b1 - b2 + eps;
+                atomicMax(&st.mx[kb], f2key(b1 - b2 + eps));
             } else {
-                sMiss[atomicAdd(sNm, 1)] = j;
+                st.miss[atomicAdd(sNm, 1)] = j;
             }
         }
     }
 }
 
-// ===========================================================================
-// 2. auction kernel: one workgroup per batch element, all iterations
-// ===========================================================================
+// a bid produced by a full scan, placed by the scanning wave's lane 0
+template <bool kG>
+__device__ __forceinline__ void place_bid(const AState<kG> &st, int j, int kb, float inc, int n) {
+    const bool valid = (unsigned)kb < (unsigned)n;  // all-NaN values: no bid (oracle: best_i = -1)
+    st.bid[j] = valid ? kb : -1;
+    st.inc[j] = inc;
+    if (valid) atomicMax(&st.mx[kb], f2key(inc));
+}
 
-// kStage: both clouds are copied into LDS (LDS-DMA at kernel start) so the
-// scans read them with LDS latency instead of L2/HBM latency (the seed kernel
-// that last touched them ran on other XCDs, whose L2s this CU does not see).
-// (Measured and rejected: the cached ids in LDS with s recomputed from the
-// staged clouds -- fewer L2 round trips, more VALU: 287 -> 294 us.)
-template <bool kStage>
-__global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(
-    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n, float eps, int iters,
-    cid_t *__restrict__ cache_idx, float *__restrict__ cache_s, float *__restrict__ cache_T,
-    const int32_t *__restrict__ bid0,
-    const float *__restrict__ inc0, float *__restrict__ dist, int32_t *__restrict__ assignment_out,
-    float *__restrict__ price_out, int32_t *__restrict__ stats) {
-    extern __shared__ __attribute__((aligned(16))) int smem[];
-    int *sAss = smem;                     // [n] assignment (point -> object)
-    int *sInv = sAss + n;                 // [n] owner (object -> point)
-    float *sPrice = (float *)(sInv + n);  // [n]
-    int *sMax = (int *)(sPrice + n);      // [n] max increment (f2key)
-    int *sClaim = sMax + n;               // [n] lowest qualifying bidder
-    int *sBid = sClaim + n;               // [n] bid object per point
-    float *sInc = (float *)(sBid + n);    // [n] bid increment per point
-    int *sU = (int *)(sInc + n);          // [n] unassigned list
-    int *sMiss = sU + n;                  // [n] points needing a full scan
-    float *sQ = (float *)(sMiss + n);     // [3n] target cloud copy (kStage)
-    float *sP = sQ + 3 * n;               // [3n] bidder cloud copy (kStage)
-    __shared__ int sNu, sNm;
-
-    const int tid = threadIdx.x;
-    const int lane = tid & 63;
-    const int wave = tid >> 6;
-    const int batch = blockIdx.x;
-    const float *Pg = xyz1 + (size_t)batch * n * 3;
-    const float *Qg = xyz2 + (size_t)batch * n * 3;
-    if (kStage) {
-        pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kEmdThreads / 64);
-        pcm_dma_to_lds(sP, Pg, 12 * n, wave, kEmdThreads / 64);
+// One job item (a full scan) by one wave, claimed through its armed ticket.
+// `price` is the job's price snapshot (helpers: LDS copy; master: its state).
+__device__ __forceinline__ void job_item(const EmdWs &ws, size_t base, int i, int g, int j_known, const float *P,
+                                         const float *Qc, const float *price, int n, float eps) {
+    const int lane = threadIdx.x & 63;
+    int ok = 0;
+    if (lane == 0) ok = atomicCAS(ws.iclaim + base + i, -g, g) == -g;
+    ok = __builtin_amdgcn_readfirstlane(ok);
+    if (!ok) return;
+    const int j = j_known >= 0 ? j_known : __builtin_amdgcn_readfirstlane(ld_sc1(ws.ml + base + i));
+    float b1, b2, T;
+    int kb;
+    scan_full(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, price, n, ws.cache + (base + j) * kL, b1, kb, b2, T);
+    if (lane == 0) {
+        st_sc1(ws.CT + base + j, T);
+        st_sc1(ws.rbid + base + i, (int)kb);
+        st_sc1(ws.rinc + base + i, b1 - b2 + eps);
     }
+    vm_drain();  // every store of this wave (cache entries included) has left the CU
+    if (lane == 0) st_sc1(ws.idone + base + i, g);
+}
+
+struct KArgs {
+    const float *xyz1, *xyz2;
+    int b, n, iters, H, offload_min;
+    float eps;
+    float *dist;
+    int32_t *ass_out;
+    float *price_out;
+    int32_t *stats;
+};
+
+// helper role: take full scans of the master's jobs until it quits
+template <bool kStage>
+__device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank, int *smem) {
+    __shared__ int sGen;
+    const int n = a.n;
+    const int tid = threadIdx.x, wave = tid >> 6;
+    float *sQ = (float *)smem;                                       // [3n] (kStage)
+    float *sPH = (float *)smem + (kStage ? 3 * (size_t)n : 0);       // [n] price snapshot
+    const size_t base = (size_t)batch * n;
+    const float *P = a.xyz1 + base * 3;
+    const float *Qg = a.xyz2 + base * 3;
+    int32_t *bw = ws.board + (size_t)batch * kBoardWords;
+    if constexpr (kStage) pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kWaves);
     const float *Qc = kStage ? (const float *)sQ : Qg;
-    const float *P = kStage ? (const float *)sP : Pg;
-    cid_t *C = cache_idx + (size_t)batch * n * kL;
-    float *CS = cache_s + (size_t)batch * n * kL;
-    float *CT = cache_T + (size_t)batch * n;
+    int last = 0;
+    for (;;) {
+        if (tid == 0) {
+            int g = -1;
+            for (int spin = 0; spin < kSpinLimit; ++spin) {
+                if (ld_sc1(bw + kBoardQuit)) break;
+                const int gv = ld_sc1(bw + kBoardGen);
+                if (gv != last) { g = gv; break; }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            sGen = g;
+        }
+        if constexpr (kStage) vm_drain();  // the staged cloud has landed (first pass)
+        __syncthreads();
+        const int g = sGen;
+        if (g < 0) return;
+        const int jn = ld_sc1(bw + kBoardJn);
+        for (int k = tid; k < n; k += kEmdThreads) sPH[k] = ld_sc1(ws.pp + base + k);
+        __syncthreads();
+        for (int i = rank * kWaves + wave; i < jn; i += a.H * kWaves) job_item(ws, base, i, g, -1, P, Qc, sPH, n, a.eps);
+        if (a.stats && tid == 0) atomicAdd(&a.stats[2 * a.iters + 12], 1);  // helper wake-ups
+        last = g;
+        __syncthreads();
+    }
+}
+
+// master role: the auction of one batch element
+template <bool kG, bool kStage>
+__device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *smem) {
+    __shared__ int sNu[2], sNm;
+    const int n = a.n, iters = a.iters;
+    const float eps = a.eps;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const size_t base = (size_t)batch * n;
+    const float *P = a.xyz1 + base * 3;
+    const float *Qg = a.xyz2 + base * 3;
+    int32_t *bw = ws.board + (size_t)batch * kBoardWords;
+    const centry *C = ws.cache + base * kL;
+    const float *CT = ws.CT + base;
+
+    AState<kG> st;
+    char *lp = (char *)smem;
+    if constexpr (!kG) {
+        st.ass = (int *)lp; lp += 4 * (size_t)n;
+        st.inv = (int *)lp; lp += 4 * (size_t)n;
+        st.price = (float *)lp; lp += 4 * (size_t)n;
+        st.mx = (int *)lp; lp += 4 * (size_t)n;
+        st.claim = (ckey *)lp; lp += 8 * (size_t)n;
+        st.bid = (int *)lp; lp += 4 * (size_t)n;
+        st.inc = (float *)lp; lp += 4 * (size_t)n;
+        st.U[0] = (int *)lp; lp += 4 * (size_t)n;
+        st.U[1] = (int *)lp; lp += 4 * (size_t)n;
+        st.miss = (int *)lp; lp += 4 * (size_t)n;
+    } else {
+        st.ass = ws.g_ass + base; st.inv = ws.g_inv + base; st.price = ws.g_price + base;
+        st.mx = ws.g_max + base; st.claim = ws.g_claim + base; st.bid = ws.g_bid + base;
+        st.inc = ws.g_inc + base; st.U[0] = ws.g_u0 + base; st.U[1] = ws.g_u1 + base;
+        st.miss = ws.g_miss + base;
+    }
+    float *sQ = (float *)lp;  // [3n] staged target cloud (kStage)
+    if constexpr (kStage) lp += 12 * (size_t)n;
+    // lane tops of the split scans: 5 words x 64 lanes x 16 waves
+    float *xA1 = (float *)lp, *xA2 = xA1 + kEmdThreads, *xA3 = xA2 + kEmdThreads;
+    int *xQ1 = (int *)(xA3 + kEmdThreads), *xQ2 = xQ1 + kEmdThreads;
+
+    if constexpr (kStage) pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kWaves);
+    const float *Qc = kStage ? (const float *)sQ : Qg;
 
     for (int j = tid; j < n; j += kEmdThreads) {
-        sAss[j] = -1;
-        sInv[j] = -1;
-        sPrice[j] = 0.f;
-        sMax[j] = f2key(0.f);  // emd_module.py:49 zero-inits max_increments
-        sClaim[j] = 0x7fffffff;
+        st.ass[j] = -1;
+        st.inv[j] = -1;
+        st.price[j] = 0.f;
+        st.mx[j] = f2key(0.f);  // emd_module.py:49 zero-inits max_increments
+        st.claim[j] = ~0ull;
+        st.U[0][j] = j;         // iteration 0: every point bids
     }
-    if (tid == 0) { sNu = 0; sNm = 0; }
-    if (kStage) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the DMA has landed
+    if (tid == 0) { sNu[0] = n; sNu[1] = 0; sNm = 0; }
+    if constexpr (kStage) vm_drain();  // the DMA has landed
     __syncthreads();
 
+    int gen = 0;  // jobs posted so far
     // diagnostics only (stats != nullptr): per-phase wall time of batch 0
     unsigned long long tprev = __builtin_amdgcn_s_memrealtime();
     const unsigned long long t_start = tprev;
 #define PCM_EMD_PHASE(i)                                                               \
-    if (stats && tid == 0 && blockIdx.x == 0) {                                        \
+    if (a.stats && tid == 0 && batch == 0) {                                           \
         const unsigned long long tn = __builtin_amdgcn_s_memrealtime();               \
-        atomicAdd(&stats[2 * iters + (i)], (int)(tn - tprev));                         \
+        atomicAdd(&a.stats[2 * iters + (i)], (int)(tn - tprev));                       \
         tprev = tn;                                                                    \
     }
     for (int it = 0; it < iters; ++it) {
         const bool last = (it == iters - 1);
-        // ---- A: compact the unassigned points (order irrelevant downstream)
-        for (int j0 = 0; j0 < n; j0 += kEmdThreads) {
-            const int j = j0 + tid;
-            const bool un = (j < n) && sAss[j] == -1;
-            const unsigned long long bal = __ballot(un);
-            int base = 0;
-            if (lane == 0 && bal) base = atomicAdd(&sNu, __popcll(bal));
-            base = __shfl(base, 0, 64);
-            if (un) sU[base + __popcll(bal & ((1ull << lane) - 1ull))] = j;
-        }
-        __syncthreads();
-        PCM_EMD_PHASE(0);
-        const int nu = sNu;
+        const int cur = it & 1;
+        const int nu = sNu[cur];
         if (nu == 0) break;  // nothing left to bid: later iterations are no-ops
+        const int *Ucur = st.U[cur];
+        int *Unext = st.U[cur ^ 1];
+        // the other list's counter was last read at the start of iteration it-1
+        if (tid == 0) sNu[cur ^ 1] = 0;
 
-        // ---- B1: bids from the caches (16 lanes per point), misses listed
+        // ---- B1: bids from the seed (iteration 0) or the caches; misses listed
         if (it == 0) {
             for (int u = tid; u < nu; u += kEmdThreads) {
-                const int j = sU[u];
-                const int k = bid0[(size_t)batch * n + j];
+                const int j = Ucur[u];
+                const int k = ws.bid0[base + j];
                 if (k >= 0) {
-                    const float inc = inc0[(size_t)batch * n + j];
-                    sBid[j] = k;
-                    sInc[j] = inc;
-                    atomicMax(&sMax[k], f2key(inc));
+                    const float inc = ws.inc0[base + j];
+                    st.bid[j] = k;
+                    st.inc[j] = inc;
+                    atomicMax(&st.mx[k], f2key(inc));
                 } else {
-                    sMiss[atomicAdd(&sNm, 1)] = j;
+                    st.miss[atomicAdd(&sNm, 1)] = j;
                 }
             }
         } else {
             const int G = cache_bid_lanes(nu);
-            if (G == 16) cache_bids<16>(nu, eps, sU, C, CS, CT, sPrice, sBid, sInc, sMax, sMiss, &sNm);
-            else if (G == 8) cache_bids<8>(nu, eps, sU, C, CS, CT, sPrice, sBid, sInc, sMax, sMiss, &sNm);
-            else if (G == 4) cache_bids<4>(nu, eps, sU, C, CS, CT, sPrice, sBid, sInc, sMax, sMiss, &sNm);
-            else if (G == 2) cache_bids<2>(nu, eps, sU, C, CS, CT, sPrice, sBid, sInc, sMax, sMiss, &sNm);
-            else cache_bids<1>(nu, eps, sU, C, CS, CT, sPrice, sBid, sInc, sMax, sMiss, &sNm);
+            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, st, &sNm);
+            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, st, &sNm);
+            else cache_bids<4>(nu, eps, Ucur, C, CT, st, &sNm);
         }
         __syncthreads();
-        if (stats && tid == 0 && blockIdx.x == 0)  // per-iteration cache-bid time of batch 0
-            stats[2 * iters + 16 + it] = (int)(__builtin_amdgcn_s_memrealtime() - tprev);
         PCM_EMD_PHASE(1);
-#ifdef PCM_EMD_DIAG_B2
-        const unsigned long long tB2 = tprev;  // diagnostics build: per-iteration full-scan phase time
-#endif
-        // ---- B2: full scans (one wave per missed point), cache rebuilt
+
+        // ---- B2: full scans of the misses, caches rebuilt
         const int nm = sNm;
-        if (stats && tid == 0) {  // diagnostics: [iter] -> (unassigned, full scans), summed over batches
-            atomicAdd(&stats[2 * it], nu);
-            atomicAdd(&stats[2 * it + 1], nm);
+        if (a.stats && tid == 0) {  // diagnostics: [iter] -> (unassigned, full scans), summed over batches
+            atomicAdd(&a.stats[2 * it], nu);
+            atomicAdd(&a.stats[2 * it + 1], nm);
         }
-        for (int q = wave; q < nm; q += kEmdThreads / 64) {
-            const int j = sMiss[q];
-            float b1, b2, T;
-            int kb;
-            const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
-            cid_t *cj = C + (size_t)j * kL;
-            float *sj = CS + (size_t)j * kL;
-            const unsigned long long ts0 = stats ? __builtin_amdgcn_s_memrealtime() : 0ull;
-            const bool fast_ok = scan_fast(x1, y1, z1, Qc, sPrice, n, cj, sj, b1, kb, b2, T);
-            const unsigned long long ts1 = stats ? __builtin_amdgcn_s_memrealtime() : 0ull;
-            if (!fast_ok) scan_exact(x1, y1, z1, Qc, sPrice, n, cj, sj, b1, kb, b2, T);
-            if (stats && lane == 0) {  // diagnostics: fallbacks; wave-0 scan times of batch 0
-                if (!fast_ok) atomicAdd(&stats[2 * iters + 6], 1);
-                if (blockIdx.x == 0 && wave == 0) {
-                    const unsigned long long ts2 = __builtin_amdgcn_s_memrealtime();
-                    atomicAdd(&stats[2 * iters + 7], 1);
-                    atomicAdd(&stats[2 * iters + 8], (int)(ts1 - ts0));
-                    atomicAdd(&stats[2 * iters + 9], (int)(ts2 - ts1));
+        if (nm > 0) {
+            if (a.H > 0 && nm > a.offload_min) {
+                // publish the job: miss list, armed tickets, price snapshot, size
+                ++gen;
+                for (int i = tid; i < nm; i += kEmdThreads) {
+                    st_sc1(ws.ml + base + i, st.miss[i]);
+                    st_sc1(ws.iclaim + base + i, -gen);
+                }
+                for (int k = tid; k < n; k += kEmdThreads) st_sc1(ws.pp + base + k, st.price[k]);
+                if (tid == 0) st_sc1(bw + kBoardJn, nm);
+                vm_drain();
+                __syncthreads();
+                if (tid == 0) st_sc1(bw + kBoardGen, gen);
+                // take items from the end while the helpers start at the front
+                for (int i = nm - 1 - wave; i >= 0; i -= kWaves)
+                    job_item(ws, base, i, gen, st.miss[i], P, Qc, st.price, n, eps);
+                // collect every item once its done word shows this job
+                for (int i = tid; i < nm; i += kEmdThreads) {
+                    int spin = 0;
+                    while (ld_sc1(ws.idone + base + i) != gen) {
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spin > kSpinLimit) { st_sc1(bw + kBoardErr, 1); break; }
+                    }
+                    const int j = st.miss[i];
+                    const int kb = ld_sc1(ws.rbid + base + i);
+                    place_bid(st, j, kb, ld_sc1(ws.rinc + base + i), n);
+                }
+                if (a.stats && tid == 0) {
+                    atomicAdd(&a.stats[2 * iters + 10], 1);   // jobs
+                    atomicAdd(&a.stats[2 * iters + 11], nm);  // items
+                }
+            } else {
+                // W waves per miss for a few misses (each scans n/W objects, the
+                // lane tops are merged in object order), one wave per miss else
+                const int W = nm <= 4 ? 4 : (nm <= 8 ? 2 : 1);
+                if (W == 1) {
+                    for (int q = wave; q < nm; q += kWaves) {
+                        const int j = st.miss[q];
+                        float b1, b2, T;
+                        int kb;
+                        scan_full(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n,
+                                  ws.cache + (base + j) * kL, b1, kb, b2, T);
+                        if (lane == 0) {
+                            st_sc1(ws.CT + base + j, T);
+                            place_bid(st, j, kb, b1 - b2 + eps, n);
+                        }
+                    }
+                } else {
+                    const int q = wave / W, r = wave - q * W;
+                    const bool act = q < nm;
+                    const int j = act ? st.miss[q] : 0;
+                    const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
+                    LaneTop t;
+                    lane_top_init(t);
+                    const int part = n / W;  // a multiple of 256
+                    if (act) scan_fast_keys(t, x1, y1, z1, Qc, st.price, r * part, (r + 1) * part);
+                    if (act && r != 0) {
+                        xA1[tid] = t.a1; xA2[tid] = t.a2; xA3[tid] = t.a3; xQ1[tid] = t.q1; xQ2[tid] = t.q2;
+                    }
+                    __syncthreads();
+                    if (act && r == 0) {
+                        for (int rr = 1; rr < W; ++rr) {
+                            const int o = tid + 64 * rr;
+                            lane_top_merge(t, xA1[o], xQ1[o], xA2[o], xQ2[o], xA3[o]);
+                        }
+                        float b1, b2, T;
+                        int kb;
+                        centry *cj = ws.cache + (base + j) * kL;
+                        if (!scan_fast_finish(t, x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T))
+                            scan_exact(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
+                        if (lane == 0) {
+                            st_sc1(ws.CT + base + j, T);
+                            place_bid(st, j, kb, b1 - b2 + eps, n);
+                        }
+                    }
                 }
             }
-            if (lane == 0) {
-                CT[j] = T;
-                const float inc = b1 - b2 + eps;
-                const bool valid = (unsigned)kb < (unsigned)n;  // all-NaN values: no bid (oracle: best_i = -1)
-                sBid[j] = valid ? kb : -1;
-                sInc[j] = inc;
-                if (valid) atomicMax(&sMax[kb], f2key(inc));
-            }
+            __syncthreads();
         }
-        __syncthreads();
         PCM_EMD_PHASE(2);
-#ifdef PCM_EMD_DIAG_B2
-        if (stats && tid == 0 && blockIdx.x == 0) stats[2 * iters + 16 + it] = (int)(tprev - tB2);
-#endif
 
         // ---- C: claim -- lowest bidder inside the reference's 1e-6 window
-        for (int u = tid; u < nu; u += kEmdThreads) {
-            const int j = sU[u];
-            const int k = sBid[j];
-            if (k < 0) continue;
-            const double bi = (double)sInc[j];
-            const double mi = (double)key2f(sMax[k]);
-            if (bi - 1e-6 <= mi && mi <= bi + 1e-6) atomicMin(&sClaim[k], j);
+        //      (emd_cuda.cu:181-194); the key carries the iteration
+        const ckey itag = (ckey)(~(unsigned)it) << 32;
+        if (!last) {
+            for (int u = tid; u < nu; u += kEmdThreads) {
+                const int j = Ucur[u];
+                const int k = st.bid[j];
+                if (k < 0) continue;
+                const double bi = (double)st.inc[j];
+                const double mi = (double)key2f(st.ld_max(k));
+                if (bi - 1e-6 <= mi && mi <= bi + 1e-6) atomicMin(&st.claim[k], itag | (unsigned)j);
+            }
+            if (tid == 0) sNm = 0;
+            __syncthreads();
         }
-        __syncthreads();
         PCM_EMD_PHASE(3);
 
-        // ---- D: assign (emd_cuda.cu:196-215).  On the last iteration every
-        // bidder takes its object; prices/owners are then dead state and are
-        // left as they were (the reference's racy updates are unobservable).
-        for (int u = tid; u < nu; u += kEmdThreads) {
-            const int j = sU[u];
-            const int k = sBid[j];
-            if (k < 0) continue;
-            if (last) {
-                sAss[j] = k;
-            } else if (sClaim[k] == j) {
-                const int old = sInv[k];
-                if (old != -1) sAss[old] = -1;
-                sInv[k] = j;
-                sAss[j] = k;
-                sPrice[k] += sInc[j];
-                sMax[k] = f2key(-1e9f);
+        // ---- D: assign (emd_cuda.cu:196-215) and the next bidder list.  On
+        // the last iteration every bidder takes its object; prices/owners are
+        // then dead state and are left as they were (the reference's racy
+        // updates are unobservable).
+        for (int u0 = 0; u0 < nu; u0 += kEmdThreads) {
+            const int u = u0 + tid;
+            int push = -1;
+            if (u < nu) {
+                const int j = Ucur[u];
+                const int k = st.bid[j];
+                if (k < 0) {
+                    push = j;  // no bid: stays unassigned
+                } else if (last) {
+                    st.ass[j] = k;
+                } else if (st.ld_claim(k) == (itag | (unsigned)j)) {
+                    const int old = st.inv[k];
+                    if (old != -1) { st.ass[old] = -1; push = old; }
+                    st.inv[k] = j;
+                    st.ass[j] = k;
+                    st.price[k] += st.inc[j];
+                    st.mx[k] = f2key(-1e9f);
+                } else {
+                    push = j;  // outbid
+                }
+            }
+            if (!last) {
+                const unsigned long long bal = __ballot(push >= 0);
+                int pos = 0;
+                if (lane == 0 && bal) pos = atomicAdd(&sNu[cur ^ 1], __popcll(bal));
+                pos = __shfl(pos, 0, 64);
+                if (push >= 0) Unext[pos + __popcll(bal & ((1ull << lane) - 1ull))] = push;
             }
         }
         __syncthreads();
         PCM_EMD_PHASE(4);
-        for (int u = tid; u < nu; u += kEmdThreads) {
-            const int k = sBid[sU[u]];
-            if (k >= 0) sClaim[k] = 0x7fffffff;
-        }
-        if (tid == 0) { sNu = 0; sNm = 0; }
-        __syncthreads();
-        PCM_EMD_PHASE(5);
     }
+#undef PCM_EMD_PHASE
+    if (a.H > 0 && tid == 0) st_sc1(bw + kBoardQuit, 1);  // helpers exit
+    if (a.stats && tid == 0)  // diagnostics: whole-auction wall time per batch element
+        a.stats[3 * iters + 16 + batch] = (int)(__builtin_amdgcn_s_memrealtime() - t_start);
 
-    if (stats && tid == 0)  // diagnostics: whole-auction wall time per batch element
-        stats[3 * iters + 16 + blockIdx.x] = (int)(__builtin_amdgcn_s_memrealtime() - t_start);
     // ---- CalcDist (emd_cuda.cu:217-226): deltas xyz1 - xyz2
     for (int j = tid; j < n; j += kEmdThreads) {
-        const int k = sAss[j];
+        const int k = st.ass[j];
         float d = 0.f;
         if (k >= 0) {
-            d = pcm_sqd(P[3 * (size_t)j + 0] - Qc[3 * (size_t)k + 0],
-                        P[3 * (size_t)j + 1] - Qc[3 * (size_t)k + 1],
+            d = pcm_sqd(P[3 * (size_t)j + 0] - Qc[3 * (size_t)k + 0], P[3 * (size_t)j + 1] - Qc[3 * (size_t)k + 1],
                         P[3 * (size_t)j + 2] - Qc[3 * (size_t)k + 2]);
         }
-        dist[(size_t)batch * n + j] = d;
-        assignment_out[(size_t)batch * n + j] = k;
-        if (price_out) price_out[(size_t)batch * n + j] = sPrice[j];
+        a.dist[base + j] = d;
+        a.ass_out[base + j] = k;
+        if (a.price_out) a.price_out[base + j] = st.price[j];
     }
+}
+
+// Grid: b masters (blocks 0..b-1) then b*H helpers.  Helper x serves the
+// batch element on its own XCD when b % 8 == 0 (blocks x and x + 8 share one
+// under round-robin dispatch -- speed only, nothing depends on it).
+template <bool kG, bool kStage>
+__global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(KArgs a, EmdWs ws) {
+    extern __shared__ __attribute__((aligned(16))) int smem[];
+    const int x = (int)blockIdx.x;
+    if (x < a.b) {
+        master_loop<kG, kStage>(a, ws, x, smem);
+        return;
+    }
+    const int h = x - a.b;
+    int batch, rank;
+    if (a.b % 8 == 0) {
+        const int per = a.b / 8;
+        batch = (h % 8) + 8 * ((h / 8) % per);
+        rank = (h / 8) / per;
+    } else {
+        batch = h % a.b;
+        rank = h / a.b;
+    }
+    if (rank >= a.H) return;
+    helper_loop<kStage>(a, ws, batch, rank, smem);
 }
 
 __global__ void emd_bwd_kernel(const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n,
@@ -693,61 +930,130 @@ __global__ void emd_bwd_kernel(const float *__restrict__ xyz1, const float *__re
          t += (size_t)gridDim.x * blockDim.x) {
         const size_t batch = t / n;
         const int k = assignment[t];
-        const float g = __fmul_rn(graddist[t], 2.f);
         const float *p = xyz1 + 3 * t;
+        if ((unsigned)k >= (unsigned)n) {
+            // a point the forward left unassigned (all-NaN bid values): no
+            // partner to pull towards -- zero gradient, no out-of-range read
+#pragma unroll
+            for (int c = 0; c < 3; ++c) grad[3 * t + c] = 0.f;
+            continue;
+        }
+        const float g = __fmul_rn(graddist[t], 2.f);
         const float *q = xyz2 + 3 * (batch * n + (size_t)k);
 #pragma unroll
         for (int c = 0; c < 3; ++c) grad[3 * t + c] = __fadd_rn(0.f, __fmul_rn(g, __fsub_rn(p[c], q[c])));
     }
 }
 
-size_t emd_lds_bytes(int n) { return (size_t)9 * 4 * n; }
+// ---- workspace layout
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// workspace layout: cache_idx [b*n*kL] i16 | cache_s [b*n*kL] f32 | cache_T [b*n] f32 |
-//                   bid0 [b*n] i32 | inc0 [b*n] f32
-size_t ws_bytes(int b, int n) {
+size_t ws_layout(int b, int n, EmdWs *w, char *basep) {
     const size_t pts = (size_t)b * n;
-    return pts * kL * (sizeof(cid_t) + 4) + pts * 4 * 3;
+    size_t off = 0;
+    auto take = [&](size_t bytes) -> char * {
+        char *p = basep ? basep + off : nullptr;
+        off = align256(off + bytes);
+        return p;
+    };
+    EmdWs t{};
+    t.cache = (centry *)take(pts * kL * sizeof(centry));
+    t.CT = (float *)take(pts * 4);
+    t.bid0 = (int32_t *)take(pts * 4);
+    t.inc0 = (float *)take(pts * 4);
+    t.board = (int32_t *)take((size_t)b * kBoardWords * 4);
+    t.ml = (int32_t *)take(pts * 4);
+    t.iclaim = (int32_t *)take(pts * 4);
+    t.idone = (int32_t *)take(pts * 4);
+    t.rbid = (int32_t *)take(pts * 4);
+    t.rinc = (float *)take(pts * 4);
+    t.pp = (float *)take(pts * 4);
+    if (n > kLdsStateMaxN) {
+        t.g_ass = (int32_t *)take(pts * 4);
+        t.g_inv = (int32_t *)take(pts * 4);
+        t.g_max = (int32_t *)take(pts * 4);
+        t.g_bid = (int32_t *)take(pts * 4);
+        t.g_u0 = (int32_t *)take(pts * 4);
+        t.g_u1 = (int32_t *)take(pts * 4);
+        t.g_miss = (int32_t *)take(pts * 4);
+        t.g_price = (float *)take(pts * 4);
+        t.g_inc = (float *)take(pts * 4);
+        t.g_claim = (ckey *)take(pts * 8);
+    }
+    if (w) *w = t;
+    return off;
 }
 
 }  // namespace
 
 extern "C" size_t pcm_emd_workspace_bytes(int b, int n) {
     if (b <= 0 || n <= 0) return 0;
-    return ws_bytes(b, n);
+    return ws_layout(b, n, nullptr, nullptr);
 }
 
 namespace {
+int default_helpers(int b, int n) {
+    if (n > kHelperMaxN) return 0;
+    const int h = 256 / b - 1;
+    return h < 0 ? 0 : (h > kMaxHelpers ? kMaxHelpers : h);
+}
+
 int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters, float *dist,
-               int32_t *assignment, float *price, void *workspace, size_t workspace_bytes,
-               int32_t *stats, void *stream) {
+               int32_t *assignment, float *price, void *workspace, size_t workspace_bytes, int helpers,
+               int offload_min, int32_t *stats, void *stream) {
     // emd_cuda.cu:236-249 (n == m is enforced by the single n here)
     if (b < 0 || n < 0 || b > 512 || n % 1024 != 0 || iters < 1) return PCM_ERR_INVALID_ARG;
     if (b == 0 || n == 0) return PCM_OK;
     if (!xyz1 || !xyz2 || !dist || !assignment) return PCM_ERR_INVALID_ARG;
-    if (n > kEmdMaxN) return PCM_ERR_UNSUPPORTED;
-    if (!workspace || workspace_bytes < ws_bytes(b, n)) return PCM_ERR_WORKSPACE;
-    const size_t pts = (size_t)b * n;
-    cid_t *cache_idx = (cid_t *)workspace;
-    float *cache_s = (float *)(cache_idx + pts * kL);
-    float *cache_T = cache_s + pts * kL;
-    int32_t *bid0 = (int32_t *)(cache_T + pts);
-    float *inc0 = (float *)(bid0 + pts);
+    const size_t need = ws_layout(b, n, nullptr, nullptr);
+    if (!workspace || workspace_bytes < need) return PCM_ERR_WORKSPACE;
+    EmdWs ws;
+    ws_layout(b, n, &ws, (char *)workspace);
     hipStream_t s = (hipStream_t)stream;
-    hipLaunchKernelGGL(emd_seed_kernel, dim3((unsigned)(pts / (kSeedThreads / 64))),
-                       dim3(kSeedThreads), 0, s, xyz1, xyz2, n, eps, cache_idx, cache_s, cache_T, bid0, inc0);
-    const bool stage = n <= kEmdStageMaxN;
-    const size_t lds = emd_lds_bytes(n) + (stage ? (size_t)24 * n : 0);
+
+    // seed
+    const bool seed_stage = n <= kStageMaxN;
+    const unsigned seed_blocks = (unsigned)((size_t)b * n / kSeedPts);
+    const size_t seed_lds = seed_stage ? 12 * (size_t)n : 0;
+    if (seed_stage) {
+        if (seed_lds > 64 * 1024 &&
+            hipFuncSetAttribute((const void *)emd_seed_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)seed_lds) != hipSuccess)
+            return PCM_ERR_LAUNCH;
+        hipLaunchKernelGGL(emd_seed_kernel<true>, dim3(seed_blocks), dim3(kSeedThreads), seed_lds, s, xyz1, xyz2,
+                           n, eps, ws);
+    } else {
+        hipLaunchKernelGGL(emd_seed_kernel<false>, dim3(seed_blocks), dim3(kSeedThreads), 0, s, xyz1, xyz2, n, eps,
+                           ws);
+    }
+
+    // auction
+    int H = helpers >= 0 ? helpers : default_helpers(b, n);
+    if (n > kHelperMaxN) H = 0;
+    if (H > kMaxHelpers) H = kMaxHelpers;
+    const bool g_state = n > kLdsStateMaxN;
+    const bool stage = n <= (g_state ? kStageMaxN : kLdsStateMaxN);
+    const size_t xchg = 5 * (size_t)kEmdThreads * 4;
+    const size_t m_lds = (g_state ? 0 : 44 * (size_t)n) + (stage ? 12 * (size_t)n : 0) + xchg;
+    const size_t h_lds = H > 0 ? (stage ? 12 * (size_t)n : 0) + 4 * (size_t)n : 0;
+    size_t lds = m_lds > h_lds ? m_lds : h_lds;
+    // one workgroup per CU when helpers run: a master never shares its SIMDs
+    if (H > 0 && lds < 84 * 1024) lds = 84 * 1024;
+    KArgs ka{xyz1, xyz2, b, n, iters, H, offload_min >= 0 ? offload_min : kDefaultOffloadMin, eps,
+             dist, assignment, price, stats};
+    const unsigned grid = (unsigned)(b * (1 + H));
     auto launch = [&](auto kfn) -> int {
         if (lds > 64 * 1024 &&
             hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
                 hipSuccess)
             return PCM_ERR_LAUNCH;
-        hipLaunchKernelGGL(kfn, dim3(b), dim3(kEmdThreads), lds, s, xyz1, xyz2, n, eps, iters, cache_idx,
-                           cache_s, cache_T, bid0, inc0, dist, assignment, price, stats);
+        hipLaunchKernelGGL(kfn, dim3(grid), dim3(kEmdThreads), lds, s, ka, ws);
         return PCM_OK;
     };
-    const int rc = stage ? launch(emd_auction_kernel<true>) : launch(emd_auction_kernel<false>);
+    int rc;
+    if (!g_state) rc = launch(emd_auction_kernel<false, true>);
+    else if (stage) rc = launch(emd_auction_kernel<true, true>);
+    else rc = launch(emd_auction_kernel<true, false>);
     if (rc != PCM_OK) return rc;
     return pcm_launch_status();
 }
@@ -756,18 +1062,49 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
 extern "C" int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int n, float eps,
                                int iters, float *dist, int32_t *assignment, float *price,
                                void *workspace, size_t workspace_bytes, void *stream) {
-    return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, price, workspace, workspace_bytes,
+    return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, price, workspace, workspace_bytes, -1, -1,
                       nullptr, stream);
 }
 
 // diagnostics: stats[2*it] += unassigned points, stats[2*it+1] += full scans
-// (summed over the batch; caller zero-fills int32[2*iters])
+// (summed over the batch), then 16 counters (phase timers of batch 0 in
+// [1..4], jobs [10], offloaded items [11], helper wake-ups [12]), then the
+// auction wall time of each batch element (caller zero-fills 3*iters+16+b).
+// helpers / offload_min < 0: the defaults.
 extern "C" int pcm_tune_emd_forward_stats(const float *xyz1, const float *xyz2, int b, int n, float eps,
                                           int iters, float *dist, int32_t *assignment,
                                           void *workspace, size_t workspace_bytes, int32_t *stats,
                                           void *stream) {
-    return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, nullptr, workspace,
-                      workspace_bytes, stats, stream);
+    return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, nullptr, workspace, workspace_bytes, -1, -1,
+                      stats, stream);
+}
+
+extern "C" int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
+                                        float *dist, int32_t *assignment, float *price, void *workspace,
+                                        size_t workspace_bytes, int helpers, int offload_min, int32_t *stats,
+                                        void *stream) {
+    return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, price, workspace, workspace_bytes, helpers,
+                      offload_min, stats, stream);
+}
+
+// sticky device-side error of the last pcm_emd_forward on this workspace
+// (a poll that timed out); synchronises `stream`.  Returns PCM_OK or
+// PCM_ERR_LAUNCH.
+extern "C" int pcm_emd_workspace_status(const void *workspace, size_t workspace_bytes, int b, int n,
+                                        void *stream) {
+    if (b <= 0 || n <= 0) return PCM_OK;
+    if (!workspace || workspace_bytes < ws_layout(b, n, nullptr, nullptr)) return PCM_ERR_WORKSPACE;
+    EmdWs ws;
+    ws_layout(b, n, &ws, (char *)workspace);
+    for (int i = 0; i < b; ++i) {
+        int32_t err = 0;
+        if (hipMemcpyAsync(&err, ws.board + (size_t)i * kBoardWords + kBoardErr, 4, hipMemcpyDeviceToHost,
+                           (hipStream_t)stream) != hipSuccess ||
+            hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+            return PCM_ERR_LAUNCH;
+        if (err) return PCM_ERR_LAUNCH;
+    }
+    return PCM_OK;
 }
 
 extern "C" int pcm_emd_backward(const float *xyz1, const float *xyz2, int b, int n,

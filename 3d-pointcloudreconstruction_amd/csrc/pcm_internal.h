@@ -28,6 +28,11 @@ int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, const uint16
 int pcm_tune_emd_forward_stats(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
                                float *dist, int32_t *assignment, void *workspace,
                                size_t workspace_bytes, int32_t *stats, void *stream);
+// helpers: helper workgroups per batch element (-1 = default); offload_min:
+// misses above which an iteration's full scans go to the helpers (-1 = default)
+int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
+                             float *dist, int32_t *assignment, float *price, void *workspace,
+                             size_t workspace_bytes, int helpers, int offload_min, int32_t *stats, void *stream);
 #ifdef __cplusplus
 }
 #endif

@@ -10,8 +10,10 @@ prediction, xyz2 the ground truth, both [B, N, 3] with equal N, N % 1024 == 0,
 B <= 512, coordinates normalised to [0, 1]; only xyz1 gets a gradient; the
 assignment is an approximation and not guaranteed to be a bijection.
 
-The auction runs entirely in libpcm_hip.so (one persistent workgroup per cloud,
-all iterations in-kernel).  Unlike the reference (racy GetMax,
+The auction runs entirely in libpcm_hip.so (one persistent master workgroup per
+cloud runs all iterations in-kernel; helper workgroups take the full scans of
+heavy iterations).  Any N % 1024 == 0 is accepted, as by the reference's
+kernel (emd_cuda.cu:236-249).  Unlike the reference (racy GetMax,
 emd_cuda.cu:188-190) the result is deterministic: bidders tying inside the
 1e-6 window resolve to the lowest point index.
 """
@@ -37,10 +39,20 @@ class emdFunction(Function):
         assert n % 1024 == 0
         assert batchsize <= 512
 
-        if xyz1.device.type != "cuda":
-            raise RuntimeError("emdFunction needs HIP device tensors; there is no CPU path")
-        device = xyz1.device
-        xyz1 = xyz1.contiguous().float()
+        # emd_module.py:41-42 moves both clouds to the GPU itself
+        # (`.contiguous().float().cuda()`); so does this wrapper: to the device
+        # of whichever cloud is already on one, else the current HIP device.
+        # Compute never happens on the host.
+        if xyz1.is_cuda:
+            device = xyz1.device
+        elif xyz2.is_cuda:
+            device = xyz2.device
+        elif torch.cuda.is_available():
+            device = torch.device("cuda", torch.cuda.current_device())
+        else:
+            raise RuntimeError("emdFunction needs a HIP device (none is visible); there is no CPU path")
+        ctx.in_devices = (xyz1.device, xyz2.device)
+        xyz1 = xyz1.contiguous().float().to(device)
         xyz2 = xyz2.contiguous().float().to(device)
         dist = torch.empty(batchsize, n, device=device)
         assignment = torch.empty(batchsize, n, device=device, dtype=torch.int32)
@@ -52,11 +64,12 @@ class emdFunction(Function):
     @staticmethod
     def backward(ctx, graddist, gradidx):
         xyz1, xyz2, assignment = ctx.saved_tensors
-        graddist = graddist.contiguous().float()
+        graddist = graddist.contiguous().float().to(xyz1.device)
         gradxyz1 = torch.empty_like(xyz1)
-        gradxyz2 = torch.zeros_like(xyz2)
         pcm_hip.emd_backward(xyz1, xyz2, graddist, assignment, gradxyz1)
-        return gradxyz1, gradxyz2, None, None
+        # gradients go back to where the inputs came from (autograd requires it)
+        dev1, dev2 = ctx.in_devices
+        return gradxyz1.to(dev1), torch.zeros(xyz2.shape, device=dev2), None, None
 
 
 class emdModule(nn.Module):

@@ -24,7 +24,7 @@ EXPORTED = (
     "pcm_version", "pcm_strerror",
     "pcm_chamfer_forward", "pcm_chamfer_backward",
     "pcm_chamfer_workspace_bytes", "pcm_chamfer_forward_loss",
-    "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward",
+    "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward", "pcm_emd_workspace_status",
     "pcm_chamfer_forward_f16", "pcm_chamfer_backward_f16",
     "pcm_chamfer_loss_grad",
     "pcm_icp_workspace_bytes", "pcm_icp", "pcm_nearest_neighbor", "pcm_best_fit_transform",
@@ -91,6 +91,10 @@ def load_library():
     L.pcm_emd_forward.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, vp, cs, vp]
     L.pcm_emd_backward.restype = ci
     L.pcm_emd_backward.argtypes = [vp, vp, ci, ci, vp, vp, vp, vp]
+    L.pcm_emd_workspace_status.restype = ci
+    L.pcm_emd_workspace_status.argtypes = [vp, cs, ci, ci, vp]
+    L.pcm_tune_emd_forward_cfg.restype = ci
+    L.pcm_tune_emd_forward_cfg.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, vp, cs, ci, ci, vp, vp]
     L.pcm_chamfer_loss_grad.restype = ci
     L.pcm_chamfer_loss_grad.argtypes = [vp, vp, ci, ci, ci, cf, cf, vp, vp, vp, vp, vp, vp, vp, vp, cs, vp]
     L.pcm_tune_chamfer_loss_grad.restype = ci
@@ -177,11 +181,16 @@ def tune_num_chamfer_f16_variants() -> int:
 _ws_cache = {}
 
 
+def _stream_id(dev: torch.device) -> int:
+    return int(torch.cuda.current_stream(dev).cuda_stream)
+
+
 def chamfer_workspace(dev: torch.device, b: int, n: int, m: int) -> torch.Tensor:
-    """Zero-filled, cached per (device, size) workspace for the fused-loss forward
-    (the kernel leaves it zeroed after every stream-ordered call)."""
+    """Zero-filled workspace for the fused-loss kernels, cached per (device,
+    current stream, size): the kernels keep cross-launch state in it (epoch,
+    arrival counters), so only stream-ordered calls may share one."""
     need = int(load_library().pcm_chamfer_workspace_bytes(b, n, m))
-    key = (dev, need)
+    key = ("chamfer", dev, _stream_id(dev), need)
     ws = _ws_cache.get(key)
     if ws is None:
         ws = torch.zeros(need, dtype=torch.uint8, device=dev)
@@ -300,21 +309,51 @@ def emd_workspace_bytes(b: int, n: int) -> int:
     return int(load_library().pcm_emd_workspace_bytes(b, n))
 
 
+def emd_workspace(dev: torch.device, b: int, n: int) -> torch.Tensor:
+    """EMD workspace cached per (device, current stream, size); its content on
+    entry is irrelevant, but a call's auction state lives in it until the call
+    ends, so concurrent calls on different streams get different buffers."""
+    ws_bytes = max(emd_workspace_bytes(b, n), 1)
+    key = ("emd", dev, _stream_id(dev), ws_bytes)
+    ws = _ws_cache.get(key)
+    if ws is None:
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        _ws_cache[key] = ws
+    return ws
+
+
 def emd_forward(xyz1, xyz2, eps: float, iters: int, dist, assignment, price=None,
-                workspace=None) -> None:
+                workspace=None, helpers=None, offload_min=None, stats=None) -> None:
+    """pcm_emd_forward; helpers / offload_min / stats select the tuning entry
+    (helper workgroups per cloud, the miss count above which an iteration's
+    full scans are offloaded, diagnostics) -- None = the library defaults."""
     dev = _require_device(xyz1, xyz2, dist, assignment)
     b, n, _ = xyz1.shape
     ws_bytes = emd_workspace_bytes(b, n)
     if ws_bytes and (workspace is None or workspace.numel() * workspace.element_size() < ws_bytes):
-        key = ("emd", dev, ws_bytes)
-        workspace = _ws_cache.get(key)
-        if workspace is None:  # content on entry is irrelevant to the kernels
-            workspace = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-            _ws_cache[key] = workspace
+        workspace = emd_workspace(dev, b, n)
     with torch.cuda.device(dev):
-        _check(load_library().pcm_emd_forward(
-            _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
-            _ptr(price), _ptr(workspace), ws_bytes, _stream(dev)), "pcm_emd_forward")
+        if helpers is None and offload_min is None and stats is None:
+            _check(load_library().pcm_emd_forward(
+                _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
+                _ptr(price), _ptr(workspace), ws_bytes, _stream(dev)), "pcm_emd_forward")
+        else:
+            if stats is not None and stats.numel() < 3 * int(iters) + 16 + b:
+                raise ValueError("stats needs 3*iters + 16 + B int32 entries")
+            _check(load_library().pcm_tune_emd_forward_cfg(
+                _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
+                _ptr(price), _ptr(workspace), ws_bytes, -1 if helpers is None else int(helpers),
+                -1 if offload_min is None else int(offload_min), _ptr(stats), _stream(dev)),
+                "pcm_tune_emd_forward_cfg")
+
+
+def emd_workspace_status(workspace, b: int, n: int) -> None:
+    """Raise PcmError if the last EMD forward on `workspace` hit a device-side
+    timeout (synchronises the current stream)."""
+    dev = workspace.device
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_emd_workspace_status(_ptr(workspace), workspace.numel(), b, n, _stream(dev)),
+               "pcm_emd_workspace_status")
 
 
 def emd_backward(xyz1, xyz2, graddist, assignment, gradxyz1) -> None:
@@ -337,7 +376,7 @@ def tune_emd_forward_stats(xyz1, xyz2, eps: float, iters: int, dist, assignment,
     dev = _require_device(xyz1, xyz2, dist, assignment, stats)
     b, n, _ = xyz1.shape
     ws_bytes = emd_workspace_bytes(b, n)
-    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+    ws = emd_workspace(dev, b, n)
     with torch.cuda.device(dev):
         _check(load_library().pcm_tune_emd_forward_stats(
             _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),

@@ -1,10 +1,24 @@
-"""Evaluation metrics -- working counterpart of the reference's utils/metrics.py.
+"""Evaluation metrics on the HIP path (counterpart of the reference's utils/metrics.py).
 
-Same ``Metrics`` class surface (utils/metrics.py:10-109): ITEMS, get, items,
-names, _get_emd_distance (EMD x100 with eps=0.005, iters=50) and
-_get_chamfer_distance (CD x100), state_dict, better_than.  The metric modules
-are constructed at class-definition time as in the reference (:16, :24);
-they hold no parameters, so this needs no device.
+Surface kept from utils/metrics.py:10-109, so testnet.py-style callers work unchanged:
+
+  * ``Metrics.ITEMS``: one descriptor per metric with the keys ``name``, ``enabled``,
+    ``eval_func``, ``eval_object``, ``is_greater_better`` and ``init_value``. Callers
+    may switch a metric off through ``enabled``.
+  * ``Metrics.get(pred, gt)`` returns the enabled metrics' values as a list, in
+    table order (EMD first, then CD; testnet.py:69 calls it this way).
+  * ``Metrics.items()`` and ``Metrics.names()``.
+  * ``Metrics._get_emd_distance``: 100 * mean over clouds of mean(sqrt(dist)) from
+    the auction with eps 0.005 and 50 iterations (utils/metrics.py:49-53).
+  * ``Metrics._get_chamfer_distance``: 100 * (mean(dist1) + mean(dist2))
+    (utils/metrics.py:56-60).
+  * ``Metrics(metric_name, values)``, where ``values`` is a list, or a dict keyed
+    by metric name (unknown names are skipped with a warning). Also
+    ``state_dict()``, ``repr()`` and ``better_than(other)``.
+
+The reference builds its two modules with ``.cuda()`` when the class is defined
+(:16, :24). The modules here hold no parameters or state, so no device is touched
+at import time. All compute goes through libpcm_hip.so.
 """
 import logging
 import os
@@ -12,97 +26,96 @@ import sys
 
 import torch
 
-_METRIC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "metric")
-for _p in (os.path.join(_METRIC, "emd"), os.path.join(_METRIC, "chamfer3D")):
-    if _p not in sys.path:
-        sys.path.append(_p)
+_METRIC_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "metric")
+for _sub in ("emd", "chamfer3D"):
+    _path = os.path.join(_METRIC_DIR, _sub)
+    if _path not in sys.path:
+        sys.path.append(_path)
 from dist_chamfer_3D import chamfer_3DDist  # noqa: E402
-import emd_module as emd_func  # noqa: E402
+import emd_module  # noqa: E402
+
+# the evaluation call setting of utils/metrics.py:51 (the training loss uses 0.05 / 3000)
+EVAL_EMD_EPS = 0.005
+EVAL_EMD_ITERS = 50
+_SCALE = 100.0
+
+_log = logging.getLogger(__name__)
+
+
+def _descriptor(name, method, module):
+    # every metric here is a distance: lower is better, and 32767 is the
+    # "not measured yet" placeholder of the reference table
+    return dict(name=name, enabled=True, eval_func=method, eval_object=module,
+                is_greater_better=False, init_value=32767)
 
 
 class Metrics(object):
-    ITEMS = [{
-        'name': 'EMD_distance',
-        'enabled': True,
-        'eval_func': '_get_emd_distance',
-        'eval_object': emd_func.emdModule(),
-        'is_greater_better': False,
-        'init_value': 32767
-    }, {
-        'name': 'ChamferDistance',
-        'enabled': True,
-        'eval_func': '_get_chamfer_distance',
-        'eval_object': chamfer_3DDist(),
-        'is_greater_better': False,
-        'init_value': 32767
-    }]
+    ITEMS = [
+        _descriptor('EMD_distance', '_get_emd_distance', emd_module.emdModule()),
+        _descriptor('ChamferDistance', '_get_chamfer_distance', chamfer_3DDist()),
+    ]
 
-    @classmethod
-    def get(cls, pred, gt):
-        _items = cls.items()
-        _values = [0] * len(_items)
-        for i, item in enumerate(_items):
-            _values[i] = getattr(cls, item['eval_func'])(pred, gt)
-        return _values
-
+    # ---- class-level evaluation -------------------------------------------------
     @classmethod
     def items(cls):
-        return [i for i in cls.ITEMS if i['enabled']]
+        return list(filter(lambda d: d['enabled'], cls.ITEMS))
 
     @classmethod
     def names(cls):
-        return [i['name'] for i in cls.items()]
+        return [d['name'] for d in cls.items()]
+
+    @classmethod
+    def get(cls, pred, gt):
+        return [getattr(cls, d['eval_func'])(pred, gt) for d in cls.items()]
+
+    @classmethod
+    def _module(cls, method):
+        for d in cls.ITEMS:
+            if d['eval_func'] == method:
+                return d['eval_object']
+        raise KeyError(method)
 
     @classmethod
     def _get_emd_distance(cls, pred, gt):
-        emd_distance = cls.ITEMS[0]['eval_object']
-        emd_1, _ = emd_distance(pred, gt, eps=0.005, iters=50)
-        emd_loss = torch.sqrt(emd_1).mean(1).mean()
-        return emd_loss.item() * 100
+        dist, _ = cls._module('_get_emd_distance')(pred, gt, eps=EVAL_EMD_EPS, iters=EVAL_EMD_ITERS)
+        per_cloud = dist.sqrt().mean(dim=1)
+        return float(per_cloud.mean()) * _SCALE
 
     @classmethod
     def _get_chamfer_distance(cls, pred, gt):
-        chamfer_distance = cls.ITEMS[1]['eval_object']
-        dist1, dist2, idx1, idx2 = chamfer_distance(pred, gt)
-        chamfer_loss = torch.mean(dist1) + torch.mean(dist2)
-        return chamfer_loss.item() * 100
+        d1, d2, _, _ = cls._module('_get_chamfer_distance')(pred, gt)
+        return float(d1.mean() + d2.mean()) * _SCALE
 
+    # ---- a recorded set of metric values ---------------------------------------
     def __init__(self, metric_name, values):
-        self._items = Metrics.items()
-        self._values = [item['init_value'] for item in self._items]
         self.metric_name = metric_name
-
-        if type(values).__name__ == 'list':
+        self._items = Metrics.items()
+        slot = {d['name']: i for i, d in enumerate(self._items)}
+        if isinstance(values, list):
             self._values = values
-        elif type(values).__name__ == 'dict':
-            metric_indexes = {}
-            for idx, item in enumerate(self._items):
-                metric_indexes[item['name']] = idx
-            for k, v in values.items():
-                if k not in metric_indexes:
-                    logging.warning('Ignore Metric[Name=%s] due to disability.' % k)
-                    continue
-                self._values[metric_indexes[k]] = v
+        elif isinstance(values, dict):
+            self._values = [d['init_value'] for d in self._items]
+            for key, val in values.items():
+                if key in slot:
+                    self._values[slot[key]] = val
+                else:
+                    _log.warning('metric %r is not enabled; value dropped', key)
         else:
             raise Exception('Unsupported value type: %s' % type(values))
 
     def state_dict(self):
-        return {self._items[i]['name']: self._values[i] for i in range(len(self._items))}
+        return dict(zip((d['name'] for d in self._items), self._values))
 
     def __repr__(self):
-        return str(self.state_dict())
+        return repr(self.state_dict())
 
     def better_than(self, other):
         if other is None:
             return True
-        _index = -1
-        for i, _item in enumerate(self._items):
-            if _item['name'] == self.metric_name:
-                _index = i
-                break
-        if _index == -1:
+        pos = next((i for i, d in enumerate(self._items) if d['name'] == self.metric_name), None)
+        if pos is None:
             raise Exception('Invalid metric name to compare.')
-        _metric = self._items[_index]
-        _value = self._values[_index]
-        other_value = other._values[_index]
-        return _value > other_value if _metric['is_greater_better'] else _value < other_value
+        mine, theirs = self._values[pos], other._values[pos]
+        if self._items[pos]['is_greater_better']:
+            return mine > theirs
+        return mine < theirs

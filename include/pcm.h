@@ -151,15 +151,23 @@ size_t pcm_emd_workspace_bytes(int b, int n);
  * bidders tying within the reference's 1e-6 window resolve to the lowest
  * point index (the reference lets a racing writer win).  Requirements as the
  * reference (emd_cuda.cu:236-249): both clouds [b, n, 3] (same n), b <= 512,
- * n % 1024 == 0; iters >= 1.  Outputs dist [b, n] (squared distance to the
- * assigned point) and assignment [b, n] (int32; not guaranteed a bijection).
- * `workspace` must hold pcm_emd_workspace_bytes(b, n) bytes; its content on
- * entry is irrelevant.  `price` may be NULL; otherwise it receives the final
+ * n % 1024 == 0 (any such n); iters >= 1.  Outputs dist [b, n] (squared
+ * distance to the assigned point) and assignment [b, n] (int32; not
+ * guaranteed a bijection).  `workspace` must hold pcm_emd_workspace_bytes(b, n)
+ * bytes; its content on entry is irrelevant; calls that share a workspace must
+ * be stream-ordered.  `price` may be NULL; otherwise it receives the final
  * object prices [b, n] (diagnostics / parity tests).
  */
 int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
                     float *dist, int32_t *assignment, float *price,
                     void *workspace, size_t workspace_bytes, void *stream);
+
+/*
+ * Device-side failure of the last pcm_emd_forward on `workspace` (a bounded
+ * wait between its workgroups that timed out; the outputs are then invalid):
+ * PCM_OK or PCM_ERR_LAUNCH.  Synchronises `stream` (it reads device memory).
+ */
+int pcm_emd_workspace_status(const void *workspace, size_t workspace_bytes, int b, int n, void *stream);
 
 /*
  * EMD backward (emd_cuda.cu:284-316): gradxyz1[j] = 2*graddist[j]*(xyz1[j] - xyz2[a[j]]).

@@ -55,6 +55,110 @@ def test_emd_forward_matches_oracle(cuda, oracle, b, n, eps, iters, seed):
     assert ((ass >= 0) & (ass < n)).all()
 
 
+@pytest.mark.parametrize("b,n,eps,iters,seed", [
+    (2, 8192, 0.005, 50, 10),     # beyond the LDS-resident auction state (workspace state, staged cloud)
+    (1, 16384, 0.005, 30, 11),    # workspace state, cloud read from global memory
+    (3, 3072, 0.05, 300, 12),     # n not a power of two
+])
+def test_emd_large_n_matches_oracle(cuda, oracle, b, n, eps, iters, seed):
+    # the reference accepts any N % 1024 == 0 (emd_cuda.cu:97-133, 236-249)
+    a, c = _clouds(seed, b, n)
+    dist, ass, price = _run(a, c, eps, iters, cuda)
+    rd, ra, rp, _ = oracle.emd_forward(a.numpy(), c.numpy(), eps, iters, with_stats=True)
+    np.testing.assert_array_equal(ass, ra)
+    np.testing.assert_array_equal(dist.view(np.int32), rd.view(np.int32))
+    np.testing.assert_array_equal(price.view(np.int32), rp.view(np.int32))
+
+
+def _generator_like(seed, b, n):
+    """Clustered predictions against uniform ground truth: the shape of a
+    random-init generator's output (tests/test_train_gpu.py), where most bids
+    need full scans and the helpers take them."""
+    g = torch.Generator().manual_seed(seed)
+    centers = torch.rand(b, 8, 3, generator=g) * 0.6 + 0.2
+    pick = torch.randint(0, 8, (b, n), generator=g)
+    pred = torch.gather(centers, 1, pick[..., None].expand(b, n, 3)) + 0.03 * torch.randn(b, n, 3, generator=g)
+    return pred.clamp(0, 1).contiguous(), torch.rand(b, n, 3, generator=g)
+
+
+@pytest.mark.parametrize("helpers,offload_min", [(-1, -1), (0, -1), (3, 0), (31, 0), (15, 4)])
+def test_emd_helper_configs_match_oracle(cuda, oracle, helpers, offload_min):
+    # every helper count / offload threshold gives the same auction
+    import pcm_hip
+    a, c = _generator_like(20, 4, 1024)
+    b, n = 4, 1024
+    x1, x2 = a.to(cuda), c.to(cuda)
+    dist = torch.empty(b, n, device=cuda)
+    ass = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    price = torch.empty(b, n, device=cuda)
+    stats = torch.zeros(3 * 400 + 16 + b, dtype=torch.int32, device=cuda)
+    pcm_hip.emd_forward(x1, x2, 0.05, 400, dist, ass, price, helpers=helpers, offload_min=offload_min, stats=stats)
+    torch.cuda.synchronize()
+    rd, ra, rp, _ = oracle.emd_forward(a.numpy(), c.numpy(), 0.05, 400, with_stats=True)
+    np.testing.assert_array_equal(ass.cpu().numpy(), ra)
+    np.testing.assert_array_equal(dist.cpu().numpy().view(np.int32), rd.view(np.int32))
+    np.testing.assert_array_equal(price.cpu().numpy().view(np.int32), rp.view(np.int32))
+    st = stats.cpu().numpy()
+    if helpers != 0 and offload_min == 0:
+        assert st[2 * 400 + 10] > 0, "no job was offloaded"
+    if helpers == 0:
+        assert st[2 * 400 + 10] == 0
+
+
+def test_emd_generator_like_training_call(cuda, oracle):
+    # loss/loss.py:23 setting on clustered predictions (the 13 ms case of round 1)
+    a, c = _generator_like(21, 16, 1024)
+    dist, ass, price = _run(a, c, 0.05, 3000, cuda)
+    rd, ra, rp, _ = oracle.emd_forward(a.numpy(), c.numpy(), 0.05, 3000, with_stats=True)
+    np.testing.assert_array_equal(ass, ra)
+    np.testing.assert_array_equal(dist.view(np.int32), rd.view(np.int32))
+    np.testing.assert_array_equal(price.view(np.int32), rp.view(np.int32))
+
+
+def test_emd_workspace_status_ok(cuda):
+    import pcm_hip
+    a, c = _clouds(22, 2, 1024)
+    x1, x2 = a.to(cuda), c.to(cuda)
+    dist = torch.empty(2, 1024, device=cuda)
+    ass = torch.empty(2, 1024, dtype=torch.int32, device=cuda)
+    ws = pcm_hip.emd_workspace(cuda, 2, 1024)
+    pcm_hip.emd_forward(x1, x2, 0.005, 50, dist, ass, workspace=ws)
+    pcm_hip.emd_workspace_status(ws, 2, 1024)  # raises on a device-side timeout
+
+
+def test_emd_host_inputs_move_to_device(cuda, oracle):
+    # emd_module.py:41-42: the reference calls .cuda() on its inputs itself
+    import emd_module
+    a, c = _clouds(23, 2, 1024)
+    x1 = a.clone().requires_grad_(True)  # host tensor
+    dist, ass = emd_module.emdModule()(x1, c, 0.005, 50)
+    assert dist.is_cuda and ass.is_cuda
+    rd, ra = oracle.emd_forward(a.numpy(), c.numpy(), 0.005, 50)
+    np.testing.assert_array_equal(ass.cpu().numpy(), ra)
+    dist.sum().backward()
+    assert x1.grad is not None and x1.grad.device.type == "cpu"
+    rg = oracle.emd_backward(a.numpy(), c.numpy(), np.ones((2, 1024), np.float32), ra)
+    np.testing.assert_array_equal(x1.grad.numpy().view(np.int32), rg.view(np.int32))
+
+
+def test_emd_backward_unassigned_point_is_zero(cuda):
+    # a point left unassigned (assignment -1, e.g. an all-NaN bid) must not
+    # read before xyz2 (ADVICE r1): zero gradient instead
+    import pcm_hip
+    a, c = _clouds(24, 2, 1024)
+    x1, x2 = a.to(cuda), c.to(cuda)
+    ass = torch.arange(1024, dtype=torch.int32, device=cuda).repeat(2, 1)
+    ass[0, 0] = -1
+    ass[1, 5] = -1
+    gd = torch.ones(2, 1024, device=cuda)
+    g = torch.empty(2, 1024, 3, device=cuda)
+    pcm_hip.emd_backward(x1, x2, gd, ass, g)
+    torch.cuda.synchronize()
+    assert (g[0, 0] == 0).all() and (g[1, 5] == 0).all()
+    ref = 2 * (x1 - x2)
+    assert torch.equal(g[0, 1:], ref[0, 1:])
+
+
 def test_emd_module_api_and_backward(cuda, oracle):
     import emd_module
     a, c = _clouds(7, 4, 1024)

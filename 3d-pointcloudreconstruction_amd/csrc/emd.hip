@@ -75,6 +75,7 @@ constexpr int kMaxHelpers = 31;
 constexpr int kBoardWords = 32;      // per batch element: gen, quit, jn, err (128-B line each group)
 constexpr int kSpinLimit = 1 << 22;  // bounded polls (sticky error word on timeout)
 constexpr int kDefaultOffloadMin = 24;  // misses above which an iteration is offloaded
+constexpr int kDefaultWsplit = 1;       // most waves one miss's scan is split over (2, 4: measured slower at config 3 and the training call)
 
 typedef unsigned long long centry;   // low 32 bits: object id (-1 unused), high 32: s bits
 typedef unsigned long long ckey;     // claim key: (~it) << 32 | point
@@ -122,60 +123,6 @@ __device__ __forceinline__ float value_of(float d, float price) {
     return value_from_s(__builtin_sqrtf(d), price);  // correctly rounded sqrtf
 }
 
-// (a better than b) in bid order: larger value, then lower index
-__device__ __forceinline__ bool vk_better(float va, int ka, float vb, int kb) {
-    return va > vb || (va == vb && ka < kb);
-}
-
-// Top-2 triples (b1, k1, b2): best value, its (lowest) id, second largest
-// value of the multiset.  Written as one asm block each: as C++ ternaries
-// hipcc emits exec-mask branches plus NaN-canonicalising v_max pairs here.
-// "Better" = larger value, then lower id (vk_better).  The trailing s_nop
-// covers the VALU-write -> DPP-read hazard of the next reduction step, and
-// the one before v_cndmask the VALU/SALU-SGPR-write -> lane-mask read.
-//
-// merge of two triples: b2 = max(min(b1, o1), max(b2, o2)), b1 = max(b1, o1)
-__device__ __forceinline__ void top2_merge(float &b1, int &k1, float &b2, float o1, int ok1, float o2) {
-    unsigned long long g, e, l;
-    float t, u, n1, n2;
-    asm("v_cmp_gt_f32_e64 %[g], %[o1], %[b1]\n\t"
-        "v_cmp_eq_f32_e64 %[e], %[o1], %[b1]\n\t"
-        "v_cmp_lt_i32_e64 %[l], %[ok1], %[k1]\n\t"
-        "v_min_f32 %[t], %[b1], %[o1]\n\t"
-        "v_max_f32 %[u], %[b2], %[o2]\n\t"
-        "v_max_f32 %[n1], %[b1], %[o1]\n\t"
-        "v_max_f32 %[n2], %[t], %[u]\n\t"
-        "s_and_b64 %[e], %[e], %[l]\n\t"
-        "s_or_b64 %[g], %[g], %[e]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e64 %[k1], %[k1], %[ok1], %[g]\n\t"
-        "s_nop 1"
-        : [k1] "+v"(k1), [t] "=&v"(t), [u] "=&v"(u), [n1] "=&v"(n1), [n2] "=&v"(n2), [g] "=&s"(g),
-          [e] "=&s"(e), [l] "=&s"(l)
-        : [o1] "v"(o1), [ok1] "v"(ok1), [o2] "v"(o2), [b1] "v"(b1), [b2] "v"(b2));
-    b1 = n1;
-    b2 = n2;
-}
-// push of one entry (v, k): b2 = med3(b1, b2, v), b1 = max(b1, v)
-__device__ __forceinline__ void top2_push(float &b1, int &k1, float &b2, float v, int k) {
-    unsigned long long g, e, l;
-    float n1, n2;
-    asm("v_cmp_gt_f32_e64 %[g], %[v], %[b1]\n\t"
-        "v_cmp_eq_f32_e64 %[e], %[v], %[b1]\n\t"
-        "v_cmp_lt_i32_e64 %[l], %[k], %[k1]\n\t"
-        "v_med3_f32 %[n2], %[b1], %[b2], %[v]\n\t"
-        "v_max_f32 %[n1], %[b1], %[v]\n\t"
-        "s_and_b64 %[e], %[e], %[l]\n\t"
-        "s_or_b64 %[g], %[g], %[e]\n\t"
-        "s_nop 1\n\t"
-        "v_cndmask_b32_e64 %[k1], %[k1], %[k], %[g]\n\t"
-        "s_nop 1"
-        : [k1] "+v"(k1), [n1] "=&v"(n1), [n2] "=&v"(n2), [g] "=&s"(g), [e] "=&s"(e), [l] "=&s"(l)
-        : [v] "v"(v), [k] "v"(k), [b1] "v"(b1), [b2] "v"(b2));
-    b1 = n1;
-    b2 = n2;
-}
-
 // ---- DPP cross-lane steps (VALU operand modifiers: no LDS crossbar round trip).
 // Lanes the DPP pattern does not feed keep their own value (old = self), so a
 // combine with it is a no-op for idempotent selections.  Hillis-Steele:
@@ -192,14 +139,6 @@ template <int CTRL, int ROWMASK>
 __device__ __forceinline__ float dpp_f(float x) {
     return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, ROWMASK,
                                                       0xf, false));
-}
-
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ void dpp_top2_step(float &b1, int &k1, float &b2) {
-    const float ob1 = dpp_f<CTRL, ROWMASK>(b1);
-    const int ok1 = dpp_i<CTRL, ROWMASK>(k1);
-    const float ob2 = dpp_f<CTRL, ROWMASK>(b2);
-    top2_merge(b1, k1, b2, ob1, ok1, ob2);
 }
 
 // full-wave reductions: result returned wave-uniform (read from lane 63)
@@ -307,23 +246,55 @@ __device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float 
     return Kstar;
 }
 
+__device__ __forceinline__ int wave_min_i(int v) {
+    v = min(v, dpp_i<kDppRowShr1, 0xf>(v));
+    v = min(v, dpp_i<kDppRowShr2, 0xf>(v));
+    v = min(v, dpp_i<kDppRowShr4, 0xf>(v));
+    v = min(v, dpp_i<kDppRowShr8, 0xf>(v));
+    v = min(v, dpp_i<kDppRowBcast15, 0xa>(v));
+    v = min(v, dpp_i<kDppRowBcast31, 0xc>(v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 // exact (best, argbest, better) over the wave: each lane offers up to two
-// (value, id) entries; result wave-uniform
+// (value, id) entries; result wave-uniform.  Three single-instruction DPP
+// reductions instead of a top-2 merge per step: best = max, argbest = the
+// lowest id among the entries equal to best, better = best again when two
+// entries tie at best, else the max of the rest (the multiset's second).
 __device__ __forceinline__ void wave_top2(float v1, int k1, float v2, int k2, float &b1, int &kb, float &b2) {
-    if (vk_better(v2, k2, v1, k1)) {
-        const float tv = v1; v1 = v2; v2 = tv;
-        const int tk = k1; k1 = k2; k2 = tk;
-    }
-    b1 = v1; kb = k1; b2 = v2;
-    dpp_top2_step<kDppRowShr1, 0xf>(b1, kb, b2);
-    dpp_top2_step<kDppRowShr2, 0xf>(b1, kb, b2);
-    dpp_top2_step<kDppRowShr4, 0xf>(b1, kb, b2);
-    dpp_top2_step<kDppRowShr8, 0xf>(b1, kb, b2);
-    dpp_top2_step<kDppRowBcast15, 0xa>(b1, kb, b2);
-    dpp_top2_step<kDppRowBcast31, 0xc>(b1, kb, b2);
-    b1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b1), 63));
-    kb = __builtin_amdgcn_readlane(kb, 63);
-    b2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(b2), 63));
+    b1 = wave_max(fmaxf(v1, v2));
+    const bool e1 = v1 == b1, e2 = v2 == b1;
+    kb = wave_min_i(min(e1 ? k1 : 0x7fffffff, e2 ? k2 : 0x7fffffff));
+    const int ties = __popcll(__ballot(e1)) + __popcll(__ballot(e2));
+    b2 = ties >= 2 ? b1 : wave_max(fmaxf(e1 ? -PCM_INF : v1, e2 ? -PCM_INF : v2));
+}
+
+// ---- all-reduce inside aligned groups of G lanes (G = 4, 8, 16) with
+// butterfly DPP permutations: every lane of the group gets the result
+constexpr int kQuadXor1 = 0xB1, kQuadXor2 = 0x4E, kRowHalfMirror = 0x141, kRowMirror = 0x140;
+template <int G>
+__device__ __forceinline__ float group_max(float v) {
+    v = fmaxf(v, dpp_f<kQuadXor1, 0xf>(v));
+    v = fmaxf(v, dpp_f<kQuadXor2, 0xf>(v));
+    if constexpr (G >= 8) v = fmaxf(v, dpp_f<kRowHalfMirror, 0xf>(v));
+    if constexpr (G >= 16) v = fmaxf(v, dpp_f<kRowMirror, 0xf>(v));
+    return v;
+}
+template <int G>
+__device__ __forceinline__ int group_min_i(int v) {
+    v = min(v, dpp_i<kQuadXor1, 0xf>(v));
+    v = min(v, dpp_i<kQuadXor2, 0xf>(v));
+    if constexpr (G >= 8) v = min(v, dpp_i<kRowHalfMirror, 0xf>(v));
+    if constexpr (G >= 16) v = min(v, dpp_i<kRowMirror, 0xf>(v));
+    return v;
+}
+template <int G>
+__device__ __forceinline__ int group_add_i(int v) {
+    v += dpp_i<kQuadXor1, 0xf>(v);
+    v += dpp_i<kQuadXor2, 0xf>(v);
+    if constexpr (G >= 8) v += dpp_i<kRowHalfMirror, 0xf>(v);
+    if constexpr (G >= 16) v += dpp_i<kRowMirror, 0xf>(v);
+    return v;
 }
 
 // ---- seed: key = -d (every price is 0: the bid value is monotone
@@ -351,6 +322,7 @@ __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const fl
 
 // ---- auction full scan, exact: key = the exact bid value.  Always exact
 // bid (the lanes' top-2 hold the global top-2); T = K*.
+template <bool kSc1>
 __device__ __noinline__ void scan_exact(float x1, float y1, float z1, const float *Qc, const float *price, int n,
                                         centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T) {
     const int lane = threadIdx.x & 63;
@@ -367,7 +339,7 @@ __device__ __noinline__ void scan_exact(float x1, float y1, float z1, const floa
         for (int r = 0; r < 4; ++r) lane_top_push(t, key[r], k0 + 64 * r);
     }
     bool s1, s2;
-    T = select_cache<true>(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cache, s1, s2);
+    T = select_cache<kSc1>(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cache, s1, s2);
     wave_top2(t.a1, t.q1, t.a2, t.q2, b1, kb, b2);
 }
 
@@ -398,12 +370,13 @@ __device__ __forceinline__ void scan_fast_keys(LaneTop &t, float x1, float y1, f
 
 // selection, bound and exact bid from the lanes' approximate-key tops;
 // returns false when the exact scan is needed
+template <bool kSc1>
 __device__ __forceinline__ bool scan_fast_finish(const LaneTop &t, float x1, float y1, float z1, const float *Qc,
                                                  const float *price, int n, centry *__restrict__ cache, float &b1,
                                                  int &kb, float &b2, float &T) {
     bool s1, s2;
     const float d1 = entry_d(x1, y1, z1, Qc, n, t.q1), d2 = entry_d(x1, y1, z1, Qc, n, t.q2);
-    const float Kp = select_cache<true>(t, d1, d2, cache, s1, s2);
+    const float Kp = select_cache<kSc1>(t, d1, d2, cache, s1, s2);
     T = Kp + 4.f * 1.1920929e-7f * (6.f + fabsf(Kp));  // +inf stays +inf
     const float v1 = s1 ? value_of(d1, price[t.q1]) : -PCM_INF;
     const float v2 = s2 ? value_of(d2, price[t.q2]) : -PCM_INF;
@@ -412,21 +385,28 @@ __device__ __forceinline__ bool scan_fast_finish(const LaneTop &t, float x1, flo
 }
 
 // one wave: the full bid of point (x1, y1, z1) with a rebuilt cache
+template <bool kSc1>
 __device__ __forceinline__ void scan_full(float x1, float y1, float z1, const float *Qc, const float *price, int n,
                                           centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T) {
     LaneTop t;
     lane_top_init(t);
     scan_fast_keys(t, x1, y1, z1, Qc, price, 0, n);
-    if (!scan_fast_finish(t, x1, y1, z1, Qc, price, n, cache, b1, kb, b2, T))
-        scan_exact(x1, y1, z1, Qc, price, n, cache, b1, kb, b2, T);
+    if (!scan_fast_finish<kSc1>(t, x1, y1, z1, Qc, price, n, cache, b1, kb, b2, T))
+        scan_exact<kSc1>(x1, y1, z1, Qc, price, n, cache, b1, kb, b2, T);
 }
 
 // ===========================================================================
 // Workspace
 // ===========================================================================
+// Two cache regions: A is written by the seed kernel and the master only
+// (plain stores and loads, L2-resident); B by the helpers only (sc1 stores,
+// read by the master with sc1 loads), so no XCD ever holds a dirty line of
+// the other's region.  CT[j] == kInB marks a point whose cache is in B.
 struct EmdWs {
-    centry *cache;   // [b*n*kL]
-    float *CT;       // [b*n] cache bound
+    centry *cache;   // [b*n*kL] region A
+    float *CT;       // [b*n] cache bound (A) or the kInB marker
+    centry *cacheB;  // [b*n*kL] region B
+    float *CTB;      // [b*n] cache bound (B)
     int32_t *bid0;   // [b*n] iteration-0 bid (-2: full scan needed)
     float *inc0;     // [b*n]
     int32_t *board;  // [b*kBoardWords]: gen, quit, jn, err (one 128-B line each)
@@ -442,6 +422,7 @@ struct EmdWs {
     ckey *g_claim;
 };
 constexpr int kBoardGen = 0, kBoardQuit = 8, kBoardJn = 16, kBoardErr = 24;
+constexpr unsigned kInB = 0x7fc0b00bu;  // a quiet NaN no bound ever equals
 
 // ===========================================================================
 // 1. seed kernel: iteration-0 bids + caches, one wave per point, 16 points
@@ -449,12 +430,23 @@ constexpr int kBoardGen = 0, kBoardQuit = 8, kBoardJn = 16, kBoardErr = 24;
 // ===========================================================================
 template <bool kStage>
 __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__restrict__ xyz1,
-                                                                const float *__restrict__ xyz2, int n, float eps,
-                                                                EmdWs ws) {
+                                                                const float *__restrict__ xyz2, int b, int n,
+                                                                float eps, EmdWs ws) {
     extern __shared__ __attribute__((aligned(16))) float sQs[];
     const int wgs_per_batch = n / kSeedPts;
-    const int blk = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
-    const int batch = blk / wgs_per_batch;
+    // batch element i's workgroups go to the XCD its master (block i of the
+    // auction launch) runs on, so the caches are written into the L2 the
+    // master reads them from (round-robin placement: speed only)
+    int batch, chunk;
+    if (b % 8 == 0) {
+        const int x = (int)blockIdx.x, sx = x / 8;
+        batch = (x % 8) + 8 * (sx / wgs_per_batch);
+        chunk = sx % wgs_per_batch;
+    } else {
+        const int blk = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
+        batch = blk / wgs_per_batch;
+        chunk = blk - batch * wgs_per_batch;
+    }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const float *Pg = xyz1 + (size_t)batch * n * 3;
     const float *Qg = xyz2 + (size_t)batch * n * 3;
@@ -464,7 +456,7 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__r
         __syncthreads();
     }
     const float *Qc = kStage ? (const float *)sQs : Qg;
-    const int j0 = (blk - batch * wgs_per_batch) * kSeedPts + wave * kSeedPtsPerWave;
+    const int j0 = chunk * kSeedPts + wave * kSeedPtsPerWave;
     for (int p = 0; p < kSeedPtsPerWave; ++p) {
         const int j = j0 + p;
         const size_t pt = (size_t)batch * n + j;
@@ -497,7 +489,7 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__r
 // form (a plain load could hit a stale L1 line).
 template <bool kG>
 struct AState {
-    int *ass, *inv, *mx, *bid, *U[2], *miss;
+    int *ass, *inv, *mx, *bid, *U0, *U1, *miss;
     float *price, *inc;
     ckey *claim;
     __device__ __forceinline__ int ld_max(int k) const {
@@ -518,9 +510,21 @@ __device__ __forceinline__ int cache_bid_lanes(int nu) {
     return nu <= 64 ? 16 : (nu <= 256 ? 8 : 4);
 }
 
+// A bid on object k.  Maxima persisted from earlier iterations are <= 0
+// (0 initially, -1e9 once assigned), and with eps > 0 every increment is > 0,
+// so an old maximum above 0 means a second bid on k in this iteration: the
+// claim phase is needed only when some object saw that (*coll).
+template <bool kG>
+__device__ __forceinline__ void bid_on(const AState<kG> &st, int j, int k, float inc, int *coll) {
+    st.bid[j] = k;
+    st.inc[j] = inc;
+    if (atomicMax(&st.mx[k], f2key(inc)) > 0) *coll = 1;
+}
+
 template <int G, bool kG>
 __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, const centry *C, const float *CT,
-                                           const AState<kG> &st, int *sNm) {
+                                           const centry *CB, const float *CTB, const AState<kG> &st, int *sNm,
+                                           int *coll) {
     static_assert(G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
     constexpr int E = kL / G;
     const int gi = threadIdx.x / G, gl = threadIdx.x % G;
@@ -528,32 +532,52 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
         const int u = u0 + gi;
         const bool act = u < nu;
         const int j = act ? Ucur[u] : 0;
-        const float tj = ld_sc1(CT + j);
+        // region A (the master's own, plain, L2-resident) is loaded together
+        // with the bound; a point whose cache a helper rebuilt (marker) is
+        // re-read from region B (sc1)
+        float tj = CT[j];
         centry ce[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) ce[e] = ld_sc1(C + (size_t)j * kL + gl + G * e);  // helpers write them
-        float b1 = -PCM_INF, b2 = -PCM_INF;
-        int kb = 0x7fffffff;
+        for (int e = 0; e < E; ++e) ce[e] = C[(size_t)j * kL + gl + G * e];
+        if (__float_as_uint(tj) == kInB) {
+            tj = ld_sc1(CTB + j);
+#pragma unroll
+            for (int e = 0; e < E; ++e) ce[e] = ld_sc1(CB + (size_t)j * kL + gl + G * e);
+        }
+        // values at current prices; an unused slot (k = -1) evaluates object
+        // 0 and is then forced to (-inf, INT_MAX), branch-free
+        float v[E];
+        int kk[E];
+        float lmax = -PCM_INF;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
-            // branch-free: an unused slot (k = -1) evaluates object 0 and is
-            // then forced to (-inf, INT_MAX)
             const int k = (int)(unsigned)ce[e];
             const float s = __uint_as_float((unsigned)(ce[e] >> 32));
             const int neg = k >> 31;
             const float v0 = value_from_s(s, st.price[k & ~neg]);
-            const float v = __int_as_float((__float_as_int(v0) & ~neg) | (int)(0xff800000u & (unsigned)neg));
-            top2_push(b1, kb, b2, v, k & 0x7fffffff);
+            v[e] = __int_as_float((__float_as_int(v0) & ~neg) | (int)(0xff800000u & (unsigned)neg));
+            kk[e] = k & 0x7fffffff;
+            lmax = fmaxf(lmax, v[e]);
         }
-        if constexpr (G >= 2) dpp_top2_step<kDppRowShr1, 0xf>(b1, kb, b2);
-        if constexpr (G >= 4) dpp_top2_step<kDppRowShr2, 0xf>(b1, kb, b2);
-        if constexpr (G >= 8) dpp_top2_step<kDppRowShr4, 0xf>(b1, kb, b2);
-        if constexpr (G >= 16) dpp_top2_step<kDppRowShr8, 0xf>(b1, kb, b2);
+        // group top-2: best = max, argbest = lowest id at best, better = best
+        // on a tie else the max of the rest
+        const float b1 = group_max<G>(lmax);
+        int lk = 0x7fffffff, lc = 0;
+        float lrest = -PCM_INF;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const bool eq = v[e] == b1;
+            lk = eq ? min(lk, kk[e]) : lk;
+            lc += eq ? 1 : 0;
+            lrest = eq ? lrest : fmaxf(lrest, v[e]);
+        }
+        const int kb = group_min_i<G>(lk);
+        const int ties = group_add_i<G>(lc);
+        const float rest = group_max<G>(lrest);
+        const float b2 = ties >= 2 ? b1 : rest;
         if (act && gl == G - 1) {
             if (b2 > tj) {
-                st.bid[j] = kb;
-                st.inc[j] = b1 - b2 + eps;
-                atomicMax(&st.mx[kb], f2key(b1 - b2 + eps));
+                bid_on(st, j, kb, b1 - b2 + eps, coll);
             } else {
                 st.miss[atomicAdd(sNm, 1)] = j;
             }
@@ -563,28 +587,35 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
 
 // a bid produced by a full scan, placed by the scanning wave's lane 0
 template <bool kG>
-__device__ __forceinline__ void place_bid(const AState<kG> &st, int j, int kb, float inc, int n) {
-    const bool valid = (unsigned)kb < (unsigned)n;  // all-NaN values: no bid (oracle: best_i = -1)
-    st.bid[j] = valid ? kb : -1;
-    st.inc[j] = inc;
-    if (valid) atomicMax(&st.mx[kb], f2key(inc));
+__device__ __forceinline__ void place_bid(const AState<kG> &st, int j, int kb, float inc, int n, int *coll) {
+    if ((unsigned)kb < (unsigned)n) {
+        bid_on(st, j, kb, inc, coll);
+    } else {  // all-NaN values: no bid (oracle: best_i = -1)
+        st.bid[j] = -1;
+        st.inc[j] = inc;
+    }
 }
 
-// One job item (a full scan) by one wave, claimed through its armed ticket.
-// `price` is the job's price snapshot (helpers: LDS copy; master: its state).
-__device__ __forceinline__ void job_item(const EmdWs &ws, size_t base, int i, int g, int j_known, const float *P,
-                                         const float *Qc, const float *price, int n, float eps) {
-    const int lane = threadIdx.x & 63;
+// claim of job item i for generation g through its armed ticket (one wave)
+__device__ __forceinline__ bool claim_item(const EmdWs &ws, size_t base, int i, int g) {
     int ok = 0;
-    if (lane == 0) ok = atomicCAS(ws.iclaim + base + i, -g, g) == -g;
-    ok = __builtin_amdgcn_readfirstlane(ok);
-    if (!ok) return;
-    const int j = j_known >= 0 ? j_known : __builtin_amdgcn_readfirstlane(ld_sc1(ws.ml + base + i));
+    if ((threadIdx.x & 63) == 0) ok = atomicCAS(ws.iclaim + base + i, -g, g) == -g;
+    return __builtin_amdgcn_readfirstlane(ok) != 0;
+}
+
+// helper side of a job item: full scan with the snapshot prices, cache into
+// region B, result words, then the done word (sc1 throughout)
+__device__ __forceinline__ void helper_item(const EmdWs &ws, size_t base, int i, int g, const float *P,
+                                            const float *Qc, const float *price, int n, float eps) {
+    const int lane = threadIdx.x & 63;
+    if (!claim_item(ws, base, i, g)) return;
+    const int j = __builtin_amdgcn_readfirstlane(ld_sc1(ws.ml + base + i));
     float b1, b2, T;
     int kb;
-    scan_full(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, price, n, ws.cache + (base + j) * kL, b1, kb, b2, T);
+    scan_full<true>(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, price, n, ws.cacheB + (base + j) * kL, b1, kb, b2,
+                    T);
     if (lane == 0) {
-        st_sc1(ws.CT + base + j, T);
+        st_sc1(ws.CTB + base + j, T);
         st_sc1(ws.rbid + base + i, (int)kb);
         st_sc1(ws.rinc + base + i, b1 - b2 + eps);
     }
@@ -594,13 +625,18 @@ __device__ __forceinline__ void job_item(const EmdWs &ws, size_t base, int i, in
 
 struct KArgs {
     const float *xyz1, *xyz2;
-    int b, n, iters, H, offload_min;
+    int b, n, iters, H, offload_min, diag, wmax;
     float eps;
     float *dist;
     int32_t *ass_out;
     float *price_out;
     int32_t *stats;
 };
+
+// diagnostics (stats != nullptr): diag 1 = per-iteration (unassigned, full
+// scans) summed over the batch plus job counters (atomics: they perturb the
+// timing); diag 2 = phase timers of batch 0 in registers, written at the end
+constexpr int kDiagHist = 1, kDiagTimers = 2;
 
 // helper role: take full scans of the master's jobs until it quits
 template <bool kStage>
@@ -635,26 +671,28 @@ __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank
         const int jn = ld_sc1(bw + kBoardJn);
         for (int k = tid; k < n; k += kEmdThreads) sPH[k] = ld_sc1(ws.pp + base + k);
         __syncthreads();
-        for (int i = rank * kWaves + wave; i < jn; i += a.H * kWaves) job_item(ws, base, i, g, -1, P, Qc, sPH, n, a.eps);
-        if (a.stats && tid == 0) atomicAdd(&a.stats[2 * a.iters + 12], 1);  // helper wake-ups
+        for (int i = rank * kWaves + wave; i < jn; i += a.H * kWaves) helper_item(ws, base, i, g, P, Qc, sPH, n, a.eps);
+        if (a.diag == kDiagHist && tid == 0) atomicAdd(&a.stats[2 * a.iters + 12], 1);  // helper wake-ups
         last = g;
         __syncthreads();
     }
 }
 
 // master role: the auction of one batch element
-template <bool kG, bool kStage>
+template <bool kG, bool kStage, bool kStageP>
 __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *smem) {
-    __shared__ int sNu[2], sNm;
+    __shared__ int sNu[2], sNm, sColl;
     const int n = a.n, iters = a.iters;
     const float eps = a.eps;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const size_t base = (size_t)batch * n;
-    const float *P = a.xyz1 + base * 3;
+    const float *Pg = a.xyz1 + base * 3;
     const float *Qg = a.xyz2 + base * 3;
     int32_t *bw = ws.board + (size_t)batch * kBoardWords;
-    const centry *C = ws.cache + base * kL;
-    const float *CT = ws.CT + base;
+    centry *C = ws.cache + base * kL;
+    float *CT = ws.CT + base;
+    const bool hist = a.diag == kDiagHist;
+    const bool timers = a.diag == kDiagTimers && batch == 0 && tid == 0;
 
     AState<kG> st;
     char *lp = (char *)smem;
@@ -666,23 +704,27 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         st.claim = (ckey *)lp; lp += 8 * (size_t)n;
         st.bid = (int *)lp; lp += 4 * (size_t)n;
         st.inc = (float *)lp; lp += 4 * (size_t)n;
-        st.U[0] = (int *)lp; lp += 4 * (size_t)n;
-        st.U[1] = (int *)lp; lp += 4 * (size_t)n;
+        st.U0 = (int *)lp; lp += 4 * (size_t)n;
+        st.U1 = (int *)lp; lp += 4 * (size_t)n;
         st.miss = (int *)lp; lp += 4 * (size_t)n;
     } else {
         st.ass = ws.g_ass + base; st.inv = ws.g_inv + base; st.price = ws.g_price + base;
         st.mx = ws.g_max + base; st.claim = ws.g_claim + base; st.bid = ws.g_bid + base;
-        st.inc = ws.g_inc + base; st.U[0] = ws.g_u0 + base; st.U[1] = ws.g_u1 + base;
+        st.inc = ws.g_inc + base; st.U0 = ws.g_u0 + base; st.U1 = ws.g_u1 + base;
         st.miss = ws.g_miss + base;
     }
     float *sQ = (float *)lp;  // [3n] staged target cloud (kStage)
     if constexpr (kStage) lp += 12 * (size_t)n;
+    float *sP = (float *)lp;  // [3n] staged bidder cloud (kStageP)
+    if constexpr (kStageP) lp += 12 * (size_t)n;
     // lane tops of the split scans: 5 words x 64 lanes x 16 waves
     float *xA1 = (float *)lp, *xA2 = xA1 + kEmdThreads, *xA3 = xA2 + kEmdThreads;
     int *xQ1 = (int *)(xA3 + kEmdThreads), *xQ2 = xQ1 + kEmdThreads;
 
     if constexpr (kStage) pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kWaves);
+    if constexpr (kStageP) pcm_dma_to_lds(sP, Pg, 12 * n, wave, kWaves);
     const float *Qc = kStage ? (const float *)sQ : Qg;
+    const float *P = kStageP ? (const float *)sP : Pg;
 
     for (int j = tid; j < n; j += kEmdThreads) {
         st.ass[j] = -1;
@@ -690,29 +732,45 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         st.price[j] = 0.f;
         st.mx[j] = f2key(0.f);  // emd_module.py:49 zero-inits max_increments
         st.claim[j] = ~0ull;
-        st.U[0][j] = j;         // iteration 0: every point bids
+        st.U0[j] = j;           // iteration 0: every point bids
     }
-    if (tid == 0) { sNu[0] = n; sNu[1] = 0; sNm = 0; }
-    if constexpr (kStage) vm_drain();  // the DMA has landed
+    if (tid == 0) { sNu[0] = n; sNu[1] = 0; sNm = 0; sColl = 0; }
+    vm_drain();  // the DMA has landed
     __syncthreads();
 
+    // the master's own full scan of point j: cache region A, bid placed
+    auto own_scan = [&](int j) {
+        float b1, b2, T;
+        int kb;
+        scan_full<false>(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, C + (size_t)j * kL, b1, kb, b2, T);
+        if (lane == 0) {
+            CT[j] = T;
+            place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
+        }
+    };
+
     int gen = 0;  // jobs posted so far
-    // diagnostics only (stats != nullptr): per-phase wall time of batch 0
-    unsigned long long tprev = __builtin_amdgcn_s_memrealtime();
-    const unsigned long long t_start = tprev;
-#define PCM_EMD_PHASE(i)                                                               \
-    if (a.stats && tid == 0 && batch == 0) {                                           \
-        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();               \
-        atomicAdd(&a.stats[2 * iters + (i)], (int)(tn - tprev));                       \
-        tprev = tn;                                                                    \
+    // timers (diag 2): cycles of batch 0 per phase, kept by thread 0
+    unsigned long long tm[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tprev = __builtin_amdgcn_s_memtime();
+    const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
+#define PCM_EMD_PHASE(i)                                                  \
+    if (timers) {                                                         \
+        const unsigned long long tn = __builtin_amdgcn_s_memtime();      \
+        tm[i] += tn - tprev;                                              \
+        tprev = tn;                                                       \
     }
+    int active = 0;
     for (int it = 0; it < iters; ++it) {
         const bool last = (it == iters - 1);
         const int cur = it & 1;
         const int nu = sNu[cur];
         if (nu == 0) break;  // nothing left to bid: later iterations are no-ops
-        const int *Ucur = st.U[cur];
-        int *Unext = st.U[cur ^ 1];
+        ++active;
+        // (two named arrays, not an indexed pair: the selected pointer keeps
+        // its address space and the list reads stay ds_read, not flat loads)
+        const int *Ucur = cur ? st.U1 : st.U0;
+        int *Unext = cur ? st.U0 : st.U1;
         // the other list's counter was last read at the start of iteration it-1
         if (tid == 0) sNu[cur ^ 1] = 0;
 
@@ -722,26 +780,25 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 const int j = Ucur[u];
                 const int k = ws.bid0[base + j];
                 if (k >= 0) {
-                    const float inc = ws.inc0[base + j];
-                    st.bid[j] = k;
-                    st.inc[j] = inc;
-                    atomicMax(&st.mx[k], f2key(inc));
+                    bid_on(st, j, k, ws.inc0[base + j], &sColl);
                 } else {
                     st.miss[atomicAdd(&sNm, 1)] = j;
                 }
             }
         } else {
+            const centry *CB = ws.cacheB + base * kL;
+            const float *CTB = ws.CTB + base;
             const int G = cache_bid_lanes(nu);
-            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, st, &sNm);
-            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, st, &sNm);
-            else cache_bids<4>(nu, eps, Ucur, C, CT, st, &sNm);
+            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl);
+            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl);
+            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl);
         }
         __syncthreads();
-        PCM_EMD_PHASE(1);
+        PCM_EMD_PHASE(0);
 
         // ---- B2: full scans of the misses, caches rebuilt
         const int nm = sNm;
-        if (a.stats && tid == 0) {  // diagnostics: [iter] -> (unassigned, full scans), summed over batches
+        if (hist && tid == 0) {
             atomicAdd(&a.stats[2 * it], nu);
             atomicAdd(&a.stats[2 * it + 1], nm);
         }
@@ -758,40 +815,40 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 vm_drain();
                 __syncthreads();
                 if (tid == 0) st_sc1(bw + kBoardGen, gen);
-                // take items from the end while the helpers start at the front
-                for (int i = nm - 1 - wave; i >= 0; i -= kWaves)
-                    job_item(ws, base, i, gen, st.miss[i], P, Qc, st.price, n, eps);
-                // collect every item once its done word shows this job
+                PCM_EMD_PHASE(4);
+                // take items from the end while the helpers start at the front;
+                // an item the master scans itself goes to region A and is
+                // marked (miss entry negated) so the collection skips it
+                for (int i = nm - 1 - wave; i >= 0; i -= kWaves) {
+                    if (!claim_item(ws, base, i, gen)) continue;
+                    const int j = st.miss[i];
+                    own_scan(j);
+                    if (lane == 0) st.miss[i] = -1 - j;
+                }
+                __syncthreads();
+                PCM_EMD_PHASE(5);
+                // collect the helpers' items once their done words show this job
                 for (int i = tid; i < nm; i += kEmdThreads) {
+                    const int j = st.miss[i];
+                    if (j < 0) continue;
                     int spin = 0;
                     while (ld_sc1(ws.idone + base + i) != gen) {
                         __builtin_amdgcn_s_sleep(1);
                         if (++spin > kSpinLimit) { st_sc1(bw + kBoardErr, 1); break; }
                     }
-                    const int j = st.miss[i];
-                    const int kb = ld_sc1(ws.rbid + base + i);
-                    place_bid(st, j, kb, ld_sc1(ws.rinc + base + i), n);
+                    CT[j] = __uint_as_float(kInB);
+                    place_bid(st, j, ld_sc1(ws.rbid + base + i), ld_sc1(ws.rinc + base + i), n, &sColl);
                 }
-                if (a.stats && tid == 0) {
+                if (hist && tid == 0) {
                     atomicAdd(&a.stats[2 * iters + 10], 1);   // jobs
                     atomicAdd(&a.stats[2 * iters + 11], nm);  // items
                 }
             } else {
                 // W waves per miss for a few misses (each scans n/W objects, the
                 // lane tops are merged in object order), one wave per miss else
-                const int W = nm <= 4 ? 4 : (nm <= 8 ? 2 : 1);
+                const int W = (nm <= 4 && a.wmax >= 4) ? 4 : ((nm <= 8 && a.wmax >= 2) ? 2 : 1);
                 if (W == 1) {
-                    for (int q = wave; q < nm; q += kWaves) {
-                        const int j = st.miss[q];
-                        float b1, b2, T;
-                        int kb;
-                        scan_full(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n,
-                                  ws.cache + (base + j) * kL, b1, kb, b2, T);
-                        if (lane == 0) {
-                            st_sc1(ws.CT + base + j, T);
-                            place_bid(st, j, kb, b1 - b2 + eps, n);
-                        }
-                    }
+                    for (int q = wave; q < nm; q += kWaves) own_scan(st.miss[q]);
                 } else {
                     const int q = wave / W, r = wave - q * W;
                     const bool act = q < nm;
@@ -804,32 +861,38 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     if (act && r != 0) {
                         xA1[tid] = t.a1; xA2[tid] = t.a2; xA3[tid] = t.a3; xQ1[tid] = t.q1; xQ2[tid] = t.q2;
                     }
+                    PCM_EMD_PHASE(4);
                     __syncthreads();
+                    PCM_EMD_PHASE(5);
                     if (act && r == 0) {
                         for (int rr = 1; rr < W; ++rr) {
                             const int o = tid + 64 * rr;
                             lane_top_merge(t, xA1[o], xQ1[o], xA2[o], xQ2[o], xA3[o]);
                         }
+                        PCM_EMD_PHASE(6);
                         float b1, b2, T;
                         int kb;
-                        centry *cj = ws.cache + (base + j) * kL;
-                        if (!scan_fast_finish(t, x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T))
-                            scan_exact(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
+                        centry *cj = C + (size_t)j * kL;
+                        if (!scan_fast_finish<false>(t, x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T))
+                            scan_exact<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
                         if (lane == 0) {
-                            st_sc1(ws.CT + base + j, T);
-                            place_bid(st, j, kb, b1 - b2 + eps, n);
+                            CT[j] = T;
+                            place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
                         }
+                        PCM_EMD_PHASE(7);
                     }
                 }
             }
             __syncthreads();
         }
-        PCM_EMD_PHASE(2);
+        PCM_EMD_PHASE(1);
 
         // ---- C: claim -- lowest bidder inside the reference's 1e-6 window
-        //      (emd_cuda.cu:181-194); the key carries the iteration
+        //      (emd_cuda.cu:181-194); the key carries the iteration.  Skipped
+        //      when every bid object has a single bidder (it then wins).
         const ckey itag = (ckey)(~(unsigned)it) << 32;
-        if (!last) {
+        const bool solo = sColl == 0 && eps > 0.f;
+        if (!last && !solo) {
             for (int u = tid; u < nu; u += kEmdThreads) {
                 const int j = Ucur[u];
                 const int k = st.bid[j];
@@ -838,10 +901,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 const double mi = (double)key2f(st.ld_max(k));
                 if (bi - 1e-6 <= mi && mi <= bi + 1e-6) atomicMin(&st.claim[k], itag | (unsigned)j);
             }
-            if (tid == 0) sNm = 0;
             __syncthreads();
         }
-        PCM_EMD_PHASE(3);
+        PCM_EMD_PHASE(2);
 
         // ---- D: assign (emd_cuda.cu:196-215) and the next bidder list.  On
         // the last iteration every bidder takes its object; prices/owners are
@@ -857,7 +919,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     push = j;  // no bid: stays unassigned
                 } else if (last) {
                     st.ass[j] = k;
-                } else if (st.ld_claim(k) == (itag | (unsigned)j)) {
+                } else if (solo || st.ld_claim(k) == (itag | (unsigned)j)) {
                     const int old = st.inv[k];
                     if (old != -1) { st.ass[old] = -1; push = old; }
                     st.inv[k] = j;
@@ -868,6 +930,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     push = j;  // outbid
                 }
             }
+            if (tid == 0) { sNm = 0; sColl = 0; }  // read before the last barrier
             if (!last) {
                 const unsigned long long bal = __ballot(push >= 0);
                 int pos = 0;
@@ -877,12 +940,16 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             }
         }
         __syncthreads();
-        PCM_EMD_PHASE(4);
+        PCM_EMD_PHASE(3);
     }
 #undef PCM_EMD_PHASE
     if (a.H > 0 && tid == 0) st_sc1(bw + kBoardQuit, 1);  // helpers exit
     if (a.stats && tid == 0)  // diagnostics: whole-auction wall time per batch element
         a.stats[3 * iters + 16 + batch] = (int)(__builtin_amdgcn_s_memrealtime() - t_start);
+    if (timers) {
+        for (int i = 0; i < 12; ++i) a.stats[2 * iters + i] = (int)(tm[i] >> 4);  // units of 16 cycles
+        a.stats[2 * iters + 12] = active;
+    }
 
     // ---- CalcDist (emd_cuda.cu:217-226): deltas xyz1 - xyz2
     for (int j = tid; j < n; j += kEmdThreads) {
@@ -901,12 +968,12 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
 // Grid: b masters (blocks 0..b-1) then b*H helpers.  Helper x serves the
 // batch element on its own XCD when b % 8 == 0 (blocks x and x + 8 share one
 // under round-robin dispatch -- speed only, nothing depends on it).
-template <bool kG, bool kStage>
+template <bool kG, bool kStage, bool kStageP>
 __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(KArgs a, EmdWs ws) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
     const int x = (int)blockIdx.x;
     if (x < a.b) {
-        master_loop<kG, kStage>(a, ws, x, smem);
+        master_loop<kG, kStage, kStageP>(a, ws, x, smem);
         return;
     }
     const int h = x - a.b;
@@ -959,6 +1026,8 @@ size_t ws_layout(int b, int n, EmdWs *w, char *basep) {
     EmdWs t{};
     t.cache = (centry *)take(pts * kL * sizeof(centry));
     t.CT = (float *)take(pts * 4);
+    t.cacheB = (centry *)take(pts * kL * sizeof(centry));
+    t.CTB = (float *)take(pts * 4);
     t.bid0 = (int32_t *)take(pts * 4);
     t.inc0 = (float *)take(pts * 4);
     t.board = (int32_t *)take((size_t)b * kBoardWords * 4);
@@ -1000,7 +1069,7 @@ int default_helpers(int b, int n) {
 
 int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters, float *dist,
                int32_t *assignment, float *price, void *workspace, size_t workspace_bytes, int helpers,
-               int offload_min, int32_t *stats, void *stream) {
+               int offload_min, int diag, int wsplit, int32_t *stats, void *stream) {
     // emd_cuda.cu:236-249 (n == m is enforced by the single n here)
     if (b < 0 || n < 0 || b > 512 || n % 1024 != 0 || iters < 1) return PCM_ERR_INVALID_ARG;
     if (b == 0 || n == 0) return PCM_OK;
@@ -1021,10 +1090,10 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
                                 (int)seed_lds) != hipSuccess)
             return PCM_ERR_LAUNCH;
         hipLaunchKernelGGL(emd_seed_kernel<true>, dim3(seed_blocks), dim3(kSeedThreads), seed_lds, s, xyz1, xyz2,
-                           n, eps, ws);
+                           b, n, eps, ws);
     } else {
-        hipLaunchKernelGGL(emd_seed_kernel<false>, dim3(seed_blocks), dim3(kSeedThreads), 0, s, xyz1, xyz2, n, eps,
-                           ws);
+        hipLaunchKernelGGL(emd_seed_kernel<false>, dim3(seed_blocks), dim3(kSeedThreads), 0, s, xyz1, xyz2, b, n,
+                           eps, ws);
     }
 
     // auction
@@ -1034,13 +1103,16 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     const bool g_state = n > kLdsStateMaxN;
     const bool stage = n <= (g_state ? kStageMaxN : kLdsStateMaxN);
     const size_t xchg = 5 * (size_t)kEmdThreads * 4;
-    const size_t m_lds = (g_state ? 0 : 44 * (size_t)n) + (stage ? 12 * (size_t)n : 0) + xchg;
+    const bool stage_p = n <= (g_state ? 4096 : 1024);
+    const size_t m_lds = (g_state ? 0 : 44 * (size_t)n) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
+                         xchg;
     const size_t h_lds = H > 0 ? (stage ? 12 * (size_t)n : 0) + 4 * (size_t)n : 0;
     size_t lds = m_lds > h_lds ? m_lds : h_lds;
     // one workgroup per CU when helpers run: a master never shares its SIMDs
     if (H > 0 && lds < 84 * 1024) lds = 84 * 1024;
-    KArgs ka{xyz1, xyz2, b, n, iters, H, offload_min >= 0 ? offload_min : kDefaultOffloadMin, eps,
-             dist, assignment, price, stats};
+    KArgs ka{xyz1, xyz2, b, n, iters, H, offload_min >= 0 ? offload_min : kDefaultOffloadMin,
+             stats ? (diag == kDiagTimers ? kDiagTimers : kDiagHist) : 0,
+             wsplit > 0 ? wsplit : kDefaultWsplit, eps, dist, assignment, price, stats};
     const unsigned grid = (unsigned)(b * (1 + H));
     auto launch = [&](auto kfn) -> int {
         if (lds > 64 * 1024 &&
@@ -1051,9 +1123,11 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
         return PCM_OK;
     };
     int rc;
-    if (!g_state) rc = launch(emd_auction_kernel<false, true>);
-    else if (stage) rc = launch(emd_auction_kernel<true, true>);
-    else rc = launch(emd_auction_kernel<true, false>);
+    if (!g_state) rc = stage_p ? launch(emd_auction_kernel<false, true, true>)
+                               : launch(emd_auction_kernel<false, true, false>);
+    else if (stage) rc = stage_p ? launch(emd_auction_kernel<true, true, true>)
+                                 : launch(emd_auction_kernel<true, true, false>);
+    else rc = launch(emd_auction_kernel<true, false, false>);
     if (rc != PCM_OK) return rc;
     return pcm_launch_status();
 }
@@ -1062,29 +1136,24 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
 extern "C" int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int n, float eps,
                                int iters, float *dist, int32_t *assignment, float *price,
                                void *workspace, size_t workspace_bytes, void *stream) {
-    return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, price, workspace, workspace_bytes, -1, -1,
-                      nullptr, stream);
+    return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, price, workspace, workspace_bytes, -1, -1, 0,
+                      0, nullptr, stream);
 }
 
-// diagnostics: stats[2*it] += unassigned points, stats[2*it+1] += full scans
-// (summed over the batch), then 16 counters (phase timers of batch 0 in
-// [1..4], jobs [10], offloaded items [11], helper wake-ups [12]), then the
-// auction wall time of each batch element (caller zero-fills 3*iters+16+b).
-// helpers / offload_min < 0: the defaults.
-extern "C" int pcm_tune_emd_forward_stats(const float *xyz1, const float *xyz2, int b, int n, float eps,
-                                          int iters, float *dist, int32_t *assignment,
-                                          void *workspace, size_t workspace_bytes, int32_t *stats,
-                                          void *stream) {
-    return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, nullptr, workspace, workspace_bytes, -1, -1,
-                      stats, stream);
-}
-
+// Tuning / diagnostics entry.  helpers, offload_min < 0: the defaults.
+// stats (caller zero-fills 3*iters + 16 + b int32) with diag 1: stats[2*it] +=
+// unassigned points, stats[2*it+1] += full scans (summed over the batch),
+// stats[2*iters + 10/11/12] = jobs / offloaded items / helper wake-ups; with
+// diag 2: stats[2*iters + 0..7] = batch-0 phase cycles / 16 (bids, full scans,
+// claim, assign; sub-phases 4..7), stats[2*iters + 8] = iterations with
+// bidders.  Both: stats[3*iters + 16 + i] = auction wall time of batch
+// element i (10 ns units).  (diag 1's atomics perturb the timing.)
 extern "C" int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
                                         float *dist, int32_t *assignment, float *price, void *workspace,
-                                        size_t workspace_bytes, int helpers, int offload_min, int32_t *stats,
-                                        void *stream) {
+                                        size_t workspace_bytes, int helpers, int offload_min, int diag,
+                                        int wsplit, int32_t *stats, void *stream) {
     return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, price, workspace, workspace_bytes, helpers,
-                      offload_min, stats, stream);
+                      offload_min, diag, wsplit, stats, stream);
 }
 
 // sticky device-side error of the last pcm_emd_forward on this workspace

@@ -25,14 +25,14 @@ int pcm_tune_read_stamps(unsigned long long *host, int nblocks);  // profiling b
 int pcm_tune_num_chamfer_f16_variants(void);
 int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
                                  float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, void *stream);
-int pcm_tune_emd_forward_stats(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
-                               float *dist, int32_t *assignment, void *workspace,
-                               size_t workspace_bytes, int32_t *stats, void *stream);
 // helpers: helper workgroups per batch element (-1 = default); offload_min:
-// misses above which an iteration's full scans go to the helpers (-1 = default)
+// misses above which an iteration's full scans go to the helpers (-1 =
+// default); diag: 1 = per-iteration counts, 2 = phase timers (csrc/emd.hip);
+// wsplit: most waves a full scan is split over (1, 2, 4; <= 0 = default)
 int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
                              float *dist, int32_t *assignment, float *price, void *workspace,
-                             size_t workspace_bytes, int helpers, int offload_min, int32_t *stats, void *stream);
+                             size_t workspace_bytes, int helpers, int offload_min, int diag, int wsplit,
+                             int32_t *stats, void *stream);
 #ifdef __cplusplus
 }
 #endif

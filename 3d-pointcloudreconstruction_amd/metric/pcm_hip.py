@@ -75,8 +75,6 @@ def load_library():
     L.pcm_tune_chamfer_backward.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
     L.pcm_tune_chamfer_forward_loss.restype = ci
     L.pcm_tune_chamfer_forward_loss.argtypes = [ci, ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, cs, vp]
-    L.pcm_tune_emd_forward_stats.restype = ci
-    L.pcm_tune_emd_forward_stats.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, cs, vp, vp]
     L.pcm_chamfer_forward_f16.restype = ci
     L.pcm_chamfer_forward_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
     L.pcm_chamfer_backward_f16.restype = ci
@@ -94,7 +92,7 @@ def load_library():
     L.pcm_emd_workspace_status.restype = ci
     L.pcm_emd_workspace_status.argtypes = [vp, cs, ci, ci, vp]
     L.pcm_tune_emd_forward_cfg.restype = ci
-    L.pcm_tune_emd_forward_cfg.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, vp, cs, ci, ci, vp, vp]
+    L.pcm_tune_emd_forward_cfg.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, vp, cs, ci, ci, ci, ci, vp, vp]
     L.pcm_chamfer_loss_grad.restype = ci
     L.pcm_chamfer_loss_grad.argtypes = [vp, vp, ci, ci, ci, cf, cf, vp, vp, vp, vp, vp, vp, vp, vp, cs, vp]
     L.pcm_tune_chamfer_loss_grad.restype = ci
@@ -323,17 +321,18 @@ def emd_workspace(dev: torch.device, b: int, n: int) -> torch.Tensor:
 
 
 def emd_forward(xyz1, xyz2, eps: float, iters: int, dist, assignment, price=None,
-                workspace=None, helpers=None, offload_min=None, stats=None) -> None:
+                workspace=None, helpers=None, offload_min=None, stats=None, diag=1, wsplit=None) -> None:
     """pcm_emd_forward; helpers / offload_min / stats select the tuning entry
     (helper workgroups per cloud, the miss count above which an iteration's
-    full scans are offloaded, diagnostics) -- None = the library defaults."""
+    full scans are offloaded, diagnostics of kind `diag`: 1 counts, 2 phase
+    timers -- csrc/emd.hip pcm_tune_emd_forward_cfg) -- None = the defaults."""
     dev = _require_device(xyz1, xyz2, dist, assignment)
     b, n, _ = xyz1.shape
     ws_bytes = emd_workspace_bytes(b, n)
     if ws_bytes and (workspace is None or workspace.numel() * workspace.element_size() < ws_bytes):
         workspace = emd_workspace(dev, b, n)
     with torch.cuda.device(dev):
-        if helpers is None and offload_min is None and stats is None:
+        if helpers is None and offload_min is None and stats is None and wsplit is None:
             _check(load_library().pcm_emd_forward(
                 _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
                 _ptr(price), _ptr(workspace), ws_bytes, _stream(dev)), "pcm_emd_forward")
@@ -343,7 +342,8 @@ def emd_forward(xyz1, xyz2, eps: float, iters: int, dist, assignment, price=None
             _check(load_library().pcm_tune_emd_forward_cfg(
                 _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
                 _ptr(price), _ptr(workspace), ws_bytes, -1 if helpers is None else int(helpers),
-                -1 if offload_min is None else int(offload_min), _ptr(stats), _stream(dev)),
+                -1 if offload_min is None else int(offload_min), int(diag), 0 if wsplit is None else int(wsplit),
+                _ptr(stats), _stream(dev)),
                 "pcm_tune_emd_forward_cfg")
 
 
@@ -363,24 +363,6 @@ def emd_backward(xyz1, xyz2, graddist, assignment, gradxyz1) -> None:
         _check(load_library().pcm_emd_backward(
             _ptr(xyz1), _ptr(xyz2), b, n, _ptr(graddist), _ptr(assignment), _ptr(gradxyz1),
             _stream(dev)), "pcm_emd_backward")
-
-
-def tune_emd_forward_stats(xyz1, xyz2, eps: float, iters: int, dist, assignment, stats) -> None:
-    """Internal: EMD forward that also accumulates diagnostics into stats (int32,
-    zero-filled, at least 3*iters + 16 + B entries): [iters, 2] unassigned points
-    and full scans, 16 phase timers and scan counters, per-iteration cache-bid
-    time of batch 0, then the auction wall time of each batch element
-    (tools/tune_emd.py)."""
-    if stats.numel() < 3 * int(iters) + 16 + xyz1.shape[0]:
-        raise ValueError("stats needs 3*iters + 16 + B int32 entries")
-    dev = _require_device(xyz1, xyz2, dist, assignment, stats)
-    b, n, _ = xyz1.shape
-    ws_bytes = emd_workspace_bytes(b, n)
-    ws = emd_workspace(dev, b, n)
-    with torch.cuda.device(dev):
-        _check(load_library().pcm_tune_emd_forward_stats(
-            _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
-            _ptr(ws), ws_bytes, _ptr(stats), _stream(dev)), "pcm_tune_emd_forward_stats")
 
 
 def _nn_workspace(dev, b: int, m: int):

@@ -15,11 +15,13 @@ sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric
 sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "train"))
 import pcm_hip  # noqa: E402
 
-NAMES = {1: "bids", 2: "full-scans", 3: "claim", 4: "assign"}
+TIMERS = ["bids", "full-scans", "claim", "assign", "scan/publish", "exchange/own-items", "merge", "finish"]
 
 
-def timed(x1, x2, eps, iters, d, a, helpers, offload, reps=5):
+def timed(x1, x2, eps, iters, d, a, helpers, offload, wsplit=None, reps=5):
     kw = {} if helpers is None else {"helpers": helpers, "offload_min": offload}
+    if wsplit is not None:
+        kw["wsplit"] = wsplit
     pcm_hip.emd_forward(x1, x2, eps, iters, d, a, **kw)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -49,11 +51,20 @@ def run(name, x1, x2, eps, iters, sweep):
     marks = [0, 1, 2, 5, 10, 20, 50, 100, 200, 500, 1000, 2000, 5000, iters - 1]
     print("  unassigned (sum over batch) at iter:", " ".join(f"{i}:{int(per[i, 0])}" for i in marks if i < iters))
     print("  full scans (sum over batch) at iter:", " ".join(f"{i}:{int(per[i, 1])}" for i in marks if i < iters))
-    print("  batch-0 phase wall (us):", ", ".join(f"{NAMES[i]}={misc[i] / 100.0:.1f}" for i in NAMES))
     print("  auction wall per batch element (us): min %.1f max %.1f" % (min(wall) / 100.0, max(wall) / 100.0))
+    st.zero_()
+    st = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=dev)
+    pcm_hip.emd_forward(x1, x2, eps, iters, d, a, stats=st, diag=2)
+    torch.cuda.synchronize()
+    tm = st.cpu()[2 * iters:2 * iters + 13].tolist()
+    act = max(tm[12], 1)
+    print(f"  batch-0 phase cycles per iteration ({act} iterations): " +
+          ", ".join(f"{nm}={16.0 * v / act:.0f}" for nm, v in zip(TIMERS, tm[:8])))
     print(f"  forward (defaults): {timed(x1, x2, eps, iters, d, a, None, None):.1f} us/call")
     for h, o in sweep:
         print(f"  forward helpers={h} offload_min={o}: {timed(x1, x2, eps, iters, d, a, h, o):.1f} us/call")
+    for w in (2, 4):
+        print(f"  forward wsplit={w}: {timed(x1, x2, eps, iters, d, a, -1, -1, w):.1f} us/call")
 
 
 def generator_clouds(b, dev):

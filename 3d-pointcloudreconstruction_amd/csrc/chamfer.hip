@@ -1170,6 +1170,23 @@ extern "C" size_t pcm_chamfer_workspace_bytes(int b, int n, int m) {
     return pcm_chamfer_loss_ws_offset(b, n, m) + pcm_chamfer_grad_ws_bytes(b, n, m);
 }
 
+// sticky device-side error words of the fused-loss kernels (a bounded wait
+// that timed out): PCM_ERR_LAUNCH when either is set.  Synchronises `stream`.
+extern "C" int pcm_chamfer_workspace_status(const void *workspace, size_t workspace_bytes, int b, int n, int m,
+                                            void *stream) {
+    if (b <= 0 || n <= 0 || m <= 0) return PCM_OK;
+    if (!workspace || workspace_bytes < pcm_chamfer_workspace_bytes(b, n, m)) return PCM_ERR_WORKSPACE;
+    unsigned words[2] = {0u, 0u};
+    const char *base = (const char *)workspace;
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemcpyAsync(&words[0], base + 4 * pcm_loss::kErrWord, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(&words[1], base + pcm_chamfer_loss_ws_offset(b, n, m) + 4 * pcm_chamfer_grad_err_word(), 4,
+                       hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return PCM_ERR_LAUNCH;
+    return (words[0] || words[1]) ? PCM_ERR_LAUNCH : PCM_OK;
+}
+
 extern "C" int pcm_chamfer_forward(const float *xyz1, const float *xyz2, int b, int n, int m,
                                    float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                    void *stream) {

@@ -701,129 +701,102 @@ __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, flo
     }
 }
 
-// Gradients of L = w1 sum(dist1) + w2 sum(dist2) for ONE batch element, by one
-// workgroup, clouds and inverse indices in LDS (chamfer3D.cu:155-195, g = 2 w):
-//   grad1[j] = g1 (p_j - q_I1[j])  then  - g2 (q_k - p_j) for k in S2(j) ascending
-//   grad2[k] = - g1 (p_j - q_k) for j in S1(k) ascending  then  g2 (q_k - p_I2[k])
-// S2(j) = {k : I2[k] = j}, S1(k) = {j : I1[j] = k}: each source claims a slot
-// of its target's bucket with one LDS atomic; the target's thread orders them.
-// A target with more than kGradSlots sources (random clouds: ~1 in 30k; a
-// collapsed cloud: all of them) is finished by the whole workgroup: ballots
-// list its sources in ascending order, one thread sums them.
-// Identical bits to chamfer_bwd_staged_kernel fed graddist = w.
-template <int NT>
-__device__ __forceinline__ void element_grad(const float *__restrict__ X1, const float *__restrict__ X2, int n,
-                                             int m, float w1, float w2, const int32_t *__restrict__ I1g,
-                                             const int32_t *__restrict__ I2g, float *__restrict__ G1,
-                                             float *__restrict__ G2, unsigned char *arena) {
-    constexpr int kPerT = (kGradCap + NT - 1) / NT;
+// Gradients of L = w1 sum(dist1) + w2 sum(dist2) for the targets
+// [q0, q0 + QW) of ONE cloud -- the query range this workgroup's forward
+// covered -- with both clouds in LDS (chamfer3D.cu:155-195, g = 2 w):
+//   cloud 1:  grad1[j] = g1 (p_j - q_I1[j])  then  - g2 (q_k - p_j) for k in S2(j) ascending
+//   cloud 2:  grad2[k] = - g1 (p_j - q_k) for j in S1(k) ascending  then  g2 (q_k - p_I2[k])
+// S2(j) = {k : I2[k] = j}, S1(k) = {j : I1[j] = k}.  Every source of the
+// other cloud whose argmin falls in the range claims a slot of its target's
+// bucket with one LDS atomic; the target's thread orders them.  A target with
+// more than kGradSlots sources (random clouds: ~1 in 30k; a collapsed cloud:
+// all of them) is finished by the whole workgroup: ballots list its sources in
+// ascending order, one thread sums them.  Identical bits to
+// chamfer_bwd_staged_kernel fed graddist = w.
+// S / A: the range's cloud and the other cloud (LDS); nq / na their sizes;
+// gs / h: 2w of the range's direction (direct term) and of the other one
+// (scatter terms); Iown / Ioth: the argmins (written by other workgroups: sc1).
+template <int NT, int QW>
+__device__ __forceinline__ void range_grad(bool dir1, int q0, int nq, int na, const float *S, const float *A,
+                                           float gs, float h, const int32_t *__restrict__ Iown,
+                                           const int32_t *__restrict__ Ioth, float *__restrict__ G,
+                                           unsigned char *scratch) {
+    constexpr int kPerS = (kGradCap + NT - 1) / NT;  // sources per thread
     constexpr int NW = NT / 64;
-    constexpr int kOvfCap = 2 * kGradCap / (kGradSlots + 1) + 1;  // > kGradSlots sources each
-    __shared__ int sOvf[kOvfCap];   // overflowed targets: j (cloud 1) or kGradCap + k (cloud 2)
-    __shared__ int sOvfD[kOvfCap];  // their own argmin (direct term)
+    __shared__ int sOvf[QW];   // overflowed targets (range slot)
     __shared__ int sNOvf;
-    __shared__ int sWcnt[kPerT][NW];
+    __shared__ int sWcnt[kPerS][NW];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
-    float *P1 = reinterpret_cast<float *>(arena);                    // [3n]
-    float *P2 = P1 + 3 * kGradCap;                                    // [3m]
-    int *cnt1 = reinterpret_cast<int *>(P2 + 3 * kGradCap);           // [n] cloud-2 sources per cloud-1 point
-    int *cnt2 = cnt1 + kGradCap;                                      // [m]
-    uint16_t *tab1 = reinterpret_cast<uint16_t *>(cnt2 + kGradCap);  // [n][slots]
-    uint16_t *tab2 = tab1 + kGradCap * kGradSlots;                    // [m][slots]
+    int *cnt = reinterpret_cast<int *>(scratch);                   // [QW] sources per target
+    uint16_t *tab = reinterpret_cast<uint16_t *>(cnt + QW);        // [QW][slots]
+    int *lst = reinterpret_cast<int *>(tab + QW * kGradSlots);     // [na] overflow source list
 
-    // (P1, P2: LDS-DMA'd by the caller before its arrival, already waited for)
-    int i1r[kPerT], i2r[kPerT];  // argmins of this thread's points (written by other workgroups: sc1)
+    const int jt = q0 + tid;  // this thread's target (tid < QW)
+    const int io = (tid < QW && jt < nq) ? ld_sc1(Iown + jt) : 0;
+    int isr[kPerS];
 #pragma unroll
-    for (int r = 0; r < kPerT; ++r) {
-        const int i = tid + r * NT;
-        i1r[r] = ld_sc1(I1g + min(i, n - 1));
-        i2r[r] = ld_sc1(I2g + min(i, m - 1));
-        if (i < n) cnt1[i] = 0;
-        if (i < m) cnt2[i] = 0;
-    }
+    for (int r = 0; r < kPerS; ++r) isr[r] = ld_sc1(Ioth + min(tid + r * NT, na - 1));
+    if (tid < QW) cnt[tid] = 0;
     if (tid == 0) sNOvf = 0;
     __syncthreads();
     PCM_STAMP2(3);
 #pragma unroll
-    for (int r = 0; r < kPerT; ++r) {
+    for (int r = 0; r < kPerS; ++r) {
         const int i = tid + r * NT;
-        if (i < m) {  // cloud-2 point i scatters onto cloud-1 point i2r
-            const int slot = atomicAdd(&cnt1[i2r[r]], 1);
-            if (slot < kGradSlots) tab1[i2r[r] * kGradSlots + slot] = (uint16_t)i;
-        }
-        if (i < n) {  // cloud-1 point i scatters onto cloud-2 point i1r
-            const int slot = atomicAdd(&cnt2[i1r[r]], 1);
-            if (slot < kGradSlots) tab2[i1r[r] * kGradSlots + slot] = (uint16_t)i;
+        const int t = isr[r] - q0;
+        if (i < na && (unsigned)t < (unsigned)QW) {
+            const int slot = atomicAdd(&cnt[t], 1);
+            if (slot < kGradSlots) tab[t * kGradSlots + slot] = (uint16_t)i;
         }
     }
     __syncthreads();
     PCM_STAMP2(4);
-
-    const float g1 = __fmul_rn(w1, 2.f), g2 = __fmul_rn(w2, 2.f);
-#pragma unroll
-    for (int r = 0; r < kPerT; ++r) {
-        const int j = tid + r * NT;
-        if (j < n) {  // cloud 1: direct term first (chamfer3D.cu:184), then the cloud-2 scatters
-            const int c = cnt1[j];
-            if (c <= kGradSlots) {
-                const float sx = P1[3 * j], sy = P1[3 * j + 1], sz = P1[3 * j + 2];
-                const int k = i1r[r];
-                float ax = __fadd_rn(0.f, __fmul_rn(g1, __fsub_rn(sx, P2[3 * k])));
-                float ay = __fadd_rn(0.f, __fmul_rn(g1, __fsub_rn(sy, P2[3 * k + 1])));
-                float az = __fadd_rn(0.f, __fmul_rn(g1, __fsub_rn(sz, P2[3 * k + 2])));
-                scatter_sum(ax, ay, az, sx, sy, sz, g2, P2, tab1 + j * kGradSlots, c);
-                G1[3 * j] = ax;
-                G1[3 * j + 1] = ay;
-                G1[3 * j + 2] = az;
-            } else {
-                const int e = atomicAdd(&sNOvf, 1);
-                sOvf[e] = j;
-                sOvfD[e] = i1r[r];
+    if (tid < QW && jt < nq) {
+        const int c = cnt[tid];
+        if (c <= kGradSlots) {
+            const float sx = S[3 * jt], sy = S[3 * jt + 1], sz = S[3 * jt + 2];
+            const float dx = __fmul_rn(gs, __fsub_rn(sx, A[3 * io]));
+            const float dy = __fmul_rn(gs, __fsub_rn(sy, A[3 * io + 1]));
+            const float dz = __fmul_rn(gs, __fsub_rn(sz, A[3 * io + 2]));
+            float ax = 0.f, ay = 0.f, az = 0.f;
+            if (dir1) {  // cloud 1: direct term first (chamfer3D.cu:184), then the cloud-2 scatters
+                ax = __fadd_rn(ax, dx);
+                ay = __fadd_rn(ay, dy);
+                az = __fadd_rn(az, dz);
             }
-        }
-        if (j < m) {  // cloud 2: cloud-1 scatters first (kernel 1 ran before kernel 2), then direct
-            const int c = cnt2[j];
-            if (c <= kGradSlots) {
-                const float sx = P2[3 * j], sy = P2[3 * j + 1], sz = P2[3 * j + 2];
-                float ax = 0.f, ay = 0.f, az = 0.f;
-                scatter_sum(ax, ay, az, sx, sy, sz, g1, P1, tab2 + j * kGradSlots, c);
-                const int k = i2r[r];
-                ax = __fadd_rn(ax, __fmul_rn(g2, __fsub_rn(sx, P1[3 * k])));
-                ay = __fadd_rn(ay, __fmul_rn(g2, __fsub_rn(sy, P1[3 * k + 1])));
-                az = __fadd_rn(az, __fmul_rn(g2, __fsub_rn(sz, P1[3 * k + 2])));
-                G2[3 * j] = ax;
-                G2[3 * j + 1] = ay;
-                G2[3 * j + 2] = az;
-            } else {
-                const int e = atomicAdd(&sNOvf, 1);
-                sOvf[e] = kGradCap + j;
-                sOvfD[e] = i2r[r];
+            scatter_sum(ax, ay, az, sx, sy, sz, h, A, tab + tid * kGradSlots, c);
+            if (!dir1) {  // cloud 2: cloud-1 scatters first (kernel 1 ran before kernel 2), then direct
+                ax = __fadd_rn(ax, dx);
+                ay = __fadd_rn(ay, dy);
+                az = __fadd_rn(az, dz);
             }
+            G[3 * jt] = ax;
+            G[3 * jt + 1] = ay;
+            G[3 * jt + 2] = az;
+        } else {
+            sOvf[atomicAdd(&sNOvf, 1)] = tid;
         }
     }
     __syncthreads();
 
     // ---- overflowed buckets: ascending source list by ballots, one summing thread
     const int nov = sNOvf;
-    int *lst = reinterpret_cast<int *>(tab1);  // the bucket tables are dead now
     for (int e = 0; e < nov; ++e) {
-        const int code = sOvf[e];
-        const bool c1 = code < kGradCap;  // target in cloud 1 (sources: cloud-2 points)
-        const int j = c1 ? code : code - kGradCap;
-        unsigned long long bal[kPerT];
+        const int t = sOvf[e];
+        const int j = q0 + t;
+        unsigned long long bal[kPerS];
 #pragma unroll
-        for (int r = 0; r < kPerT; ++r) {
+        for (int r = 0; r < kPerS; ++r) {
             const int i = tid + r * NT;
-            const bool match = c1 ? (i < m && i2r[r] == j) : (i < n && i1r[r] == j);
-            bal[r] = __ballot(match);
+            bal[r] = __ballot(i < na && isr[r] == j);
             if (lane == 0) sWcnt[r][wave] = __popcll(bal[r]);
         }
         __syncthreads();
         int total = 0;
 #pragma unroll
-        for (int r = 0; r < kPerT; ++r) {
+        for (int r = 0; r < kPerS; ++r) {
             int base = total;
             for (int w = 0; w < NW; ++w) {
                 base += (w < wave) ? sWcnt[r][w] : 0;
@@ -832,16 +805,13 @@ __device__ __forceinline__ void element_grad(const float *__restrict__ X1, const
             if ((bal[r] >> lane) & 1ull) lst[base + __popcll(bal[r] & ((1ull << lane) - 1ull))] = tid + r * NT;
         }
         __syncthreads();
-        if (tid == 0) {
-            const float *S = c1 ? P1 : P2, *A = c1 ? P2 : P1;
+        if (tid == t) {  // the target's own thread holds its argmin
             const float sx = S[3 * j], sy = S[3 * j + 1], sz = S[3 * j + 2];
-            const float gs = c1 ? g1 : g2, h = c1 ? g2 : g1;
-            const int k = sOvfD[e];
-            const float dx = __fmul_rn(gs, __fsub_rn(sx, A[3 * k]));
-            const float dy = __fmul_rn(gs, __fsub_rn(sy, A[3 * k + 1]));
-            const float dz = __fmul_rn(gs, __fsub_rn(sz, A[3 * k + 2]));
+            const float dx = __fmul_rn(gs, __fsub_rn(sx, A[3 * io]));
+            const float dy = __fmul_rn(gs, __fsub_rn(sy, A[3 * io + 1]));
+            const float dz = __fmul_rn(gs, __fsub_rn(sz, A[3 * io + 2]));
             float ax = 0.f, ay = 0.f, az = 0.f;
-            if (c1) {
+            if (dir1) {
                 ax = __fadd_rn(ax, dx);
                 ay = __fadd_rn(ay, dy);
                 az = __fadd_rn(az, dz);
@@ -852,12 +822,11 @@ __device__ __forceinline__ void element_grad(const float *__restrict__ X1, const
                 ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(A[3 * src + 1], sy)));
                 az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(A[3 * src + 2], sz)));
             }
-            if (!c1) {
+            if (!dir1) {
                 ax = __fadd_rn(ax, dx);
                 ay = __fadd_rn(ay, dy);
                 az = __fadd_rn(az, dz);
             }
-            float *G = c1 ? G1 : G2;
             G[3 * j] = ax;
             G[3 * j + 1] = ay;
             G[3 * j + 2] = az;
@@ -867,24 +836,32 @@ __device__ __forceinline__ void element_grad(const float *__restrict__ X1, const
 }
 
 // Workspace of the fused kernel (after pcm_chamfer_forward_loss's bytes, so one
-// zero-filled buffer serves both): the loss epoch word, an arrival counter per
-// batch element (left zeroed), a partial sum per workgroup, and two 8-byte
+// zero-filled buffer serves both): the loss epoch word and the sticky error
+// word (kGradErrWord) on the first line, an arrival and a departure counter per
+// batch element (both left zeroed), a partial sum per workgroup, and two 8-byte
 // {epoch, sum} granules per batch element (sum of dist1, sum of dist2).
 struct GradWs {
-    unsigned *epoch, *bcount;
+    unsigned *epoch, *bcount, *bdepart;
     float *wpart;
     unsigned long long *gran;
 };
+constexpr int kGradErrWord = 4;  // word of the first line: non-zero after a timed-out wait (sticky)
+// each batch element's arrival and departure counters on 128-byte lines of
+// their own: with all of them in one line, the 8 adds and the polls per
+// element queue behind every other element's at the memory side
+constexpr int kCtrStride = 32;  // unsigned words
 inline size_t grad_ws_bytes(int b, long long blocks) {
-    const size_t c = ((size_t)b * 4 + 127) / 128 * 128, p = ((size_t)blocks * 4 + 127) / 128 * 128;
-    return 128 + c + p + (size_t)b * 16;
+    const size_t c = (size_t)b * 128, p = ((size_t)blocks * 4 + 127) / 128 * 128;
+    return 128 + 2 * c + p + (size_t)b * 16;
 }
 inline GradWs grad_ws(void *base, int b, long long blocks) {
     char *p = (char *)base;
+    const size_t c = (size_t)b * 128;
     GradWs w;
     w.epoch = (unsigned *)p;
     w.bcount = (unsigned *)(p + 128);
-    w.wpart = (float *)(p + 128 + ((size_t)b * 4 + 127) / 128 * 128);
+    w.bdepart = (unsigned *)(p + 128 + c);
+    w.wpart = (float *)(p + 128 + 2 * c);
     w.gran = (unsigned long long *)((char *)w.wpart + ((size_t)blocks * 4 + 127) / 128 * 128);
     return w;
 }
@@ -892,7 +869,8 @@ inline GradWs grad_ws(void *base, int b, long long blocks) {
 // the grid's last workgroup: sweep the 2b granules until all carry this
 // call's epoch (bounded: NaN means on timeout), fixed-order sums, advance the
 // epoch (chamfer_loss.h poll_loss, with the granules per batch element)
-__device__ __forceinline__ void poll_grad_loss(int b, int n, int m, const GradWs &ws, float *__restrict__ mean_out) {
+__device__ __forceinline__ void poll_grad_loss(int b, int n, int m, const GradWs &ws, float *__restrict__ mean_out,
+                                               unsigned max_spins) {
     if (threadIdx.x >= 64) return;
     const int lane = threadIdx.x;
     const unsigned epoch = ws.epoch[0] + 1u;
@@ -904,7 +882,7 @@ __device__ __forceinline__ void poll_grad_loss(int b, int n, int m, const GradWs
         for (unsigned spins = 0;; ++spins) {
             if (i < 2 * b) x = __hip_atomic_load(ws.gran + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (__all((unsigned)(x >> 32) == epoch)) break;
-            if (spins >= kPollMaxSpins) { ok = false; break; }
+            if (spins >= max_spins) { ok = false; break; }
             __builtin_amdgcn_s_sleep(1);
         }
         const float v = __uint_as_float((unsigned)x);
@@ -915,7 +893,12 @@ __device__ __forceinline__ void poll_grad_loss(int b, int n, int m, const GradWs
     }
     s1 = wave_sum(s1);
     s2 = wave_sum(s2);
+    // a timed-out sweep sets the sticky error word: from then on every call on
+    // this workspace reports NaN means until the caller re-zeroes it
+    // (pcm_chamfer_workspace_status tells)
     if (lane == 0) {
+        if (!ok) __hip_atomic_store(ws.epoch + kGradErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = ok && ws.epoch[kGradErrWord] == 0u;
         const float m1 = ok ? s1 / ((float)b * (float)n) : __builtin_nanf("");
         const float m2 = ok ? s2 / ((float)b * (float)m) : __builtin_nanf("");
         mean_out[0] = m1;
@@ -930,13 +913,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
     float *__restrict__ mean_out, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
-    GradWs ws) {
+    GradWs ws, unsigned max_spins) {
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
     constexpr int kFwd = FiltLds<W, QPT, TILE>::kBytes;
     constexpr int kArena = kFwd > kGradBytes ? kFwd : kGradBytes;
+    static_assert(QW <= NT, "one target per thread in the gradient phase");
     __shared__ float sRed[16];
-    __shared__ int sFlag;
+    __shared__ int sFlag, sLate;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -944,7 +928,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int nprod = (int)gridDim.x - 1;
     if ((int)blockIdx.x == nprod) {
         PCM_STAMP2(5);
-        poll_grad_loss(b, n, m, ws, mean_out);
+        poll_grad_loss(b, n, m, ws, mean_out, max_spins);
         PCM_STAMP2(6);
         return;
     }
@@ -956,10 +940,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int batch = bid / per;
     const int r = bid - batch * per;
     const bool first = r < nblk1;
+    const int q0 = (first ? r : r - nblk1) * QW;
     const float *X1 = xyz1 + (size_t)batch * n * 3;
     const float *X2 = xyz2 + (size_t)batch * m * 3;
     const float my_d = filt_forward<float, W, QPT, C, TILE, true>(
-        first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, (first ? r : r - nblk1) * QW,
+        first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
         first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
         first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena);
     PCM_STAMP2(1);
@@ -973,27 +958,45 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         for (int w = 0; w < W; ++w) t += sRed[w];
         __hip_atomic_store(ws.wpart + bid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // Every workgroup stages its batch element's clouds for the gradient phase
-    // now (L2-hot; the forward is done with the arena): whichever arrives last
-    // then finds them in LDS, and the copies land during the arrival round trip.
+    // the batch element's clouds for the gradient phase (L2-hot; the forward
+    // is done with the arena); they land during the arrival round trip
     pcm_dma_to_lds(arena, X1, 12 * n, wave, W);
     pcm_dma_to_lds(arena + 12 * kGradCap, X2, 12 * m, wave, W);
     // every storing wave drains its sc1 stores (and the LDS-DMA lands)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // ---- arrive, then wait (bounded) until every workgroup of this batch
+    // element has arrived: all argmins are then published.  The grid (b *
+    // per + 1 workgroups of 64 W threads) is sized to be co-resident; a wait
+    // that times out sets the sticky error word and yields NaN gradients.
     if (tid == 0) {
-        const unsigned old =
-            __hip_atomic_fetch_add(ws.bcount + batch, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned *ctr = ws.bcount + (size_t)batch * kCtrStride;
+        unsigned *dep_ctr = ws.bdepart + (size_t)batch * kCtrStride;
+        const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         sFlag = (old == (unsigned)per - 1);
+        int late = 0;
+        if (old != (unsigned)per - 1) {
+            for (unsigned spins = 0;; ++spins) {
+                if (ld_sc1((const int32_t *)ctr) == per) break;
+                if (spins >= max_spins) { late = 1; break; }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+        sLate = late;
+        if (late) __hip_atomic_store(ws.epoch + kGradErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the last to leave the wait re-arms both counters for the next call
+        const unsigned dep = __hip_atomic_fetch_add(dep_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (dep == (unsigned)per - 1) {
+            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(dep_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
     __syncthreads();
     PCM_STAMP2(2);
-    if (!sFlag) return;
 
-    // ---- the batch element's last arriver: its loss sums (wave 0; the
-    // granule is the flag, nothing waits on it here) and its gradients
-    if (tid == 0) __hip_atomic_store(ws.bcount + batch, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (wave == 0) {
+    // ---- the batch element's last arriver also publishes its loss sums
+    // (wave 0; the granule is the flag, nothing waits on it here)
+    if (sFlag && wave == 0) {
         float v1 = 0.f, v2 = 0.f;
         for (int i = lane; i < per; i += 64) {
             const float v = ld_sc1(ws.wpart + (size_t)batch * per + i);
@@ -1008,8 +1011,23 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
                                __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    element_grad<NT>(X1, X2, n, m, w1, w2, idx1 + (size_t)batch * n, idx2 + (size_t)batch * m,
-                     grad1 + (size_t)batch * n * 3, grad2 + (size_t)batch * m * 3, arena);
+    float *G = first ? grad1 + (size_t)batch * n * 3 : grad2 + (size_t)batch * m * 3;
+    if (sLate) {  // the argmins of the other direction may be missing
+        const int nq = first ? n : m;
+        for (int t = tid; t < 3 * QW; t += NT)
+            if (q0 * 3 + t < 3 * nq) G[3 * q0 + t] = __builtin_nanf("");
+        return;
+    }
+    // ---- gradients of this workgroup's query range
+    const float *P1 = reinterpret_cast<const float *>(arena);
+    const float *P2 = P1 + 3 * kGradCap;
+    const float g1 = __fmul_rn(w1, 2.f), g2 = __fmul_rn(w2, 2.f);
+    if (first)
+        range_grad<NT, QW>(true, q0, n, m, P1, P2, g1, g2, idx1 + (size_t)batch * n, idx2 + (size_t)batch * m, G,
+                           arena + 24 * kGradCap);
+    else
+        range_grad<NT, QW>(false, q0, m, n, P2, P1, g2, g1, idx2 + (size_t)batch * m, idx1 + (size_t)batch * n, G,
+                           arena + 24 * kGradCap);
     PCM_STAMP2(7);
 }
 
@@ -1040,7 +1058,7 @@ const int kPcmNumFilt16Variants = sizeof(kPcmFilt16Variants) / sizeof(kPcmFilt16
 // ---- fused loss + gradient: variants (tools/tune_chamfer.py) and entry points
 namespace {
 typedef void (*grad_kernel_t)(const float *, const float *, int, int, int, float, float, float *, float *,
-                              int32_t *, int32_t *, float *, float *, float *, int, int, GradWs);
+                              int32_t *, int32_t *, float *, float *, float *, int, int, GradWs, unsigned);
 struct GradVariant {
     grad_kernel_t k;
     int waves, qpt;
@@ -1074,7 +1092,8 @@ long long grad_blocks_max(int b, int n, int m) {
 
 int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, int n, int m, float w1, float w2,
                      float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out, float *grad1,
-                     float *grad2, void *workspace, size_t workspace_bytes, void *stream) {
+                     float *grad2, void *workspace, size_t workspace_bytes, void *stream,
+                     unsigned max_spins = pcm_loss::kPollMaxSpins) {
     if (b <= 0 || n <= 0 || m <= 0) return PCM_ERR_INVALID_ARG;
     if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
     if (variant < 0 || variant >= kNumGradVariants) return PCM_ERR_INVALID_ARG;
@@ -1089,10 +1108,12 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
     const GradWs ws = grad_ws((char *)workspace + off, b, blocks);
     // + the polling workgroup (the grid's last)
     hipLaunchKernelGGL(v.k, dim3((unsigned)blocks + 1), dim3(64 * v.waves), 0, (hipStream_t)stream, xyz1, xyz2, b,
-                       n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out, grad1, grad2, nblk1, nblk2, ws);
+                       n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out, grad1, grad2, nblk1, nblk2, ws, max_spins);
     return pcm_launch_status();
 }
 }  // namespace
+
+int pcm_chamfer_grad_err_word(void) { return kGradErrWord; }
 
 size_t pcm_chamfer_grad_ws_bytes(int b, int n, int m) {
     if (b <= 0 || n <= 0 || m <= 0) return 0;
@@ -1116,6 +1137,17 @@ extern "C" int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const 
 }
 
 extern "C" int pcm_tune_num_chamfer_loss_grad_variants(void) { return kNumGradVariants; }
+
+// the default variant with a given bound on every wait (tests: 0 forces the
+// timeout path -- sticky error word, NaN means and gradients)
+extern "C" int pcm_tune_chamfer_loss_grad_spins(unsigned max_spins, const float *xyz1, const float *xyz2, int b,
+                                                int n, int m, float w1, float w2, float *dist1, float *dist2,
+                                                int32_t *idx1, int32_t *idx2, float *mean_out, float *gradxyz1,
+                                                float *gradxyz2, void *workspace, size_t workspace_bytes,
+                                                void *stream) {
+    return launch_loss_grad(kDefaultGradVariant, xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out,
+                            gradxyz1, gradxyz2, workspace, workspace_bytes, stream, max_spins);
+}
 
 #ifdef PCM_STAMPS
 extern "C" int pcm_tune_read_stamps(unsigned long long *host, int nblocks) {

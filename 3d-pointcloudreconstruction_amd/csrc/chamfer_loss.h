@@ -100,14 +100,18 @@ __device__ __forceinline__ void finish_loss(int nb1, int b, int n, int m, const 
 // the ticket line): producers and poller read it at start, the poller
 // advances it at the end, so stream-ordered calls (and graph replays) never
 // match a previous call's granules and nothing needs re-zeroing.  The poll is
-// bounded: after kPollMaxSpins sweeps it writes NaN means and still advances
-// the epoch (no hang, no stale match on the next call).
+// bounded: after kPollMaxSpins sweeps it writes NaN means, advances the epoch
+// and sets the sticky error word kErrWord; every later call on the workspace
+// then reports NaN means until the caller re-zeroes it (a producer that ran
+// late could otherwise tag a granule with a later call's epoch).
+// pcm_chamfer_workspace_status reads the word.
 constexpr int kEpochWord = 1;
+constexpr int kErrWord = 2;
 constexpr unsigned kPollMaxSpins = 1u << 22;
 
 __device__ __forceinline__ void poll_loss(int nb1, int nbt, int b, int n, int m,
                                           const unsigned long long *__restrict__ gran, unsigned *ticket,
-                                          float *__restrict__ mean_out) {
+                                          float *__restrict__ mean_out, unsigned max_spins = kPollMaxSpins) {
     if (threadIdx.x >= 64) return;  // one polling wave
     const int lane = threadIdx.x;
     const unsigned epoch = ticket[kEpochWord] + 1u;
@@ -126,7 +130,7 @@ __device__ __forceinline__ void poll_loss(int nb1, int nbt, int b, int n, int m,
                 ready &= (unsigned)(x[r] >> 32) == epoch;
             }
             if (__all(ready)) break;
-            if (spins >= kPollMaxSpins) { ok = false; break; }
+            if (spins >= max_spins) { ok = false; break; }
             __builtin_amdgcn_s_sleep(1);
         }
 #pragma unroll
@@ -140,6 +144,8 @@ __device__ __forceinline__ void poll_loss(int nb1, int nbt, int b, int n, int m,
     s1 = wave_sum(s1);
     s2 = wave_sum(s2);
     if (lane == 0) {
+        if (!ok) __hip_atomic_store(ticket + kErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = ok && ticket[kErrWord] == 0u;
         mean_out[0] = ok ? s1 / ((float)b * (float)n) : __builtin_nanf("");
         mean_out[1] = ok ? s2 / ((float)b * (float)m) : __builtin_nanf("");
         ticket[kEpochWord] = epoch;
@@ -177,3 +183,4 @@ extern const int kPcmNumFilt16Variants;
 // chamfer_filt.hip).
 size_t pcm_chamfer_loss_ws_offset(int b, int n, int m);
 size_t pcm_chamfer_grad_ws_bytes(int b, int n, int m);
+int pcm_chamfer_grad_err_word(void);  // word index of the fused kernel's sticky error (its region)

@@ -21,6 +21,10 @@ int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const float *xyz2
                                float w2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out,
                                float *gradxyz1, float *gradxyz2, void *workspace, size_t workspace_bytes,
                                void *stream);
+int pcm_tune_chamfer_loss_grad_spins(unsigned max_spins, const float *xyz1, const float *xyz2, int b, int n, int m,
+                                     float w1, float w2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                                     float *mean_out, float *gradxyz1, float *gradxyz2, void *workspace,
+                                     size_t workspace_bytes, void *stream);
 int pcm_tune_read_stamps(unsigned long long *host, int nblocks);  // profiling build only (make stamps)
 int pcm_tune_num_chamfer_f16_variants(void);
 int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,

@@ -108,13 +108,33 @@ class chamfer_3DLossFunction(Function):
         return gradxyz1 * grad_loss, gradxyz2 * grad_loss
 
 
+def _chamfer_loss_value(xyz1, xyz2):
+    """mean(dist1) + mean(dist2) with no gradient: the forward with the in-kernel
+    loss reduction (pcm_chamfer_forward_loss), no gradient work."""
+    xyz1, xyz2 = xyz1.contiguous(), xyz2.contiguous()
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    dev = xyz1.device
+    dist1 = torch.empty(b, n, device=dev)
+    dist2 = torch.empty(b, m, device=dev)
+    idx1 = torch.empty(b, n, dtype=torch.int32, device=dev)
+    idx2 = torch.empty(b, m, dtype=torch.int32, device=dev)
+    means = torch.empty(2, device=dev)
+    pcm_hip.chamfer_forward_loss(xyz1, xyz2, dist1, dist2, idx1, idx2, means)
+    return means[0] + means[1]
+
+
 class chamfer_3DLoss(nn.Module):
-    """loss/loss.py:34-36 in one launch (see chamfer_3DLossFunction); falls back
-    to chamfer_3DDist + torch.mean where the one-launch kernel does not apply."""
+    """loss/loss.py:34-36 in one launch (see chamfer_3DLossFunction); without
+    autograd (torch.no_grad, or neither cloud requires grad) only the forward
+    with its in-kernel loss runs; chamfer_3DDist + torch.mean where the fused
+    kernels do not apply."""
 
     def forward(self, input1, input2):
         if pcm_hip.loss_grad_supported(input1, input2) and input1.is_cuda:
-            return chamfer_3DLossFunction.apply(input1, input2)
+            if torch.is_grad_enabled() and (input1.requires_grad or input2.requires_grad):
+                return chamfer_3DLossFunction.apply(input1, input2)
+            return _chamfer_loss_value(input1, input2)
         dist1, dist2, _, _ = chamfer_3DDist()(input1, input2)
         return torch.mean(dist1) + torch.mean(dist2)
 

@@ -23,7 +23,7 @@ _lib = None
 EXPORTED = (
     "pcm_version", "pcm_strerror",
     "pcm_chamfer_forward", "pcm_chamfer_backward",
-    "pcm_chamfer_workspace_bytes", "pcm_chamfer_forward_loss",
+    "pcm_chamfer_workspace_bytes", "pcm_chamfer_forward_loss", "pcm_chamfer_workspace_status",
     "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward", "pcm_emd_workspace_status",
     "pcm_chamfer_forward_f16", "pcm_chamfer_backward_f16",
     "pcm_chamfer_loss_grad",
@@ -65,6 +65,11 @@ def load_library():
     L.pcm_chamfer_backward.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
     L.pcm_chamfer_workspace_bytes.restype = cs
     L.pcm_chamfer_workspace_bytes.argtypes = [ci, ci, ci]
+    L.pcm_chamfer_workspace_status.restype = ci
+    L.pcm_chamfer_workspace_status.argtypes = [vp, cs, ci, ci, ci, vp]
+    L.pcm_tune_chamfer_loss_grad_spins.restype = ci
+    L.pcm_tune_chamfer_loss_grad_spins.argtypes = [ctypes.c_uint, vp, vp, ci, ci, ci, cf, cf, vp, vp, vp, vp, vp, vp,
+                                                   vp, vp, cs, vp]
     L.pcm_chamfer_forward_loss.restype = ci
     L.pcm_chamfer_forward_loss.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, cs, vp]
     L.pcm_tune_num_chamfer_variants.restype = ci
@@ -237,6 +242,30 @@ def chamfer_loss_grad(xyz1, xyz2, w1, w2, dist1, dist2, idx1, idx2, mean_out, gr
             _check(L.pcm_chamfer_loss_grad(*args), "pcm_chamfer_loss_grad")
         else:
             _check(L.pcm_tune_chamfer_loss_grad(int(variant), *args), "pcm_tune_chamfer_loss_grad")
+
+
+def chamfer_workspace_status(workspace, b: int, n: int, m: int) -> None:
+    """Raise PcmError if a fused-loss kernel on `workspace` hit a device-side
+    timeout (sticky until the workspace is zero-filled again; synchronises the
+    current stream)."""
+    dev = workspace.device
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_chamfer_workspace_status(_ptr(workspace), workspace.numel(), b, n, m, _stream(dev)),
+               "pcm_chamfer_workspace_status")
+
+
+def tune_chamfer_loss_grad_spins(max_spins, xyz1, xyz2, w1, w2, dist1, dist2, idx1, idx2, mean_out, gradxyz1,
+                                 gradxyz2, workspace) -> None:
+    """Internal: pcm_chamfer_loss_grad with every wait bounded by max_spins
+    polls (0 forces the timeout path; tests)."""
+    dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2, mean_out, gradxyz1, gradxyz2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_tune_chamfer_loss_grad_spins(
+            int(max_spins), _ptr(xyz1), _ptr(xyz2), b, n, m, float(w1), float(w2), _ptr(dist1), _ptr(dist2),
+            _ptr(idx1), _ptr(idx2), _ptr(mean_out), _ptr(gradxyz1), _ptr(gradxyz2), _ptr(workspace),
+            workspace.numel(), _stream(dev)), "pcm_tune_chamfer_loss_grad_spins")
 
 
 def tune_num_chamfer_loss_grad_variants() -> int:

@@ -82,8 +82,8 @@ int pcm_chamfer_forward(const float *xyz1, const float *xyz2, int b, int n, int 
  *   mean_out[0] = mean(dist1), mean_out[1] = mean(dist2)   (device float[2])
  * summed in a fixed order (deterministic run to run).  Needs b, n, m > 0 and a
  * device workspace of pcm_chamfer_workspace_bytes(b, n, m) bytes that is
- * ZERO-FILLED when first allocated; each call leaves it zeroed again, so it
- * can be reused by stream-ordered calls (not by concurrent ones).
+ * ZERO-FILLED when first allocated; the kernels keep it consistent across
+ * stream-ordered calls (not concurrent ones), so it is zero-filled only once.
  */
 size_t pcm_chamfer_workspace_bytes(int b, int n, int m);
 int pcm_chamfer_forward_loss(const float *xyz1, const float *xyz2, int b, int n, int m,
@@ -110,6 +110,16 @@ int pcm_chamfer_loss_grad(const float *xyz1, const float *xyz2, int b, int n, in
                           float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out,
                           float *gradxyz1, float *gradxyz2, void *workspace, size_t workspace_bytes,
                           void *stream);
+
+/*
+ * Device-side failure of the fused-loss kernels on `workspace` (the loss
+ * poller or a gradient-phase wait that timed out -- workgroups that could not
+ * all be resident): PCM_OK or PCM_ERR_LAUNCH.  The error is sticky: every later
+ * call on that workspace reports NaN means (and the failed call's NaN
+ * gradients) until the caller zero-fills the workspace again.  Synchronises
+ * `stream` (it reads device memory).
+ */
+int pcm_chamfer_workspace_status(const void *workspace, size_t workspace_bytes, int b, int n, int m, void *stream);
 
 /*
  * Chamfer backward (chamfer3D.cu:155-195).  With g = 2*graddist:

@@ -338,7 +338,8 @@ def test_f16_duplicates_and_nonfinite(cuda, oracle):
         np.testing.assert_array_equal(g[fin].view(np.int32), r[fin].view(np.int32))
 
 
-@pytest.mark.parametrize("b,n,m,seed", [(4, 256, 256, 90), (8, 1024, 1024, 91), (2, 3000, 1500, 92)])
+@pytest.mark.parametrize("b,n,m,seed", [(4, 256, 256, 90), (8, 1024, 1024, 91), (2, 3000, 1500, 92),
+                                        (8, 16384, 16384, 94)])  # BASELINE config 5, full size
 def test_backward_f16_is_rounded_fp32_gradient(cuda, oracle, b, n, m, seed):
     a, c = _clouds(seed, b, n, m)
     ah, ch = a.half(), c.half()
@@ -569,26 +570,79 @@ def test_loss_grad_rejects_large_clouds(cuda):
 
 
 @pytest.mark.parametrize("b,n,m", [(32, 1024, 1024), (3, 700, 1000), (2, 2048, 100)])
-def test_loss_module_matches_reference_sequence(cuda, b, n, m):
-    # Loss.get_chamfer_loss (one launch where it applies) against the
-    # reference sequence chamfer_3DDist + torch.mean + autograd
-    import dist_chamfer_3D
+def test_loss_module_matches_reference_sequence(cuda, oracle, b, n, m):
+    # Loss.get_chamfer_loss (one launch where it applies) against the ORACLE
+    # running the reference sequence: chamfer_3DDist forward, mean(dist1) +
+    # mean(dist2) (loss/loss.py:34-36), and the backward autograd feeds it
+    # (graddist = 1/(b n), 1/(b m); chamfer3D.cu:155-195)
     import loss as loss_mod
     a, c = _clouds(121, b, n, m)
     x1 = a.to(cuda).requires_grad_(True)
     x2 = c.to(cuda).requires_grad_(True)
     L = loss_mod.Loss().get_chamfer_loss(x1, x2)
     (L * 1.0).backward()
-    y1 = a.to(cuda).requires_grad_(True)
-    y2 = c.to(cuda).requires_grad_(True)
-    d1, d2, _, _ = dist_chamfer_3D.chamfer_3DDist()(y1, y2)
-    R = torch.mean(d1) + torch.mean(d2)
-    R.backward()
     torch.cuda.synchronize()
-    np.testing.assert_allclose(L.item(), R.item(), rtol=2e-6)
-    # same per-point gradient formula and order: bit-identical
-    assert torch.equal(x1.grad, y1.grad)
-    assert torch.equal(x2.grad, y2.grad)
+    r1, r2, j1, j2 = oracle.chamfer_forward(a.numpy(), c.numpy())
+    ref = float(r1.astype(np.float64).mean()) + float(r2.astype(np.float64).mean())
+    np.testing.assert_allclose(L.item(), ref, rtol=2e-6)
+    g1 = np.full((b, n), 1.0 / (b * n), np.float32)
+    g2 = np.full((b, m), 1.0 / (b * m), np.float32)
+    rg1, rg2 = oracle.chamfer_backward(a.numpy(), c.numpy(), g1, g2, j1, j2)
+    np.testing.assert_array_equal(x1.grad.cpu().numpy().view(np.int32), rg1.view(np.int32))
+    np.testing.assert_array_equal(x2.grad.cpu().numpy().view(np.int32), rg2.view(np.int32))
+
+
+def test_loss_module_no_grad_skips_gradient_kernel(cuda, oracle, monkeypatch):
+    # under no_grad (evaluation) chamfer_3DLoss must not run the gradient work
+    import dist_chamfer_3D
+    import pcm_hip
+
+    def refuse(*args, **kw):
+        raise AssertionError("gradient kernel launched under no_grad")
+
+    monkeypatch.setattr(pcm_hip, "chamfer_loss_grad", refuse)
+    a, c = _clouds(122, 4, 1024, 1024)
+    with torch.no_grad():
+        L = dist_chamfer_3D.chamfer_3DLoss()(a.to(cuda), c.to(cuda))
+    r1, r2, _, _ = oracle.chamfer_forward(a.numpy(), c.numpy())
+    ref = float(r1.astype(np.float64).mean()) + float(r2.astype(np.float64).mean())
+    np.testing.assert_allclose(L.item(), ref, rtol=2e-6)
+    # inputs that do not require grad take the same forward-only path
+    L2 = dist_chamfer_3D.chamfer_3DLoss()(a.to(cuda), c.to(cuda))
+    assert not L2.requires_grad
+    np.testing.assert_allclose(L2.item(), ref, rtol=2e-6)
+
+
+def test_loss_grad_timeout_sets_sticky_error(cuda, oracle):
+    # every wait bounded to zero polls: the timeout path must be visible
+    # (sticky error word, NaN means) and a re-zeroed workspace must recover
+    import pcm_hip
+    b, n, m = 32, 1024, 1024
+    a, c = _clouds(123, b, n, m)
+    x1, x2 = a.to(cuda), c.to(cuda)
+    d1, d2 = torch.empty(b, n, device=cuda), torch.empty(b, m, device=cuda)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+    gx1, gx2 = torch.empty_like(x1), torch.empty_like(x2)
+    means = torch.empty(3, device=cuda)
+    ws = torch.zeros(pcm_hip.load_library().pcm_chamfer_workspace_bytes(b, n, m), dtype=torch.uint8, device=cuda)
+    pcm_hip.tune_chamfer_loss_grad_spins(0, x1, x2, 1 / (b * n), 1 / (b * m), d1, d2, i1, i2, means, gx1, gx2, ws)
+    torch.cuda.synchronize()
+    with pytest.raises(pcm_hip.PcmError):
+        pcm_hip.chamfer_workspace_status(ws, b, n, m)
+    assert torch.isnan(means).all()
+    # sticky: a normal call on the same workspace still reports NaN
+    pcm_hip.chamfer_loss_grad(x1, x2, 1 / (b * n), 1 / (b * m), d1, d2, i1, i2, means, gx1, gx2, ws)
+    torch.cuda.synchronize()
+    assert torch.isnan(means).all()
+    # re-zeroed: correct again
+    ws.zero_()
+    pcm_hip.chamfer_loss_grad(x1, x2, 1 / (b * n), 1 / (b * m), d1, d2, i1, i2, means, gx1, gx2, ws)
+    torch.cuda.synchronize()
+    pcm_hip.chamfer_workspace_status(ws, b, n, m)
+    r1, r2, _, _ = oracle.chamfer_forward(a.numpy(), c.numpy())
+    ref = float(r1.astype(np.float64).mean()) + float(r2.astype(np.float64).mean())
+    np.testing.assert_allclose(means[2].item(), ref, rtol=2e-6)
 
 
 def test_loss_function_scales_upstream_gradient(cuda):

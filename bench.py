@@ -52,11 +52,18 @@ GRAPH_STEPS = 10                   # steps captured per hipGraph replay
 FWD_KERNEL = "chamfer_fwd_sgpr_kernel<8, 2, 16, 3>"
 BWD_KERNEL = "chamfer_bwd_staged_kernel"
 FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024>"
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r01", "pmc_summary.json")
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r02", "pmc_summary.json")
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0
 FP32_VALU_PEAK_TFLOPS = 157.3
+# VALU issue: a wave64 instruction every 2 cycles per SIMD (guide, per-instruction
+# constants: v_fma_f32 2 cyc) = 32 lane-ops/cycle/SIMD x 4 SIMD x 256 CU x 2.4 GHz
+VALU_LANE_OPS_PEAK = 256 * 4 * 32 * 2.4e9
+# the reference's Bid (emd_cuda.cu:139-155) per (bidder, object) pair: 3 sub,
+# 1 mul + 2 fma, sqrt, 2 f32->f64 cvt, 2 f64 sub, f64->f32 cvt, 2 compares
+# + 3 selects of the top-2 update ~= 20 lane-ops
+EMD_LANE_OPS_PER_PAIR = 20
 # algorithmic FLOPs per point pair of the squared distance: 3 sub + 3 mul + 2 add
 FLOP_PER_PAIR = 8
 # algorithmic HBM bytes of the forward launch: read both clouds, write
@@ -176,24 +183,64 @@ def kernel_avg_us(launch, reps, dev, graph=True):
     return e0.elapsed_time(e1) * 1000.0 / reps
 
 
-def emd_leg(dev, reps=10, eps=EMD_EPS, iters=EMD_ITERS):
+def generator_predictions(dev, b=EMD_B, n=EMD_N):
+    """The clouds a seeded random-init 3D-FENet generator predicts (train/fenet.py,
+    the model train.py:160 runs; its RepVGG checkpoint is absent, so seeded
+    weights) for synthetic images, and uniform [0,1) ground truth: the inputs
+    the training call loss/loss.py:23 sees early in training."""
+    sys.path.insert(0, os.path.join(PKG, "train"))
+    import fenet
+    import train_step as T
+    gen = fenet.seeded_init(fenet.Generator(n), 0).to(dev).train()
+    images, points = T.synthetic_batch(b, n, dev, seed=0)
+    with torch.no_grad():
+        pred = gen(images)[2].transpose(2, 1).contiguous()
+    del gen
+    torch.cuda.empty_cache()
+    return pred, points
+
+
+def emd_leg(dev, reps=10, eps=EMD_EPS, iters=EMD_ITERS, clouds=None, label="uniform [0,1) clouds, seeded"):
     """BASELINE config 3 by default; with eps=0.05, iters=3000 the training call
-    of loss/loss.py:23 (the auction stops early once every point is assigned,
-    so iters/s there counts the requested iterations, as the reference runs them)."""
-    g = torch.Generator(device="cpu").manual_seed(3)
-    x1 = torch.rand(EMD_B, EMD_N, 3, generator=g).to(dev)
-    x2 = torch.rand(EMD_B, EMD_N, 3, generator=g).to(dev)
-    d = torch.empty(EMD_B, EMD_N, device=dev)
-    a = torch.empty(EMD_B, EMD_N, dtype=torch.int32, device=dev)
-    ws_b = pcm_hip.emd_workspace_bytes(EMD_B, EMD_N)
-    ws = torch.empty(max(ws_b, 1), dtype=torch.uint8, device=dev)
+    of loss/loss.py:23.  The auction stops once every point is assigned, so
+    both rates are given: iters_per_s counts the REQUESTED iterations (the
+    reference launches all of them), active_iters_per_s the iterations that
+    had bidders.  Roofline: the reference's work, every bidder scanning every
+    object each iteration (emd_cuda.cu:139-155), in VALU lane-ops."""
+    if clouds is None:
+        g = torch.Generator(device="cpu").manual_seed(3)
+        x1 = torch.rand(EMD_B, EMD_N, 3, generator=g).to(dev)
+        x2 = torch.rand(EMD_B, EMD_N, 3, generator=g).to(dev)
+    else:
+        x1, x2 = clouds
+    b, n, _ = x1.shape
+    d = torch.empty(b, n, device=dev)
+    a = torch.empty(b, n, dtype=torch.int32, device=dev)
+    ws = pcm_hip.emd_workspace(dev, b, n)
+    # counts (a separate, untimed run: the counters perturb the timing)
+    st = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=dev)
+    pcm_hip.emd_forward(x1, x2, eps, iters, d, a, workspace=ws, stats=st, diag=1)
+    torch.cuda.synchronize(dev)
+    per = st[:2 * iters].view(iters, 2).cpu()
+    active = int((per[:, 0] > 0).sum())
+    bids = int(per[:, 0].sum())
+    full_scans = int(per[:, 1].sum())
 
     def run():
         pcm_hip.emd_forward(x1, x2, eps, iters, d, a, None, ws)
 
     us = kernel_avg_us(run, reps, dev, graph=False)  # >= 250 us launches: host cost hidden
-    return {"config": f"B={EMD_B} N=M={EMD_N} iters={iters} eps={eps}",
-            "ms_per_forward": us / 1000.0, "iters_per_s": iters / (us * 1e-6)}
+    pairs = bids * n
+    lane_ops = pairs * EMD_LANE_OPS_PER_PAIR / (us * 1e-6)
+    return {"config": f"B={b} N=M={n} iters={iters} eps={eps}", "clouds": label,
+            "ms_per_forward": us / 1000.0, "iters_requested": iters, "iters_run": active,
+            "iters_per_s": iters / (us * 1e-6), "active_iters_per_s": active / (us * 1e-6),
+            "bids": bids, "full_scans": full_scans, "bid_pair_evals_per_s": pairs / (us * 1e-6),
+            "roofline": {"bound": "valu", "kernel": "emd_seed_kernel + emd_auction_kernel",
+                         "achieved": lane_ops / 1e12, "peak": VALU_LANE_OPS_PEAK / 1e12,
+                         "unit": "T lane-ops/s", "frac": lane_ops / VALU_LANE_OPS_PEAK,
+                         "note": f"{EMD_LANE_OPS_PER_PAIR} lane-ops per (bidder, object) pair the reference "
+                                 "evaluates; the build evaluates fewer (caches), so this is the reference-work rate"}}
 
 
 def dense_f16_leg(dev, reps=10):
@@ -279,32 +326,53 @@ def pmc_bytes(kernel):
         return None
 
 
-def cpu_baseline(target_s=10.0):
-    """The oracle's C restatement of the reference O(N*M) loop, OpenMP over
-    (batch, query), on the host cores, on a bounded sample of the workload."""
+def host_cores():
+    """The CPU share this process may use: the scheduler affinity, capped by
+    OMP_NUM_THREADS when set (the GPU box exports 16, its share of a larger
+    host whose every core nproc would report)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
+
+
+def cpu_baseline(target_s=8.0):
+    """The oracle's C restatement of the reference O(N*M) loop (chamfer3D.cu:
+    12-195 / utils/utils.py:246-266), OpenMP over (batch, query), on the FULL
+    B=32 workload: the box's host cores (value) and one core (single_core)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import numpy as np
     import oracle as O  # CPU baseline leg only
     O.build()
-    threads = min(16, os.cpu_count() or 1)
     rng = np.random.default_rng(0)
-    bs = 4  # sample: 4 of the 32 clouds per rep
-    a = rng.random((bs, N, 3), dtype=np.float32)
-    c = rng.random((bs, M, 3), dtype=np.float32)
-    g1 = np.full((bs, N), 1.0 / (B * N), np.float32)
-    g2 = np.full((bs, M), 1.0 / (B * M), np.float32)
-    reps, t0 = 0, time.perf_counter()
-    while True:
-        d1, d2, i1, i2 = O.chamfer_forward(a, c, nthreads=threads)
-        O.chamfer_backward(a, c, g1, g2, i1, i2, nthreads=threads)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= target_s or reps >= 10000:
-            break
-    pairs = 2 * bs * N * M * reps
-    return {"value": pairs / el, "unit": "point-pairs/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} reps of Chamfer fwd+bwd on {bs} of the {B} clouds "
-                      f"(N=M={N}), oracle/pcm_oracle.c, OpenMP {threads} threads, {el:.1f} s"}
+    a = rng.random((B, N, 3), dtype=np.float32)
+    c = rng.random((B, M, 3), dtype=np.float32)
+    g1 = np.full((B, N), 1.0 / (B * N), np.float32)
+    g2 = np.full((B, M), 1.0 / (B * M), np.float32)
+
+    def timed(threads, budget):
+        reps, t0 = 0, time.perf_counter()
+        while True:
+            d1, d2, i1, i2 = O.chamfer_forward(a, c, nthreads=threads)
+            O.chamfer_backward(a, c, g1, g2, i1, i2, nthreads=threads)
+            reps += 1
+            el = time.perf_counter() - t0
+            if el >= budget or reps >= 10000:
+                return reps, el
+
+    threads = host_cores()
+    reps, el = timed(threads, target_s)
+    reps1, el1 = timed(1, target_s / 2)
+    pairs = 2 * B * N * M
+    return {"value": pairs * reps / el, "unit": "point-pairs/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} reps of the full Chamfer fwd+bwd workload (B={B}, N=M={N}), oracle/pcm_oracle.c, "
+                      f"OpenMP {threads} threads (the box's CPU share), {el:.1f} s",
+            "single_core": {"value": pairs * reps1 / el1, "unit": "point-pairs/s", "cores": 1,
+                            "sample": f"{reps1} reps of the same workload on 1 thread, {el1:.1f} s"}}
 
 
 def main():
@@ -399,7 +467,7 @@ def main():
                      "achieved": dom_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": dom_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": pmc_bytes(dom_kernel),
                      "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE*2+WRITE_SIZE, "
-                                     "profiles/r01/pmc_summary.json)",
+                                     "profiles/r02/pmc_summary.json)",
                      "kernel_us": dom_us,
                      "note": "FLOPs = 8 per point pair (algorithmic); VALU-bound, see DESIGN.md"},
         "roofline_hbm": {"bound": "hbm", "kernel": dom_kernel,
@@ -414,9 +482,25 @@ def main():
                        "bwd_algorithmic_bytes": BWD_BYTES, "bwd_traffic": pmc_bytes(BWD_KERNEL),
                        "step_us": fwd_us + bwd_us},
     }
+    if world > 1:
+        # the per-step variant: every step's 8-byte loss all-reduced right
+        # after it (eager: a collective is not captured into the graph)
+        def per_step(k):
+            for _ in range(k):
+                step(0)
+                dist.all_reduce(step.loss[0])
+        per_step(3)
+        t_ps = time_region(lambda: per_step(args.steps), 1, dev, world)
+        out["per_step_allreduce"] = {
+            "launch": "eager, one RCCL all-reduce of the step's loss per step",
+            "ms_per_step": t_ps * 1000.0 / args.steps,
+            "value": world * args.steps * 2 * B * N * M / t_ps}
     if not args.no_emd:
         out["emd"] = emd_leg(dev)
-        out["emd_training_call"] = emd_leg(dev, reps=5, eps=0.05, iters=3000)
+        pred, points = generator_predictions(dev)
+        out["emd_training_call"] = emd_leg(dev, reps=3, eps=0.05, iters=3000, clouds=(pred, points),
+                                           label="seeded random-init generator predictions vs uniform GT")
+        out["emd_training_call_uniform"] = emd_leg(dev, reps=3, eps=0.05, iters=3000)
     if not args.no_dense:
         out["dense_fp16"] = dense_f16_leg(dev)
     if not args.no_icp:

@@ -253,13 +253,14 @@ __device__ __forceinline__ float row_d(const pcm_f4 t, float qx, float qy, float
 // lowest index attaining it, d2 = min over j != k1 of d'.  Chunk minima are
 // tracked with their second best (med3), then the winning chunk is rescanned
 // per candidate.
-__device__ __forceinline__ void nn_screen(pcm_cf4 *rows, const pcm_f4 *__restrict__ rows_v, int mpad, float qx,
+template <typename RowPtr, typename RowPtrV>
+__device__ __forceinline__ void nn_screen(RowPtr rows, RowPtrV rows_v, int mpad, float qx,
                                           float qy, float qz, float &d1, float &d2, int &k1) {
     float b1 = PCM_INF, b2 = PCM_INF;
     int c1 = 0;
     const int nch = mpad / kChunk;
     for (int c = 0; c < nch; ++c) {
-        pcm_cf4 *tk = rows + c * kChunk;
+        RowPtr tk = rows + c * kChunk;
         float mn = PCM_INF;
 #pragma unroll
         for (int k = 0; k < kChunk; k += 2) {
@@ -272,8 +273,8 @@ __device__ __forceinline__ void nn_screen(pcm_cf4 *rows, const pcm_f4 *__restric
         b1 = lt ? mn : b1;
         c1 = lt ? c : c1;
     }
-    // rescan the winning chunk (per-lane chunk: vector loads, L1/L2 resident)
-    const pcm_f4 *tk = rows_v + c1 * kChunk;
+    // rescan the winning chunk (per-lane chunk: vector loads, L1/L2 resident, or LDS)
+    RowPtrV tk = rows_v + c1 * kChunk;
     float e1 = PCM_INF, e2 = PCM_INF;
     int j1 = 0;
 #pragma unroll 8
@@ -300,8 +301,9 @@ __device__ __forceinline__ void nn_screen(pcm_cf4 *rows, const pcm_f4 *__restric
 // distance in sklearn's expression.
 typedef const __attribute__((address_space(4))) double pcm_cd;
 
+template <typename RowPtr>
 __device__ __forceinline__ int nn_decide(double sx, double sy, double sz, float qx, float qy, float qz, float d1,
-                                         float d2, int k1, pcm_cf4 *rows, int mpad, const double *__restrict__ dst,
+                                         float d2, int k1, RowPtr rows, int mpad, const double *__restrict__ dst,
                                          double &e2) {
     // local bound: any row that could beat k1 lies within sqrt(D1) of q
     // (D1 = exact squared distance to k1), so |t| <= |q| + sqrt(D1) for every
@@ -324,7 +326,7 @@ __device__ __forceinline__ int nn_decide(double sx, double sy, double sz, float 
         double best = __builtin_huge_val();
         const int nch = mpad / kChunk;
         for (int c = 0; c < nch; ++c) {
-            pcm_cf4 *tk = rows + c * kChunk;
+            RowPtr tk = rows + c * kChunk;
             float mn = PCM_INF;
 #pragma unroll
             for (int k = 0; k < kChunk; k += 2) {
@@ -362,7 +364,8 @@ __device__ __forceinline__ void centroid3(const double *__restrict__ p, int n, d
 
 // One workgroup per destination cloud: centroid, rows, R.
 __global__ __launch_bounds__(kPrepThreads) void nn_prep_kernel(const double *__restrict__ dst, int m,
-                                                               NnHdr *__restrict__ hdr, pcm_f4 *__restrict__ rows) {
+                                                               NnHdr *__restrict__ hdr, pcm_f4 *__restrict__ rows,
+                                                               unsigned *__restrict__ arrive, unsigned *__restrict__ err) {
     constexpr int W = kPrepThreads / 64;
     __shared__ double red[3][W];
     __shared__ double tot[3];
@@ -393,46 +396,249 @@ __global__ __launch_bounds__(kPrepThreads) void nn_prep_kernel(const double *__r
         hdr[bi].c[0] = c[0]; hdr[bi].c[1] = c[1]; hdr[bi].c[2] = c[2];
         hdr[bi].R = R;
         hdr[bi].pad = 0;
+        if (arrive) arrive[(size_t)bi * 32] = 0u;  // pcm_icp's per-pair pass counter (kArriveStride)
+        if (err && bi == 0) *err = 0u;
     }
 }
 
-// ---- ICP kernel: one workgroup per (A, B) pair -----------------------------
+__device__ __forceinline__ void st_sc1_d(double *p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_sc1_d(const double *p) {
+    return __hip_atomic_load(const_cast<double *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
-#ifdef PCM_STAMPS  // profiling build: per-phase time of workgroup 0 (tools/tune_icp.py)
+// ---- ICP kernel: K workgroups per (A, B) pair -------------------------------
+//
+// Workgroup (pair, k) owns the source slice [k S, min(n, (k + 1) S)) in LDS
+// (float64, homogeneous).  Per pass it screens its slice, sums its 16 float64
+// partials (fixed-order DPP + LDS), stores them write-through and adds to the
+// pair's arrival counter; once all K partials of the pass are in (bounded
+// sc1 poll), EVERY workgroup of the pair reduces them in the same fixed order
+// and runs the same Kabsch on thread 0, so all K reach identical transforms
+// and the same stop decision without a broadcast (MI355X_MICROARCH.md
+// visibility row 1: sc1 stores, s_waitcnt vmcnt(0), agent atomic; sc1 polls
+// and loads).  K = 1 skips the hand-off.  The grid (b K workgroups of at most
+// 1024 threads and ~10 KB of LDS) is sized to be co-resident; a wait that
+// times out sets the sticky error word and ends the loop.
+
+struct IcpWs {
+    unsigned *arrive;  // [b] arrival counter per pair (own 128-B line each), zeroed by nn_prep_kernel
+    double *part;      // [2][b][K][16] partial sums, double-buffered by pass parity
+    unsigned *err;     // sticky error word
+};
+constexpr int kArriveStride = 32;  // unsigned words per pair
+constexpr unsigned kIcpMaxSpins = 1u << 22;
+
+// partial sums of NV doubles over the workgroup (fixed order), result in out[0..NV) for every thread
+// (only the first nw waves hold values: the others skip the reduction)
+template <int NV>
+__device__ __forceinline__ void wg_sum(double (&v)[NV], double (*red)[kIcpWaves], double *out, int nw) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (wave < nw) {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0xb1>(v[i]);   // quad_perm [1,0,3,2]
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0x4e>(v[i]);   // quad_perm [2,3,0,1]
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0x114>(v[i]);  // row_shr:4
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0x118>(v[i]);  // row_shr:8
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0x142>(v[i]);  // row_bcast:15
+#pragma unroll
+    for (int i = 0; i < NV; ++i) v[i] += dpp_move<0x143>(v[i]);  // row_bcast:31
+    if (lane == 63) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) red[i][wave] = v[i];
+    }
+    }
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        double s = 0.0;
+        for (int w = 0; w < nw; ++w) s += red[threadIdx.x][w];
+        out[threadIdx.x] = s;
+    }
+    __syncthreads();
+}
+
+// the pair's totals of the NV partials: this workgroup's own when K == 1,
+// else published, all K awaited and reduced in slice order.  Returns false
+// on a timed-out wait.
+template <int NV>
+__device__ __forceinline__ bool pair_sum(double *loc, double *tot, const IcpWs &ws, int pair, int k, int K, int b,
+                                         unsigned pass, int *sOk, double *stage) {
+    if (K == 1) {
+        if (threadIdx.x < NV) tot[threadIdx.x] = loc[threadIdx.x];
+        __syncthreads();
+        return true;
+    }
+    double *slot = ws.part + (((size_t)(pass & 1u) * b + pair) * K) * 16;
+    if (threadIdx.x < NV) st_sc1_d(slot + (size_t)k * 16 + threadIdx.x, loc[threadIdx.x]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned *ctr = ws.arrive + (size_t)pair * kArriveStride;
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned target = (pass + 1u) * (unsigned)K;
+        int ok = 1;
+        for (unsigned spins = 0;; ++spins) {
+            if ((int)(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - target) >= 0) break;
+            if (spins >= kIcpMaxSpins) {
+                ok = 0;
+                __hip_atomic_store(ws.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        *sOk = ok;
+    }
+    __syncthreads();
+    // every partial by its own thread (independent loads), then fixed-order
+    // sums over the K slices
+    // (stage: K * 16 doubles of LDS the caller does not need here)
+    if ((int)threadIdx.x < K * 16) stage[threadIdx.x] = ld_sc1_d(slot + threadIdx.x);
+    __syncthreads();
+    if (threadIdx.x < NV) {
+        double s = 0.0;
+        for (int q = 0; q < K; ++q) s += stage[q * 16 + threadIdx.x];
+        tot[threadIdx.x] = s;
+    }
+    __syncthreads();
+    return *sOk != 0;
+}
+
+#ifdef PCM_STAMPS  // profiling build: cycles per phase of workgroup 0, summed over passes (tools/tune_icp.py)
 __device__ unsigned long long g_icp_stamps[8];
-#define ICP_T(v) unsigned long long v = (blockIdx.x == 0 && threadIdx.x == 0) ? __builtin_amdgcn_s_memrealtime() : 0
-#define ICP_ACC(i, a, b) if (blockIdx.x == 0 && threadIdx.x == 0) acc[i] += (b) - (a)
+#define ICP_T(v) const unsigned long long v = (blockIdx.x == 0 && threadIdx.x == 0) ? __builtin_amdgcn_s_memtime() : 0
+#define ICP_ACC(i, t_a, t_b) if (blockIdx.x == 0 && threadIdx.x == 0) acc[i] += (t_b) - (t_a)
 #else
 #define ICP_T(v)
-#define ICP_ACC(i, a, b)
+#define ICP_ACC(i, t_a, t_b)
 #endif
 
+// Row-split screen of the workgroup's query slice: all 16 waves hold the same
+// queries (QPT per lane: query r*64 + lane), wave w screens the 32-row chunks
+// c = w, w + 16, ... (SGPR stream, as nn_screen), rescans its best chunk per
+// query, and the waves' results meet in LDS: a 64-bit atomicMin of
+// (order-preserving key of d1, row) gives the lowest-index minimum, then every
+// non-winning wave offers its d1 and every wave its second best to the d2 slot.
+// Per wave that is n/16 rows instead of n: the screen is a latency chain per
+// row, so splitting the rows over the waves is what shortens it.
+__device__ __forceinline__ unsigned f2ukey(float f) {
+    const unsigned u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);  // order-preserving, unsigned
+}
+__device__ __forceinline__ float ukey2f(unsigned k) {
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7fffffffu) : ~k);
+}
+
+template <int QPT>
+__device__ __forceinline__ void nn_screen_split(pcm_cf4 *rows, const pcm_f4 *__restrict__ rows_v, int mpad,
+                                                const float (&qx)[QPT], const float (&qy)[QPT],
+                                                const float (&qz)[QPT], unsigned long long *mk, unsigned *m2,
+                                                int nq) {
+    // wave index made provably uniform: the chunk index must live in an SGPR for
+    // the rows to stream through s_load (a VGPR index turns every row into a
+    // per-lane vector load)
+    const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    float b1[QPT], b2[QPT];
+    int c1[QPT];
+#pragma unroll
+    for (int r = 0; r < QPT; ++r) { b1[r] = PCM_INF; b2[r] = PCM_INF; c1[r] = 0; }
+    const int nch = mpad / kChunk;
+    for (int c = wave; c < nch; c += kIcpWaves) {
+        pcm_cf4 *tk = rows + c * kChunk;
+        float mn[QPT];
+#pragma unroll
+        for (int r = 0; r < QPT; ++r) mn[r] = PCM_INF;
+#pragma unroll
+        for (int k = 0; k < kChunk; k += 2) {
+            const pcm_f4 ta = tk[k], tb = tk[k + 1];
+#pragma unroll
+            for (int r = 0; r < QPT; ++r) {
+                const float da = row_d(ta, qx[r], qy[r], qz[r]);
+                const float db = row_d(tb, qx[r], qy[r], qz[r]);
+                mn[r] = __builtin_fminf(__builtin_fminf(mn[r], da), db);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < QPT; ++r) {
+            b2[r] = __builtin_amdgcn_fmed3f(b1[r], b2[r], mn[r]);
+            const bool lt = mn[r] < b1[r];
+            b1[r] = lt ? mn[r] : b1[r];
+            c1[r] = lt ? c : c1[r];
+        }
+    }
+    unsigned long long key[QPT];
+#pragma unroll
+    for (int r = 0; r < QPT; ++r) {
+        float e1 = PCM_INF, e2 = PCM_INF;
+        int j1 = 0;
+        if (b1[r] < PCM_INF) {  // this wave saw a finite row for the query
+            const pcm_f4 *tk = rows_v + c1[r] * kChunk;
+#pragma unroll 8
+            for (int k = 0; k < kChunk; ++k) {
+                const float d = row_d(tk[k], qx[r], qy[r], qz[r]);
+                e2 = __builtin_amdgcn_fmed3f(e1, e2, d);
+                const bool lt = d < e1;
+                e1 = lt ? d : e1;
+                j1 = lt ? k : j1;
+            }
+        }
+        const int i = r * 64 + lane;
+        key[r] = ((unsigned long long)f2ukey(e1) << 32) | (unsigned)(c1[r] * kChunk + j1);
+        if (i < nq) {
+            atomicMin(mk + i, key[r]);
+            atomicMin(m2 + i, f2ukey(__builtin_fminf(e2, b2[r])));
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < QPT; ++r) {  // the non-winning waves' minima are second-best candidates
+        const int i = r * 64 + lane;
+        if (i < nq && mk[i] != key[r]) atomicMin(m2 + i, (unsigned)(key[r] >> 32));
+    }
+    __syncthreads();
+}
+
+template <int QPT>
 __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restrict__ A, const double *__restrict__ B,
-                                                          int n, const double *__restrict__ init_pose, int max_it,
+                                                          int b, int n, int K, int S,
+                                                          const double *__restrict__ init_pose, int max_it,
                                                           double tol, const NnHdr *__restrict__ hdr,
-                                                          const pcm_f4 *__restrict__ rows_all,
+                                                          const pcm_f4 *__restrict__ rows_all, IcpWs ws,
                                                           double *__restrict__ T_out, double *__restrict__ dist_out,
                                                           int32_t *__restrict__ iters_out) {
     extern __shared__ __align__(16) unsigned char smem[];
-    double *sx = reinterpret_cast<double *>(smem);
-    double *sy = sx + n, *sz = sy + n, *sw = sz + n;
+    pcm_f4 *sRows = reinterpret_cast<pcm_f4 *>(smem);                      // [mpad] rows, for the rescans
+    unsigned long long *mk = reinterpret_cast<unsigned long long *>(smem + (size_t)nn_mpad(n) * 16);  // [S]
+    unsigned *m2 = reinterpret_cast<unsigned *>(mk + S);                   // [S] merged d2 key
+    double *sx = reinterpret_cast<double *>(m2 + ((S + 1) & ~1));
+    double *sy = sx + S, *sz = sy + S, *sw = sz + S;
     __shared__ double red[16][kIcpWaves];
+    __shared__ double loc[16];
     __shared__ double tot[16];
     __shared__ double sT[12];
-    __shared__ int sDone;
+    __shared__ int sDone, sOk;
 
-    const int bi = blockIdx.x, tid = threadIdx.x;
+    const int bi = blockIdx.x / K, k = blockIdx.x - bi * K, tid = threadIdx.x, lane = tid & 63;
+    const int j0 = k * S, j1 = min(n, j0 + S), ns = j1 - j0;  // this workgroup's slice
     const double *a = A + (size_t)bi * n * 3;
     const double *bb = B + (size_t)bi * n * 3;
     const double *P = init_pose ? init_pose + (size_t)bi * 16 : nullptr;
     const int mpad = nn_mpad(n);
-    const pcm_f4 *rows_v = rows_all + (size_t)bi * mpad;
-    pcm_cf4 *rows = (pcm_cf4 *)(uintptr_t)rows_v;
+    const pcm_f4 *rows_g = rows_all + (size_t)bi * mpad;
+    pcm_cf4 *rows = (pcm_cf4 *)(uintptr_t)rows_g;  // the screen: SGPR stream (wave-uniform)
+    const pcm_f4 *rows_v = sRows;                 // the rescans: per-lane chunks, from LDS
+    pcm_dma_to_lds(sRows, rows_g, 16 * mpad, tid >> 6, kIcpWaves);
     const double c[3] = {hdr[bi].c[0], hdr[bi].c[1], hdr[bi].c[2]};
+    const int nwq = min(kIcpWaves, (ns + 63) / 64);  // waves holding queries in the per-query loops
 
     // src = init_pose @ [A^T; 1] (icp.py:89-96), kept homogeneous
-    for (int j = tid; j < n; j += kIcpThreads) {
-        const double x = a[3 * (size_t)j], y = a[3 * (size_t)j + 1], z = a[3 * (size_t)j + 2];
+    for (int j = tid; j < ns; j += kIcpThreads) {
+        const double *pa = a + 3 * (size_t)(j0 + j);
+        const double x = pa[0], y = pa[1], z = pa[2];
         if (P) {
             sx[j] = ((P[0] * x + P[1] * y) + P[2] * z) + P[3];
             sy[j] = ((P[4] * x + P[5] * y) + P[6] * z) + P[7];
@@ -442,57 +648,72 @@ __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restri
             sx[j] = x; sy[j] = y; sz[j] = z; sw[j] = 1.0;
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the rows have landed
+    __syncthreads();
 
     double prev = 0.0;
     int it = 0;
+    unsigned pass = 0;
+    bool ok = true;
     double vw[9] = {1.0, 0.0, 0.0, 0.0, 1.0, 0.0, 0.0, 0.0, 1.0};  // thread 0's warm start
 #ifdef PCM_STAMPS
     unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
 #endif
     for (;; ++it) {
         ICP_T(t0);
-        // 1. nearest neighbours (each thread owns points tid, tid + kIcpThreads, ...),
-        //    and in the same sweep the sums for best_fit_transform (icp.py:23-29):
+        // 1. nearest neighbours of the slice (screen split over the waves),
+        //    then per query (thread tid) the exact decision and, in the same
+        //    sweep, the sums for best_fit_transform (icp.py:23-29):
         //    S = sum of (a - c)(b - c)^T about B's centroid c, so that
         //    H = S - n (ca - c)(cb - c)^T is the centred cross-covariance
-        //    without a second pass (c is within the clouds' extent, so the
-        //    correction is small and nothing cancels catastrophically)
+        //    without a second pass
+        for (int i = tid; i < ns; i += kIcpThreads) {
+            mk[i] = ~0ull;
+            m2[i] = ~0u;
+        }
+        float qx[QPT], qy[QPT], qz[QPT];
+#pragma unroll
+        for (int r = 0; r < QPT; ++r) {
+            const int q = min(r * 64 + lane, ns - 1);
+            qx[r] = (float)(sx[q] - c[0]);
+            qy[r] = (float)(sy[q] - c[1]);
+            qz[r] = (float)(sz[q] - c[2]);
+        }
+        __syncthreads();
+        nn_screen_split<QPT>(rows, rows_v, mpad, qx, qy, qz, mk, m2, ns);
+        ICP_T(t0b);
         double s16[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) s16[i] = 0.0;
-        for (int base = 0; base < n; base += kIcpThreads) {
-            const int q = min(base + tid, n - 1);
-            const float qx = (float)(sx[q] - c[0]);
-            const float qy = (float)(sy[q] - c[1]);
-            const float qz = (float)(sz[q] - c[2]);
-            float d1, d2;
-            int k1;
-            nn_screen(rows, rows_v, mpad, qx, qy, qz, d1, d2, k1);
-            if (base + tid < n) {
-                double e2;
-                const int k = nn_decide(sx[q], sy[q], sz[q], qx, qy, qz, d1, d2, k1, rows, mpad, bb, e2);
-                const double dist = sqrt(e2);
-                dist_out[(size_t)bi * n + q] = dist;
-                const double ax = sx[q], ay = sy[q], az = sz[q];
-                const double bx = bb[3 * (size_t)k], by = bb[3 * (size_t)k + 1], bz = bb[3 * (size_t)k + 2];
-                s16[0] += ax; s16[1] += ay; s16[2] += az;
-                s16[3] += bx; s16[4] += by; s16[5] += bz;
-                s16[6] += dist;
-                const double ux = ax - c[0], uy = ay - c[1], uz = az - c[2];
-                const double vx = bx - c[0], vy = by - c[1], vz = bz - c[2];
-                s16[7] += ux * vx; s16[8] += ux * vy; s16[9] += ux * vz;
-                s16[10] += uy * vx; s16[11] += uy * vy; s16[12] += uy * vz;
-                s16[13] += uz * vx; s16[14] += uz * vy; s16[15] += uz * vz;
-            }
+        for (int q = tid; q < ns; q += kIcpThreads) {
+            const unsigned long long key = mk[q];
+            const float d1 = ukey2f((unsigned)(key >> 32)), d2 = ukey2f(m2[q]);
+            const int k1 = (int)(unsigned)key;
+            const float fx = (float)(sx[q] - c[0]), fy = (float)(sy[q] - c[1]), fz = (float)(sz[q] - c[2]);
+            double e2;
+            const int kk = nn_decide(sx[q], sy[q], sz[q], fx, fy, fz, d1, d2, k1, rows, mpad, bb, e2);
+            const double dist = sqrt(e2);
+            dist_out[(size_t)bi * n + j0 + q] = dist;
+            const double ax = sx[q], ay = sy[q], az = sz[q];
+            const double bx = bb[3 * (size_t)kk], by = bb[3 * (size_t)kk + 1], bz = bb[3 * (size_t)kk + 2];
+            s16[0] += ax; s16[1] += ay; s16[2] += az;
+            s16[3] += bx; s16[4] += by; s16[5] += bz;
+            s16[6] += dist;
+            const double ux = ax - c[0], uy = ay - c[1], uz = az - c[2];
+            const double vx = bx - c[0], vy = by - c[1], vz = bz - c[2];
+            s16[7] += ux * vx; s16[8] += ux * vy; s16[9] += ux * vz;
+            s16[10] += uy * vx; s16[11] += uy * vy; s16[12] += uy * vz;
+            s16[13] += uz * vx; s16[14] += uz * vy; s16[15] += uz * vz;
         }
         ICP_T(t1);
-        block_sum<16, kIcpWaves>(s16, red, tot);
+        wg_sum<16>(s16, red, loc, nwq);
         ICP_T(t2);
+        ok = pair_sum<16>(loc, tot, ws, bi, k, K, b, pass++, &sOk, &red[0][0]);
+        ICP_T(t3);
         const double ca[3] = {tot[0] / n, tot[1] / n, tot[2] / n};
         const double cb[3] = {tot[3] / n, tot[4] / n, tot[5] / n};
         const double mean = tot[6] / n;
-        ICP_T(t3);
-        // 3. SVD / transform / convergence (icp.py:105-114)
+        // 3. SVD / transform / convergence (icp.py:105-114), identical in all K
         if (tid == 0) {
             const double ea[3] = {ca[0] - c[0], ca[1] - c[1], ca[2] - c[2]};
             const double eb[3] = {cb[0] - c[0], cb[1] - c[1], cb[2] - c[2]};
@@ -500,12 +721,12 @@ __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restri
             for (int i = 0; i < 3; ++i)
                 for (int j = 0; j < 3; ++j) H[3 * i + j] = tot[7 + 3 * i + j] - n * (ea[i] * eb[j]);
             kabsch(H, ca, cb, sT, vw);
-            sDone = (fabs(prev - mean) < tol) || (it + 1 >= max_it);
+            sDone = (fabs(prev - mean) < tol) || (it + 1 >= max_it) || !ok;
         }
         __syncthreads();
         ICP_T(t4);
         // 4. src = T src
-        for (int j = tid; j < n; j += kIcpThreads) {
+        for (int j = tid; j < ns; j += kIcpThreads) {
             const double x = sx[j], y = sy[j], z = sz[j], w = sw[j];
             sx[j] = ((sT[0] * x + sT[1] * y) + sT[2] * z) + sT[3] * w;
             sy[j] = ((sT[4] * x + sT[5] * y) + sT[6] * z) + sT[7] * w;
@@ -513,41 +734,52 @@ __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restri
         }
         prev = mean;
         ICP_T(t5);
-        ICP_ACC(0, t0, t1);
+        ICP_ACC(0, t0, t0b);
+        ICP_ACC(5, t0b, t1);
         ICP_ACC(1, t1, t2);
-        ICP_ACC(2, t2, t3);  // (empty since the covariance moved into the sweep)
+        ICP_ACC(2, t2, t3);
         ICP_ACC(3, t3, t4);
         ICP_ACC(4, t4, t5);
         if (sDone) break;  // uniform: written before the barrier above, rewritten only after two more
+        __syncthreads();   // the update is read by the next pass's query loads
     }
 #ifdef PCM_STAMPS
     if (blockIdx.x == 0 && threadIdx.x == 0)
-        for (int i = 0; i < 5; ++i) g_icp_stamps[i] = acc[i];
+        for (int i = 0; i < 6; ++i) g_icp_stamps[i] = acc[i];
 #endif
     __syncthreads();
-    // final: best_fit_transform(A, src) (icp.py:117)
-    double s6[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int j = tid; j < n; j += kIcpThreads) {
-        s6[0] += a[3 * (size_t)j]; s6[1] += a[3 * (size_t)j + 1]; s6[2] += a[3 * (size_t)j + 2];
+    // final: best_fit_transform(A, src) (icp.py:117): centroids of A and src,
+    // then H about them -- two pair-wide sums
+    double s6[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s6[i] = 0.0;
+    for (int j = tid; j < ns; j += kIcpThreads) {
+        const double *pa = a + 3 * (size_t)(j0 + j);
+        s6[0] += pa[0]; s6[1] += pa[1]; s6[2] += pa[2];
         s6[3] += sx[j]; s6[4] += sy[j]; s6[5] += sz[j];
     }
-    block_sum<6, kIcpWaves>(s6, red, tot);
+    wg_sum<16>(s6, red, loc, nwq);
+    ok = pair_sum<6>(loc, tot, ws, bi, k, K, b, pass++, &sOk, &red[0][0]) && ok;
     const double ca[3] = {tot[0] / n, tot[1] / n, tot[2] / n};
     const double cs[3] = {tot[3] / n, tot[4] / n, tot[5] / n};
-    double h[9] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    for (int j = tid; j < n; j += kIcpThreads) {
-        const double ax = a[3 * (size_t)j] - ca[0], ay = a[3 * (size_t)j + 1] - ca[1], az = a[3 * (size_t)j + 2] - ca[2];
+    double h[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) h[i] = 0.0;
+    for (int j = tid; j < ns; j += kIcpThreads) {
+        const double *pa = a + 3 * (size_t)(j0 + j);
+        const double ax = pa[0] - ca[0], ay = pa[1] - ca[1], az = pa[2] - ca[2];
         const double bx = sx[j] - cs[0], by = sy[j] - cs[1], bz = sz[j] - cs[2];
         h[0] += ax * bx; h[1] += ax * by; h[2] += ax * bz;
         h[3] += ay * bx; h[4] += ay * by; h[5] += ay * bz;
         h[6] += az * bx; h[7] += az * by; h[8] += az * bz;
     }
-    block_sum<9, kIcpWaves>(h, red, tot);
-    if (tid == 0) {
+    wg_sum<16>(h, red, loc, nwq);
+    ok = pair_sum<9>(loc, tot, ws, bi, k, K, b, pass++, &sOk, &red[0][0]) && ok;
+    if (k == 0 && tid == 0) {
         double T[12];
         kabsch(tot, ca, cs, T);
         double *o = T_out + (size_t)bi * 16;
-        for (int i = 0; i < 12; ++i) o[i] = T[i];
+        for (int i = 0; i < 12; ++i) o[i] = ok ? T[i] : __builtin_nan("");
         o[12] = 0.0; o[13] = 0.0; o[14] = 0.0; o[15] = 1.0;
         iters_out[bi] = it;
     }
@@ -615,21 +847,46 @@ size_t nn_ws_bytes(int b, int m) {
     return (size_t)b * sizeof(NnHdr) + (size_t)b * nn_mpad(m) * sizeof(pcm_f4);
 }
 
+// pcm_icp: the rows, then the pass counters, the error word and the partials
+constexpr int kIcpMaxSlices = 16;
+size_t icp_ws_bytes(int b, int m) {
+    const size_t base = (nn_ws_bytes(b, m) + 127) / 128 * 128;
+    return base + (size_t)b * kArriveStride * 4 + 128 + (size_t)2 * b * kIcpMaxSlices * 16 * 8;
+}
+IcpWs icp_ws(void *workspace, int b, int m) {
+    char *p = (char *)workspace + (nn_ws_bytes(b, m) + 127) / 128 * 128;
+    IcpWs w;
+    w.arrive = (unsigned *)p;
+    w.err = (unsigned *)(p + (size_t)b * kArriveStride * 4);
+    w.part = (double *)(p + (size_t)b * kArriveStride * 4 + 128);
+    return w;
+}
+
 int launch_prep(const double *dst, int b, int m, void *workspace, hipStream_t s, const NnHdr **hdr,
-                const pcm_f4 **rows) {
+                const pcm_f4 **rows, unsigned *arrive = nullptr, unsigned *err = nullptr) {
     NnHdr *h = reinterpret_cast<NnHdr *>(workspace);
     pcm_f4 *r = reinterpret_cast<pcm_f4 *>(h + b);
-    hipLaunchKernelGGL(nn_prep_kernel, dim3(b), dim3(kPrepThreads), 0, s, dst, m, h, r);
+    hipLaunchKernelGGL(nn_prep_kernel, dim3(b), dim3(kPrepThreads), 0, s, dst, m, h, r, arrive, err);
     *hdr = h;
     *rows = r;
     return pcm_launch_status();
+}
+
+// slices per pair: fill the chip (K b <= 256 one-per-CU workgroups), at least
+// 64 points each, at most 1024 (16 per lane)
+int icp_slices(int b, int n) {
+    int K = 256 / b;
+    K = K < 1 ? 1 : (K > kIcpMaxSlices ? kIcpMaxSlices : K);
+    const int most = (n + 63) / 64, least = (n + 1023) / 1024;
+    K = K < most ? K : most;
+    return K > least ? K : least;
 }
 
 }  // namespace
 
 extern "C" size_t pcm_icp_workspace_bytes(int b, int m) {
     if (b <= 0 || m <= 0) return 0;
-    return nn_ws_bytes(b, m);
+    return icp_ws_bytes(b, m);
 }
 
 extern "C" int pcm_icp(const double *A, const double *B, int b, int n, const double *init_pose, int max_iterations,
@@ -639,19 +896,55 @@ extern "C" int pcm_icp(const double *A, const double *B, int b, int n, const dou
     if (b == 0) return PCM_OK;
     if (n == 0 || !A || !B || !T_out || !distances || !iterations) return PCM_ERR_INVALID_ARG;
     if (n > kIcpMaxN || b > 65535) return PCM_ERR_UNSUPPORTED;
-    if (!workspace || workspace_bytes < nn_ws_bytes(b, n)) return PCM_ERR_WORKSPACE;
+    if (!workspace || workspace_bytes < icp_ws_bytes(b, n)) return PCM_ERR_WORKSPACE;
     hipStream_t s = (hipStream_t)stream;
     const NnHdr *hdr;
     const pcm_f4 *rows;
-    if (launch_prep(B, b, n, workspace, s, &hdr, &rows) != PCM_OK) return PCM_ERR_LAUNCH;
-    const size_t lds = (size_t)n * (32 + 4);
-    if (lds > 64 * 1024 &&
-        hipFuncSetAttribute((const void *)icp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) !=
-            hipSuccess)
-        return PCM_ERR_LAUNCH;
-    hipLaunchKernelGGL(icp_kernel, dim3(b), dim3(kIcpThreads), lds, s, A, B, n, init_pose, max_iterations,
-                       tolerance, hdr, rows, T_out, distances, iterations);
+    const IcpWs ws = icp_ws(workspace, b, n);
+    if (launch_prep(B, b, n, workspace, s, &hdr, &rows, ws.arrive, ws.err) != PCM_OK) return PCM_ERR_LAUNCH;
+    const int K = icp_slices(b, n);
+    const int S = (n + K - 1) / K;  // points per slice (<= 1024)
+    const int qpt = S <= 64 ? 1 : S <= 128 ? 2 : S <= 256 ? 4 : S <= 512 ? 8 : 16;
+    const size_t lds = (size_t)nn_mpad(n) * 16 + (size_t)S * (8 + 4 + 32) + 8;
+    auto launch = [&](auto kfn) -> int {
+        if (lds > 64 * 1024 &&
+            hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+            return PCM_ERR_LAUNCH;
+        hipLaunchKernelGGL(kfn, dim3((unsigned)(b * K)), dim3(kIcpThreads), lds, s, A, B, b, n, K, S, init_pose,
+                           max_iterations, tolerance, hdr, rows, ws, T_out, distances, iterations);
+        return PCM_OK;
+    };
+    int rc;
+    switch (qpt) {
+        case 1: rc = launch(icp_kernel<1>); break;
+        case 2: rc = launch(icp_kernel<2>); break;
+        case 4: rc = launch(icp_kernel<4>); break;
+        case 8: rc = launch(icp_kernel<8>); break;
+        default: rc = launch(icp_kernel<16>); break;
+    }
+    if (rc != PCM_OK) return rc;
     return pcm_launch_status();
+}
+
+#ifdef PCM_STAMPS
+extern "C" int pcm_tune_read_icp_stamps(unsigned long long *host, int n) {
+    if (n > 8) n = 8;
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_icp_stamps), n * sizeof(unsigned long long)) == hipSuccess
+               ? PCM_OK : PCM_ERR_LAUNCH;
+}
+#endif
+
+// sticky device-side error of the last pcm_icp on `workspace` (a timed-out
+// wait between the workgroups of a pair): PCM_OK or PCM_ERR_LAUNCH; synchronises.
+extern "C" int pcm_icp_workspace_status(const void *workspace, size_t workspace_bytes, int b, int n, void *stream) {
+    if (b <= 0 || n <= 0) return PCM_OK;
+    if (!workspace || workspace_bytes < icp_ws_bytes(b, n)) return PCM_ERR_WORKSPACE;
+    unsigned err = 0;
+    const IcpWs ws = icp_ws(const_cast<void *>(workspace), b, n);
+    if (hipMemcpyAsync(&err, ws.err, 4, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+        return PCM_ERR_LAUNCH;
+    return err ? PCM_ERR_LAUNCH : PCM_OK;
 }
 
 extern "C" int pcm_nearest_neighbor(const double *src, const double *dst, int b, int n, int m, double *distances,
@@ -671,13 +964,6 @@ extern "C" int pcm_nearest_neighbor(const double *src, const double *dst, int b,
     return pcm_launch_status();
 }
 
-#ifdef PCM_STAMPS
-extern "C" int pcm_tune_read_icp_stamps(unsigned long long *host, int n) {
-    if (n > 8) n = 8;
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_icp_stamps), n * sizeof(unsigned long long)) == hipSuccess
-               ? PCM_OK : PCM_ERR_LAUNCH;
-}
-#endif
 
 extern "C" int pcm_best_fit_transform(const double *A, const double *B, int b, int n, double *T_out, void *stream) {
     if (b < 0 || n < 0) return PCM_ERR_INVALID_ARG;

@@ -27,7 +27,8 @@ EXPORTED = (
     "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward", "pcm_emd_workspace_status",
     "pcm_chamfer_forward_f16", "pcm_chamfer_backward_f16",
     "pcm_chamfer_loss_grad",
-    "pcm_icp_workspace_bytes", "pcm_icp", "pcm_nearest_neighbor", "pcm_best_fit_transform",
+    "pcm_icp_workspace_bytes", "pcm_icp", "pcm_icp_workspace_status", "pcm_nearest_neighbor",
+    "pcm_best_fit_transform",
     "pcm_npy_cloud_points", "pcm_npy_load_clouds",
 )
 
@@ -108,6 +109,8 @@ def load_library():
     cd = ctypes.c_double
     L.pcm_icp.restype = ci
     L.pcm_icp.argtypes = [vp, vp, ci, ci, vp, ci, cd, vp, vp, vp, vp, cs, vp]
+    L.pcm_icp_workspace_status.restype = ci
+    L.pcm_icp_workspace_status.argtypes = [vp, cs, ci, ci, vp]
     L.pcm_icp_workspace_bytes.restype = cs
     L.pcm_icp_workspace_bytes.argtypes = [ci, ci]
     L.pcm_nearest_neighbor.restype = ci
@@ -417,6 +420,15 @@ def icp(A, B, init_pose, max_iterations: int, tolerance: float, T_out, distances
         _check(load_library().pcm_icp(
             _ptr(A), _ptr(B), b, n, _ptr(init_pose), int(max_iterations), float(tolerance), _ptr(T_out),
             _ptr(distances), _ptr(iterations), _ptr(workspace), workspace.numel(), _stream(dev)), "pcm_icp")
+
+
+def icp_workspace_status(workspace, b: int, n: int) -> None:
+    """Raise PcmError if the last pcm_icp on `workspace` hit a device-side
+    timeout between the workgroups of a pair (synchronises the current stream)."""
+    dev = workspace.device
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_icp_workspace_status(_ptr(workspace), workspace.numel(), b, n, _stream(dev)),
+               "pcm_icp_workspace_status")
 
 
 def nearest_neighbor(src, dst, distances, indices, workspace=None) -> None:

@@ -205,7 +205,8 @@ int pcm_emd_backward(const float *xyz1, const float *xyz2, int b, int n,
  *   iterations [b] = the reference's returned loop index i.
  * A prep launch writes B's float32 screening rows into `workspace`
  * (pcm_icp_workspace_bytes(b, n) bytes, content on entry irrelevant); then the
- * whole loop runs in one launch (one workgroup per pair).  Needs
+ * whole loop runs in one launch (each pair's source points split over K <= 16
+ * workgroups, K b <= 256, so a batch of one pair still fills 16 CUs).  Needs
  * max_iterations >= 1 (the reference fails otherwise), 0 < n <= 4096
  * (else PCM_ERR_UNSUPPORTED).  Non-finite inputs give unspecified values (the
  * reference's sklearn rejects them; the Python wrapper does the same).
@@ -214,6 +215,14 @@ size_t pcm_icp_workspace_bytes(int b, int m);
 int pcm_icp(const double *A, const double *B, int b, int n, const double *init_pose, int max_iterations,
             double tolerance, double *T_out, double *distances, int32_t *iterations, void *workspace,
             size_t workspace_bytes, void *stream);
+
+/*
+ * Device-side failure of the last pcm_icp on `workspace`: a pair's source
+ * points are split over up to 16 workgroups that meet once per pass; a wait
+ * that timed out (workgroups that could not all be resident) sets an error
+ * word: PCM_ERR_LAUNCH, and the transforms are NaN.  Synchronises `stream`.
+ */
+int pcm_icp_workspace_status(const void *workspace, size_t workspace_bytes, int b, int n, void *stream);
 
 /*
  * nearest_neighbor (utils/icp.py:49-65, sklearn NearestNeighbors(n_neighbors=1)):

@@ -16,21 +16,28 @@ if TRAIN not in sys.path:
 pytestmark = pytest.mark.gpu
 
 
-def test_generator_forward_gpu_vs_reference_golden(cuda):
+@pytest.mark.parametrize("channels_last", [False, True])
+def test_generator_forward_gpu_vs_reference_golden(cuda, channels_last):
+    # channels_last: NHWC activations (TrainStep's option); MIOpen's NHWC
+    # kernels sum in other orders, so the same tolerance applies
     import fenet
     z = np.load(os.path.join(HERE, "golden", "fenet_golden.npz"))
     g = fenet.seeded_init(fenet.Generator(1024), int(z["seed"])).to(cuda).train()
+    img = torch.from_numpy(z["img"]).to(cuda)
+    if channels_last:
+        g = g.to(memory_format=torch.channels_last)
+        img = img.contiguous(memory_format=torch.channels_last)
     with torch.no_grad():
-        out = g(torch.from_numpy(z["img"]).to(cuda))
+        out = g(img)
     for name, t in zip(("pc1", "pc2", "pc3"), out):
         # MIOpen / hipBLASLt fp32 kernels sum in other orders than the CPU reference
         np.testing.assert_allclose(t.cpu().numpy(), z[name], rtol=2e-3, atol=2e-3, err_msg=name)
 
 
-@pytest.mark.parametrize("epoch", [1, 31])
-def test_train_step_losses_match_oracle(cuda, oracle, epoch):
+@pytest.mark.parametrize("epoch,channels_last", [(1, False), (31, False), (1, True)])
+def test_train_step_losses_match_oracle(cuda, oracle, epoch, channels_last):
     import train_step as T
-    step = T.TrainStep(device=cuda, emd_iters=50, seed=1)
+    step = T.TrainStep(device=cuda, emd_iters=50, seed=1, channels_last=channels_last)
     step.set_epoch(epoch)
     images, points = T.synthetic_batch(2, 1024, cuda, seed=5)
     cap = []  # the clouds the step's own forward produced (the auction is input-sensitive)

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
-"""Time pcm_icp / pcm_nearest_neighbor across cloud sizes (per-pass cost split
-into the n^2 scan and the per-pass constant: reductions + 3x3 SVD).
+"""Time pcm_icp / pcm_nearest_neighbor across cloud sizes and batch sizes
+(per-pass cost of the whole ICP loop; the batch of 1 is testnet.py's call).
 
-ICP_STAMPS=1: use the profiling build (make -C 3d-pointcloudreconstruction_amd/csrc
-stamps) and print workgroup 0's time per phase of one pass."""
+ICP_STAMPS=1: the profiling build (make -C 3d-pointcloudreconstruction_amd/csrc
+stamps): cycles per phase of workgroup 0, per pass."""
 import ctypes
 import os
 import sys
@@ -11,9 +11,9 @@ import sys
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3d-pointcloudreconstruction_amd", "metric"))
 if os.environ.get("ICP_STAMPS"):
     os.environ["PCM_HIP_LIB"] = os.path.join(ROOT, "3d-pointcloudreconstruction_amd", "lib", "libpcm_hip_stamps.so")
-sys.path.insert(0, os.path.join(ROOT, "3d-pointcloudreconstruction_amd", "metric"))
 import pcm_hip  # noqa: E402
 
 
@@ -32,8 +32,8 @@ def time_us(fn, reps=3):
 def main():
     dev = torch.device("cuda:0")
     g = torch.Generator(device="cpu").manual_seed(7)
-    b = int(os.environ.get("ICP_B", "32"))
-    for n in (64, 256, 1024, 2048):
+    for b, n in [(int(x.split("x")[0]), int(x.split("x")[1])) for x in
+                 os.environ.get("ICP_CASES", "1x1024,32x1024,100x1024,32x256,8x2048,2x4096").split(",")]:
         A = (torch.randn(b, n, 3, generator=g, dtype=torch.float64) * 0.3).to(dev)
         B = A + 0.01 * torch.randn(b, n, 3, generator=g, dtype=torch.float64).to(dev)
         T = torch.empty(b, 4, 4, dtype=torch.float64, device=dev)
@@ -53,10 +53,10 @@ def main():
             buf = (ctypes.c_ulonglong * 8)()
             L.pcm_tune_read_icp_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int]
             L.pcm_tune_read_icp_stamps(ctypes.cast(buf, ctypes.c_void_p), 8)
-            names = ["screen+decide", "sum7", "H+sum9", "kabsch+barrier", "update"]
-            print("   per pass (us): " + ", ".join(f"{nm} {buf[i] / 100.0 / 11:.2f}" for i, nm in enumerate(names)))
-        print(f"n={n:5d} b={b}: icp 1 pass {res[0]:8.1f} us, per extra pass {per_pass:8.1f} us "
-              f"({n * n / per_pass / 1e3:.2f} Gpair/s per pair-WG); nearest_neighbor {nn_us:7.1f} us", flush=True)
+            names = ["screen", "wg-sum", "pair hand-off", "kabsch", "update", "decide"]
+            print("   cycles per pass: " + ", ".join(f"{nm} {buf[i] / 11:.0f}" for i, nm in enumerate(names)))
+        print(f"n={n:5d} b={b:3d}: icp 1 pass {res[0]:8.1f} us, per extra pass {per_pass:8.1f} us "
+              f"({b * n * n / per_pass / 1e3:.2f} Gpair/s); nearest_neighbor {nn_us:7.1f} us", flush=True)
 
 
 if __name__ == "__main__":

@@ -75,6 +75,7 @@ constexpr int kMaxHelpers = 31;
 constexpr int kBoardWords = 32;      // per batch element: gen, quit, jn, err (128-B line each group)
 constexpr int kSpinLimit = 1 << 22;  // bounded polls (sticky error word on timeout)
 constexpr int kDefaultOffloadMin = 24;  // misses above which an iteration is offloaded
+constexpr int kDefaultTailMax = 16;     // bidders at or below which an iteration runs in tail mode
 constexpr int kDefaultWsplit = 1;       // most waves one miss's scan is split over (2, 4: measured slower at config 3 and the training call)
 
 typedef unsigned long long centry;   // low 32 bits: object id (-1 unused), high 32: s bits
@@ -384,6 +385,28 @@ __device__ __forceinline__ bool scan_fast_finish(const LaneTop &t, float x1, flo
     return b2 > T;
 }
 
+// one wave's part of a split exact bid: objects r*64 + lane + 64*W*i (every
+// lane ascending), exact values, the wave's (best, argbest, better)
+// returned wave-uniform.  The top-2 of the whole cloud is the top-2 of the
+// parts' top-2s (part_merge).
+__device__ __forceinline__ void part_top2(float x1, float y1, float z1, const float *Qc, const float *price, int n,
+                                          int r, int W, float &b1, int &kb, float &b2) {
+    const int lane = threadIdx.x & 63;
+    LaneTop t;
+    lane_top_init(t);
+    for (int k = r * 64 + lane; k < n; k += 64 * W) lane_top_push(t, value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), price[k]), k);
+    wave_top2(t.a1, t.q1, t.a2, t.q2, b1, kb, b2);
+}
+// merge of W parts' results (lanes < W read part i's slot); the second
+// entries carry no id: a tie at the best already lists the lowest id first
+__device__ __forceinline__ void part_merge(const float *pb1, const int *pkb, const float *pb2, int W, float &b1,
+                                           int &kb, float &b2) {
+    const int lane = threadIdx.x & 63;
+    const bool in = lane < W;
+    wave_top2(in ? pb1[lane] : -PCM_INF, in ? pkb[lane] : 0x7fffffff, in ? pb2[lane] : -PCM_INF, 0x7fffffff, b1, kb,
+              b2);
+}
+
 // one wave: the full bid of point (x1, y1, z1) with a rebuilt cache
 template <bool kSc1>
 __device__ __forceinline__ void scan_full(float x1, float y1, float z1, const float *Qc, const float *price, int n,
@@ -625,7 +648,7 @@ __device__ __forceinline__ void helper_item(const EmdWs &ws, size_t base, int i,
 
 struct KArgs {
     const float *xyz1, *xyz2;
-    int b, n, iters, H, offload_min, diag, wmax;
+    int b, n, iters, H, offload_min, diag, wmax, tail_max;
     float eps;
     float *dist;
     int32_t *ass_out;
@@ -681,7 +704,9 @@ __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank
 // master role: the auction of one batch element
 template <bool kG, bool kStage, bool kStageP>
 __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *smem) {
-    __shared__ int sNu[2], sNm, sColl;
+    __shared__ int sNu[2], sNm, sColl, sChainJ;
+    __shared__ float sPb1[kWaves], sPb2[kWaves];  // split bids: each wave's part
+    __shared__ int sPkb[kWaves];
     const int n = a.n, iters = a.iters;
     const float eps = a.eps;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -692,7 +717,8 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     centry *C = ws.cache + base * kL;
     float *CT = ws.CT + base;
     const bool hist = a.diag == kDiagHist;
-    const bool timers = a.diag == kDiagTimers && batch == 0 && tid == 0;
+    // diag >= 2: timers of batch element diag - 2
+    const bool timers = a.diag >= kDiagTimers && batch == a.diag - kDiagTimers && tid == 0;
 
     AState<kG> st;
     char *lp = (char *)smem;
@@ -750,17 +776,21 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     };
 
     int gen = 0;  // jobs posted so far
-    // timers (diag 2): cycles of batch 0 per phase, kept by thread 0
-    unsigned long long tm[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tprev = __builtin_amdgcn_s_memtime();
+    // timers (diag >= 2): cycles per phase, kept by thread 0 in LDS (not in
+    // registers the whole kernel would reserve)
+    __shared__ unsigned long long sTm[13];  // [12] = the previous stamp
+    if (timers) {
+        for (int i = 0; i < 12; ++i) sTm[i] = 0;
+        sTm[12] = __builtin_amdgcn_s_memtime();
+    }
     const unsigned long long t_start = __builtin_amdgcn_s_memrealtime();
 #define PCM_EMD_PHASE(i)                                                  \
     if (timers) {                                                         \
         const unsigned long long tn = __builtin_amdgcn_s_memtime();      \
-        tm[i] += tn - tprev;                                              \
-        tprev = tn;                                                       \
+        sTm[i] += tn - sTm[12];                                           \
+        sTm[12] = tn;                                                     \
     }
-    int active = 0;
+    int active = 0, chain_its = 0, tail_its = 0;
     for (int it = 0; it < iters; ++it) {
         const bool last = (it == iters - 1);
         const int cur = it & 1;
@@ -774,6 +804,105 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         // the other list's counter was last read at the start of iteration it-1
         if (tid == 0) sNu[cur ^ 1] = 0;
 
+        // ---- chain mode: a single bidder.  Its bid can only collide with
+        // itself, so every later iteration is bid -> resolve -> assign of one
+        // point, and the evicted owner (if any) is the next iteration's only
+        // bidder.  Wave 0 runs the chain alone, with no workgroup barrier per
+        // iteration; the resolution is the claim/assign phases' below for
+        // one bidder (solo rule, else the 1e-6 window).
+        if (it > 0 && nu == 1 && a.tail_max > 0) {
+            int j = Ucur[0];
+            for (; it < iters; ++it) {
+                ++active;
+                ++chain_its;
+                PCM_EMD_PHASE(8);
+                if (hist && tid == 0) {
+                    atomicAdd(&a.stats[2 * it], 1);
+                    atomicAdd(&a.stats[2 * it + 1], 1);
+                }
+                // the bid, split over the 16 waves
+                {
+                    float b1, b2;
+                    int kb;
+                    part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, wave, kWaves, b1, kb, b2);
+                    if (lane == 0) { sPb1[wave] = b1; sPkb[wave] = kb; sPb2[wave] = b2; }
+                }
+                __syncthreads();
+                PCM_EMD_PHASE(9);
+                if (wave == 0) {
+                    float b1, b2;
+                    int kb;
+                    part_merge(sPb1, sPkb, sPb2, kWaves, b1, kb, b2);
+                    int next = j;  // no bid / not won: j bids again
+                    if ((unsigned)kb < (unsigned)n && lane == 0) {
+                        if (it == iters - 1) {
+                            st.ass[j] = kb;
+                        } else {
+                            const float inc = b1 - b2 + eps;
+                            const bool coll = atomicMax(&st.mx[kb], f2key(inc)) > 0;
+                            bool won = true;
+                            if (coll || !(eps > 0.f)) {
+                                const double bi = (double)inc, mi = (double)key2f(st.ld_max(kb));
+                                won = bi - 1e-6 <= mi && mi <= bi + 1e-6;
+                            }
+                            if (won) {
+                                const int old = st.inv[kb];
+                                if (old != -1) st.ass[old] = -1;
+                                st.inv[kb] = j;
+                                st.ass[j] = kb;
+                                st.price[kb] += inc;
+                                st.mx[kb] = f2key(-1e9f);
+                                next = old;  // -1: nobody left to bid
+                            }
+                        }
+                    }
+                    if (lane == 0) sChainJ = next;
+                }
+                __syncthreads();
+                PCM_EMD_PHASE(10);
+                j = sChainJ;
+                if (j < 0) break;
+            }
+            break;
+        }
+
+        // ---- tail mode (few bidders; the count never grows): one wave per
+        // bidder, full scan without a cache, no cache-bid phase
+        if (it > 0 && nu <= a.tail_max) {
+            ++tail_its;
+            // W waves per bidder (16 / the next power of two >= nu), each
+            // scanning every W-th 64-object chunk; the bidder's first wave merges
+            const int W = nu <= 1 ? 16 : (nu <= 2 ? 8 : (nu <= 4 ? 4 : (nu <= 8 ? 2 : 1)));
+            const int q = wave / W, r = wave - q * W;
+            if (W == 1) {  // whole bids, one wave each (more than 8 bidders)
+                for (int u = wave; u < nu; u += kWaves) {
+                    const int j = Ucur[u];
+                    float b1, b2;
+                    int kb;
+                    part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, 0, 1, b1, kb, b2);
+                    if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
+                }
+            } else if (q < nu) {
+                const int j = Ucur[q];
+                float b1, b2;
+                int kb;
+                part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, r, W, b1, kb, b2);
+                if (lane == 0) { sPb1[wave] = b1; sPkb[wave] = kb; sPb2[wave] = b2; }
+            }
+            if (hist && tid == 0) {
+                atomicAdd(&a.stats[2 * it], nu);
+                atomicAdd(&a.stats[2 * it + 1], nu);
+            }
+            __syncthreads();
+            if (W > 1 && q < nu && r == 0) {
+                float b1, b2;
+                int kb;
+                part_merge(sPb1 + wave, sPkb + wave, sPb2 + wave, W, b1, kb, b2);
+                if (lane == 0) place_bid(st, Ucur[q], kb, b1 - b2 + eps, n, &sColl);
+            }
+            __syncthreads();
+            PCM_EMD_PHASE(1);
+        } else {
         // ---- B1: bids from the seed (iteration 0) or the caches; misses listed
         if (it == 0) {
             for (int u = tid; u < nu; u += kEmdThreads) {
@@ -886,6 +1015,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             __syncthreads();
         }
         PCM_EMD_PHASE(1);
+        }  // not tail mode
 
         // ---- C: claim -- lowest bidder inside the reference's 1e-6 window
         //      (emd_cuda.cu:181-194); the key carries the iteration.  Skipped
@@ -947,8 +1077,10 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     if (a.stats && tid == 0)  // diagnostics: whole-auction wall time per batch element
         a.stats[3 * iters + 16 + batch] = (int)(__builtin_amdgcn_s_memrealtime() - t_start);
     if (timers) {
-        for (int i = 0; i < 12; ++i) a.stats[2 * iters + i] = (int)(tm[i] >> 4);  // units of 16 cycles
+        for (int i = 0; i < 12; ++i) a.stats[2 * iters + i] = (int)(sTm[i] >> 4);  // units of 16 cycles
         a.stats[2 * iters + 12] = active;
+        a.stats[2 * iters + 13] = tail_its;
+        a.stats[2 * iters + 14] = chain_its;
     }
 
     // ---- CalcDist (emd_cuda.cu:217-226): deltas xyz1 - xyz2
@@ -1069,7 +1201,7 @@ int default_helpers(int b, int n) {
 
 int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters, float *dist,
                int32_t *assignment, float *price, void *workspace, size_t workspace_bytes, int helpers,
-               int offload_min, int diag, int wsplit, int32_t *stats, void *stream) {
+               int offload_min, int diag, int wsplit, int tail_max, int32_t *stats, void *stream) {
     // emd_cuda.cu:236-249 (n == m is enforced by the single n here)
     if (b < 0 || n < 0 || b > 512 || n % 1024 != 0 || iters < 1) return PCM_ERR_INVALID_ARG;
     if (b == 0 || n == 0) return PCM_OK;
@@ -1111,8 +1243,9 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     // one workgroup per CU when helpers run: a master never shares its SIMDs
     if (H > 0 && lds < 84 * 1024) lds = 84 * 1024;
     KArgs ka{xyz1, xyz2, b, n, iters, H, offload_min >= 0 ? offload_min : kDefaultOffloadMin,
-             stats ? (diag == kDiagTimers ? kDiagTimers : kDiagHist) : 0,
-             wsplit > 0 ? wsplit : kDefaultWsplit, eps, dist, assignment, price, stats};
+             stats ? (diag >= kDiagTimers ? diag : kDiagHist) : 0,
+             wsplit > 0 ? wsplit : kDefaultWsplit, tail_max >= 0 ? tail_max : kDefaultTailMax, eps, dist, assignment,
+             price, stats};
     const unsigned grid = (unsigned)(b * (1 + H));
     auto launch = [&](auto kfn) -> int {
         if (lds > 64 * 1024 &&
@@ -1137,7 +1270,7 @@ extern "C" int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int 
                                int iters, float *dist, int32_t *assignment, float *price,
                                void *workspace, size_t workspace_bytes, void *stream) {
     return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, price, workspace, workspace_bytes, -1, -1, 0,
-                      0, nullptr, stream);
+                      0, -1, nullptr, stream);
 }
 
 // Tuning / diagnostics entry.  helpers, offload_min < 0: the defaults.
@@ -1151,9 +1284,9 @@ extern "C" int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int 
 extern "C" int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
                                         float *dist, int32_t *assignment, float *price, void *workspace,
                                         size_t workspace_bytes, int helpers, int offload_min, int diag,
-                                        int wsplit, int32_t *stats, void *stream) {
+                                        int wsplit, int tail_max, int32_t *stats, void *stream) {
     return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, price, workspace, workspace_bytes, helpers,
-                      offload_min, diag, wsplit, stats, stream);
+                      offload_min, diag, wsplit, tail_max, stats, stream);
 }
 
 // sticky device-side error of the last pcm_emd_forward on this workspace

@@ -32,11 +32,12 @@ int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, const uint16
 // helpers: helper workgroups per batch element (-1 = default); offload_min:
 // misses above which an iteration's full scans go to the helpers (-1 =
 // default); diag: 1 = per-iteration counts, 2 = phase timers (csrc/emd.hip);
-// wsplit: most waves a full scan is split over (1, 2, 4; <= 0 = default)
+// wsplit: most waves a full scan is split over (1, 2, 4; <= 0 = default);
+// tail_max: bidders at or below which an iteration runs in tail mode (-1 = default, 0 = never)
 int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
                              float *dist, int32_t *assignment, float *price, void *workspace,
                              size_t workspace_bytes, int helpers, int offload_min, int diag, int wsplit,
-                             int32_t *stats, void *stream);
+                             int tail_max, int32_t *stats, void *stream);
 #ifdef __cplusplus
 }
 #endif

@@ -98,7 +98,7 @@ def load_library():
     L.pcm_emd_workspace_status.restype = ci
     L.pcm_emd_workspace_status.argtypes = [vp, cs, ci, ci, vp]
     L.pcm_tune_emd_forward_cfg.restype = ci
-    L.pcm_tune_emd_forward_cfg.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, vp, cs, ci, ci, ci, ci, vp, vp]
+    L.pcm_tune_emd_forward_cfg.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, vp, cs, ci, ci, ci, ci, ci, vp, vp]
     L.pcm_chamfer_loss_grad.restype = ci
     L.pcm_chamfer_loss_grad.argtypes = [vp, vp, ci, ci, ci, cf, cf, vp, vp, vp, vp, vp, vp, vp, vp, cs, vp]
     L.pcm_tune_chamfer_loss_grad.restype = ci
@@ -353,18 +353,21 @@ def emd_workspace(dev: torch.device, b: int, n: int) -> torch.Tensor:
 
 
 def emd_forward(xyz1, xyz2, eps: float, iters: int, dist, assignment, price=None,
-                workspace=None, helpers=None, offload_min=None, stats=None, diag=1, wsplit=None) -> None:
+                workspace=None, helpers=None, offload_min=None, stats=None, diag=1, wsplit=None,
+                tail_max=None) -> None:
     """pcm_emd_forward; helpers / offload_min / stats select the tuning entry
     (helper workgroups per cloud, the miss count above which an iteration's
-    full scans are offloaded, diagnostics of kind `diag`: 1 counts, 2 phase
-    timers -- csrc/emd.hip pcm_tune_emd_forward_cfg) -- None = the defaults."""
+    full scans are offloaded, diagnostics of kind `diag`: 1 counts, 2 + i phase
+    timers of batch element i; wsplit: waves per few-miss full scan; tail_max:
+    bidders at or below which an iteration runs in tail mode, 0 = never --
+    csrc/emd.hip pcm_tune_emd_forward_cfg) -- None = the defaults."""
     dev = _require_device(xyz1, xyz2, dist, assignment)
     b, n, _ = xyz1.shape
     ws_bytes = emd_workspace_bytes(b, n)
     if ws_bytes and (workspace is None or workspace.numel() * workspace.element_size() < ws_bytes):
         workspace = emd_workspace(dev, b, n)
     with torch.cuda.device(dev):
-        if helpers is None and offload_min is None and stats is None and wsplit is None:
+        if helpers is None and offload_min is None and stats is None and wsplit is None and tail_max is None:
             _check(load_library().pcm_emd_forward(
                 _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
                 _ptr(price), _ptr(workspace), ws_bytes, _stream(dev)), "pcm_emd_forward")
@@ -375,7 +378,7 @@ def emd_forward(xyz1, xyz2, eps: float, iters: int, dist, assignment, price=None
                 _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
                 _ptr(price), _ptr(workspace), ws_bytes, -1 if helpers is None else int(helpers),
                 -1 if offload_min is None else int(offload_min), int(diag), 0 if wsplit is None else int(wsplit),
-                _ptr(stats), _stream(dev)),
+                -1 if tail_max is None else int(tail_max), _ptr(stats), _stream(dev)),
                 "pcm_tune_emd_forward_cfg")
 
 

@@ -81,9 +81,11 @@ def _generator_like(seed, b, n):
     return pred.clamp(0, 1).contiguous(), torch.rand(b, n, 3, generator=g)
 
 
-@pytest.mark.parametrize("helpers,offload_min", [(-1, -1), (0, -1), (3, 0), (31, 0), (15, 4)])
-def test_emd_helper_configs_match_oracle(cuda, oracle, helpers, offload_min):
-    # every helper count / offload threshold gives the same auction
+@pytest.mark.parametrize("helpers,offload_min,tail_max", [(-1, -1, -1), (0, -1, -1), (3, 0, -1), (31, 0, -1),
+                                                          (15, 4, -1), (-1, -1, 0), (-1, -1, 48), (0, -1, 1024)])
+def test_emd_helper_configs_match_oracle(cuda, oracle, helpers, offload_min, tail_max):
+    # every helper count / offload threshold / tail-mode threshold (bidders at
+    # or below which every bid is a cache-less full scan) gives the same auction
     import pcm_hip
     a, c = _generator_like(20, 4, 1024)
     b, n = 4, 1024
@@ -92,7 +94,8 @@ def test_emd_helper_configs_match_oracle(cuda, oracle, helpers, offload_min):
     ass = torch.empty(b, n, dtype=torch.int32, device=cuda)
     price = torch.empty(b, n, device=cuda)
     stats = torch.zeros(3 * 400 + 16 + b, dtype=torch.int32, device=cuda)
-    pcm_hip.emd_forward(x1, x2, 0.05, 400, dist, ass, price, helpers=helpers, offload_min=offload_min, stats=stats)
+    pcm_hip.emd_forward(x1, x2, 0.05, 400, dist, ass, price, helpers=helpers, offload_min=offload_min, stats=stats,
+                        tail_max=tail_max)
     torch.cuda.synchronize()
     rd, ra, rp, _ = oracle.emd_forward(a.numpy(), c.numpy(), 0.05, 400, with_stats=True)
     np.testing.assert_array_equal(ass.cpu().numpy(), ra)

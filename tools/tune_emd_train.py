@@ -15,13 +15,16 @@ sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric
 sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "train"))
 import pcm_hip  # noqa: E402
 
-TIMERS = ["bids", "full-scans", "claim", "assign", "scan/publish", "exchange/own-items", "merge", "finish"]
+TIMERS = ["bids", "full-scans", "claim", "assign", "scan/publish", "exchange/own-items", "merge", "finish",
+          "chain-entry", "chain-scan", "chain-resolve", "chain-assign"]
 
 
-def timed(x1, x2, eps, iters, d, a, helpers, offload, wsplit=None, reps=5):
+def timed(x1, x2, eps, iters, d, a, helpers, offload, wsplit=None, reps=5, tail_max=None):
     kw = {} if helpers is None else {"helpers": helpers, "offload_min": offload}
     if wsplit is not None:
         kw["wsplit"] = wsplit
+    if tail_max is not None:
+        kw["tail_max"] = tail_max
     pcm_hip.emd_forward(x1, x2, eps, iters, d, a, **kw)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
@@ -53,16 +56,20 @@ def run(name, x1, x2, eps, iters, sweep):
     print("  full scans (sum over batch) at iter:", " ".join(f"{i}:{int(per[i, 1])}" for i in marks if i < iters))
     print("  auction wall per batch element (us): min %.1f max %.1f" % (min(wall) / 100.0, max(wall) / 100.0))
     st.zero_()
+    slow = max(range(b), key=lambda i: wall[i])
     st = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=dev)
-    pcm_hip.emd_forward(x1, x2, eps, iters, d, a, stats=st, diag=2)
+    pcm_hip.emd_forward(x1, x2, eps, iters, d, a, stats=st, diag=2 + slow)
     torch.cuda.synchronize()
-    tm = st.cpu()[2 * iters:2 * iters + 13].tolist()
+    tm = st.cpu()[2 * iters:2 * iters + 15].tolist()
     act = max(tm[12], 1)
-    print(f"  batch-0 phase cycles per iteration ({act} iterations): " +
-          ", ".join(f"{nm}={16.0 * v / act:.0f}" for nm, v in zip(TIMERS, tm[:8])))
+    print(f"  slowest batch element {slow}: {act} iterations ({tm[13]} tail mode, {tm[14]} chain mode); "
+          "phase cycles per iteration: " + ", ".join(f"{nm}={16.0 * v / act:.0f}" for nm, v in zip(TIMERS, tm[:12])))
+    print("  phase cycles total (M): " + ", ".join(f"{nm}={16.0 * v / 1e6:.2f}" for nm, v in zip(TIMERS, tm[:12])))
     print(f"  forward (defaults): {timed(x1, x2, eps, iters, d, a, None, None):.1f} us/call")
     for h, o in sweep:
         print(f"  forward helpers={h} offload_min={o}: {timed(x1, x2, eps, iters, d, a, h, o):.1f} us/call")
+    for t in (0, 8, 32, 64, 128):
+        print(f"  forward tail_max={t}: {timed(x1, x2, eps, iters, d, a, -1, -1, tail_max=t):.1f} us/call")
     for w in (2, 4):
         print(f"  forward wsplit={w}: {timed(x1, x2, eps, iters, d, a, -1, -1, w):.1f} us/call")
 

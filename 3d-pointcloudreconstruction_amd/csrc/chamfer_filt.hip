@@ -99,6 +99,56 @@ __device__ __forceinline__ void out_st(Tv *p, Tv v) {
     else *p = v;
 }
 
+// One 4-candidate group against four queries (QPT = 4): the 24 packed FMAs
+// of a(q, t) = fma(qx, ux, fma(qy, uy, fma(qz, uz, w))) for 8 independent
+// (query, candidate pair) chains issued stage by stage, then the min folds.
+// Left to itself hipcc interleaves only two chains in most groups and each
+// FMA waits on its predecessor; the arithmetic here is the same, in the same
+// order.
+__device__ __forceinline__ void filt_group4(float (&mn)[4], const pcm_f2 (&px)[4], const pcm_f2 (&py)[4],
+                                            const pcm_f2 (&pz)[4], pcm_f4 X4, pcm_f4 Y4, pcm_f4 Z4, pcm_f4 W4) {
+    const pcm_f2 xa = X4.xy, xb = X4.zw, ya = Y4.xy, yb = Y4.zw, za = Z4.xy, zb = Z4.zw, wa = W4.xy, wb = W4.zw;
+    pcm_f2 a0, a1, a2, a3, b0, b1, b2, b3;
+    asm("v_pk_fma_f32 %[a0], %[z0], %[za], %[wa]\n\t"
+        "v_pk_fma_f32 %[b0], %[z0], %[zb], %[wb]\n\t"
+        "v_pk_fma_f32 %[a1], %[z1], %[za], %[wa]\n\t"
+        "v_pk_fma_f32 %[b1], %[z1], %[zb], %[wb]\n\t"
+        "v_pk_fma_f32 %[a2], %[z2], %[za], %[wa]\n\t"
+        "v_pk_fma_f32 %[b2], %[z2], %[zb], %[wb]\n\t"
+        "v_pk_fma_f32 %[a3], %[z3], %[za], %[wa]\n\t"
+        "v_pk_fma_f32 %[b3], %[z3], %[zb], %[wb]\n\t"
+        "v_pk_fma_f32 %[a0], %[y0], %[ya], %[a0]\n\t"
+        "v_pk_fma_f32 %[b0], %[y0], %[yb], %[b0]\n\t"
+        "v_pk_fma_f32 %[a1], %[y1], %[ya], %[a1]\n\t"
+        "v_pk_fma_f32 %[b1], %[y1], %[yb], %[b1]\n\t"
+        "v_pk_fma_f32 %[a2], %[y2], %[ya], %[a2]\n\t"
+        "v_pk_fma_f32 %[b2], %[y2], %[yb], %[b2]\n\t"
+        "v_pk_fma_f32 %[a3], %[y3], %[ya], %[a3]\n\t"
+        "v_pk_fma_f32 %[b3], %[y3], %[yb], %[b3]\n\t"
+        "v_pk_fma_f32 %[a0], %[x0], %[xa], %[a0]\n\t"
+        "v_pk_fma_f32 %[b0], %[x0], %[xb], %[b0]\n\t"
+        "v_pk_fma_f32 %[a1], %[x1], %[xa], %[a1]\n\t"
+        "v_pk_fma_f32 %[b1], %[x1], %[xb], %[b1]\n\t"
+        "v_pk_fma_f32 %[a2], %[x2], %[xa], %[a2]\n\t"
+        "v_pk_fma_f32 %[b2], %[x2], %[xb], %[b2]\n\t"
+        "v_pk_fma_f32 %[a3], %[x3], %[xa], %[a3]\n\t"
+        "v_pk_fma_f32 %[b3], %[x3], %[xb], %[b3]"
+        : [a0] "=&v"(a0), [a1] "=&v"(a1), [a2] "=&v"(a2), [a3] "=&v"(a3), [b0] "=&v"(b0), [b1] "=&v"(b1),
+          [b2] "=&v"(b2), [b3] "=&v"(b3)
+        : [x0] "v"(px[0]), [x1] "v"(px[1]), [x2] "v"(px[2]), [x3] "v"(px[3]), [y0] "v"(py[0]), [y1] "v"(py[1]),
+          [y2] "v"(py[2]), [y3] "v"(py[3]), [z0] "v"(pz[0]), [z1] "v"(pz[1]), [z2] "v"(pz[2]), [z3] "v"(pz[3]),
+          [xa] "v"(xa), [xb] "v"(xb), [ya] "v"(ya), [yb] "v"(yb), [za] "v"(za), [zb] "v"(zb), [wa] "v"(wa),
+          [wb] "v"(wb));
+    mn[0] = __builtin_fminf(__builtin_fminf(mn[0], a0.x), a0.y);
+    mn[1] = __builtin_fminf(__builtin_fminf(mn[1], a1.x), a1.y);
+    mn[2] = __builtin_fminf(__builtin_fminf(mn[2], a2.x), a2.y);
+    mn[3] = __builtin_fminf(__builtin_fminf(mn[3], a3.x), a3.y);
+    mn[0] = __builtin_fminf(__builtin_fminf(mn[0], b0.x), b0.y);
+    mn[1] = __builtin_fminf(__builtin_fminf(mn[1], b1.x), b1.y);
+    mn[2] = __builtin_fminf(__builtin_fminf(mn[2], b2.x), b2.y);
+    mn[3] = __builtin_fminf(__builtin_fminf(mn[3], b3.x), b3.y);
+}
+
 // One workgroup's share of the forward: queries [qbase, qbase + 64 QPT) of
 // cloud Q (nq points) against the nt points of T.  Writes D[q], I[q]; returns
 // the distance of query slot threadIdx.x (0 past nq and for threads >= 64 QPT),
@@ -271,6 +321,10 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                 // the next group's four reads stay ahead of this group's math
                 // (hipcc otherwise sinks them to their use and waits on each)
                 __builtin_amdgcn_sched_barrier(0);
+                if constexpr (QPT == 4) {
+                    filt_group4(mn, px, py, pz, X4, Y4, Z4, W4);
+                    continue;
+                }
 #pragma unroll
                 for (int qq = 0; qq < QPT; ++qq) {
                     const pcm_f2 a01 = __builtin_elementwise_fma(
@@ -958,21 +1012,28 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         for (int w = 0; w < W; ++w) t += sRed[w];
         __hip_atomic_store(ws.wpart + bid, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    // the batch element's clouds for the gradient phase (L2-hot; the forward
-    // is done with the arena); they land during the arrival round trip
-    pcm_dma_to_lds(arena, X1, 12 * n, wave, W);
-    pcm_dma_to_lds(arena + 12 * kGradCap, X2, 12 * m, wave, W);
-    // every storing wave drains its sc1 stores (and the LDS-DMA lands)
+    // every storing wave drains its sc1 stores
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     // ---- arrive, then wait (bounded) until every workgroup of this batch
     // element has arrived: all argmins are then published.  The grid (b *
     // per + 1 workgroups of 64 W threads) is sized to be co-resident; a wait
     // that times out sets the sticky error word and yields NaN gradients.
+    // The batch element's clouds for the gradient phase (L2-hot; the forward
+    // is done with the arena) are fetched into LDS during the wait: issued
+    // after the arrival (wave 0: after its add returned), so no arrival
+    // waits for them.
+    unsigned old_arrivals = 0;
+    if (tid == 0) {
+        old_arrivals = __hip_atomic_fetch_add(ws.bcount + (size_t)batch * kCtrStride, 1u, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+    }
+    pcm_dma_to_lds(arena, X1, 12 * n, wave, W);
+    pcm_dma_to_lds(arena + 12 * kGradCap, X2, 12 * m, wave, W);
     if (tid == 0) {
         unsigned *ctr = ws.bcount + (size_t)batch * kCtrStride;
         unsigned *dep_ctr = ws.bdepart + (size_t)batch * kCtrStride;
-        const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned old = old_arrivals;
         sFlag = (old == (unsigned)per - 1);
         int late = 0;
         if (old != (unsigned)per - 1) {
@@ -991,6 +1052,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
             __hip_atomic_store(dep_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the LDS-DMA has landed
     __syncthreads();
     PCM_STAMP2(2);
 
@@ -1067,6 +1129,9 @@ const GradVariant kGradVariants[] = {
     {chamfer_loss_grad_kernel<8, 2, 16, 1024>, 8, 2},  // 0
     {chamfer_loss_grad_kernel<8, 4, 16, 1024>, 8, 4},  // 1
     {chamfer_loss_grad_kernel<4, 2, 16, 1024>, 4, 2},  // 2
+    {chamfer_loss_grad_kernel<16, 4, 16, 1024>, 16, 4},  // 3
+    {chamfer_loss_grad_kernel<8, 4, 32, 1024>, 8, 4},  // 4
+    {chamfer_loss_grad_kernel<16, 4, 32, 1024>, 16, 4},  // 5
 };
 constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
 // tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,

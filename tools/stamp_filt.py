@@ -94,9 +94,30 @@ def run_fused(v, b, n, m, dev):
     print(f"  starts: {(max(r[0] for r in rows) - t0) * TICK_US:.2f} us spread; waits end "
           f"{(min(r[2] for r in rows) - t0) * TICK_US:.2f} .. {(max(r[2] for r in rows) - t0) * TICK_US:.2f} us")
     print(f"  poller: starts {(poll[5] - t0) * TICK_US:.2f} us, done {(poll[6] - t0) * TICK_US:.2f} us")
+    # per batch element: its last forward -> its waits' end (arrival
+    # propagation), using the kernel's workgroup -> (batch element) mapping
+    g = nblk - 1
+    per_el = (n + qw - 1) // qw + (m + qw - 1) // qw
+    pr, rem = g // 8, g % 8
+    el = {}
+    for i, r in enumerate(rows):
+        x, s_ = i % 8, i // 8
+        bid = (x * (pr + 1) if x < rem else rem * (pr + 1) + (x - rem) * pr) + s_
+        el.setdefault(bid // per_el, []).append(r)
+    lags = sorted(((max(r[2] for r in rs) - max(r[1] for r in rs)) * TICK_US, k) for k, rs in el.items())
+    spread = [((max(r[2] for r in rs) - min(r[2] for r in rs)) * TICK_US) for rs in el.values()]
+    print(f"  per element: last forward -> last wait end median {statistics.median([l for l, _ in lags]):.2f} us, "
+          f"max {lags[-1][0]:.2f} us (element {lags[-1][1]}); wait-end spread inside an element median "
+          f"{statistics.median(spread):.2f} max {max(spread):.2f} us")
+    # the forward's own stamps (table's lower half, same workgroup numbering)
+    lo = [[buf[i * 8 + k] for k in range(8)] for i in range(nblk - 1)]
+    for nm, k0, k1 in [("centre", 0, 1), ("stage", 1, 2), ("scan", 2, 3), ("proof", 3, 4), ("rescan", 4, 5),
+                       ("ties", 5, 6)]:
+        dur = [(r[k1] - r[k0]) * TICK_US for r in lo]
+        print(f"  fwd {nm:7s} median {statistics.median(dur):7.2f} us  max {max(dur):7.2f}")
 
 
-FUSED_QPT = [2, 4, 2]                       # csrc/chamfer_filt.hip kGradVariants
+FUSED_QPT = [2, 4, 2, 4, 4, 4]              # csrc/chamfer_filt.hip kGradVariants
 
 
 def main():

@@ -105,7 +105,14 @@ def main():
                                      pcm_hip.chamfer_backward(x1, x2, g1, g2, i1, i2, gx1, gx2)), reps)
             tsep = statistics.median([time_graph_us(gsep, reps) for _ in range(rounds)])
             print(f"  step as two launches (fused-loss fwd + bwd): {tsep:9.2f} us")
+            pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo3, gx1, gx2, ws)
+            torch.cuda.synchronize()
+            gref = [t.clone() for t in (d1, d2, i1, i2, gx1, gx2, mo3)]
             for v in range(pcm_hip.tune_num_chamfer_loss_grad_variants()):
+                pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo3, gx1, gx2, ws, variant=v)
+                torch.cuda.synchronize()
+                same = all(torch.equal(a, r) for a, r in zip((d1, d2, i1, i2, gx1, gx2, mo3), gref))
+                print(f"  loss+grad fused variant {v}: bit-identical to the default: {same}")
                 gv = graph_of(lambda v=v: pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo3, gx1, gx2,
                                                                     ws, variant=v), reps)
                 tv = statistics.median([time_graph_us(gv, reps) for _ in range(rounds)])

@@ -616,6 +616,426 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
 }
 
 // ---------------------------------------------------------------------------
+// Filtered forward on the matrix cores (single-tile clouds, nt <= 1024; 8
+// waves, 256 queries).  Same contract and results as filt_forward.
+//
+// The screen value a(q, t) = w + u.q' (u = -2t', w = |t'|^2 as filt_forward
+// computes them) is evaluated by v_mfma_f32_16x16x32_bf16 on a three-way
+// bf16 split of every operand: v = vh + vm + vl + e, |e| <= 2^-24 |v| (each
+// part the round-to-nearest bf16 of the remainder, remainders exact in fp32).
+// Per dimension the K axis carries uh.qh, uh.qm, um.qh, uh.ql, ul.qh, um.qm
+// (dropped: um.ql, ul.qm, ul.ql, each <= 2^-24 |u_d q_d|), then wh, wm, wl
+// against 1: 21 of the 32 K slots, products exact in fp32.  Error of the
+// screened value against the real w + u.q':
+//   split and dropped terms   <= 4.01 u |u||q| + u w <= 4.01 u (R + |q'|)^2
+//   20 fp32 additions, any order, rounding or truncating (2u each)
+//                              <= 40 u * 1.02 (w + |u||q|) <= 41 u (R + |q'|)^2
+// plus filt_forward's own terms (w 2u, centring 2u, the exact formula 5u,
+// slack): 59 u; the proof uses E = 80 u (R + |q'|)^2 (kFiltU80) and an
+// absolute 2^-100 for subnormal parts.
+//
+// MFMA roles: A = 16 targets x 32 K (rows), B = 32 K x 16 queries (columns),
+// so lane l receives D[targets 4(l>>4)..+3][query l&15] -- four candidates of
+// ONE query, folded with two v_min3 and no cross-lane work.  Wave (quarter,
+// half): queries of half h (8 tiles of 16), target groups of 64 (4 tiles)
+// g = quarter, quarter + 4, ...  A chunk (the unit of the proof) is one
+// target group seen by one lane group: targets 64 g + 16 i + 4 (l>>4) + r,
+// i, r in 0..3 -- 16 candidates, rescanned in ascending order.
+// ---------------------------------------------------------------------------
+constexpr float kFiltU80 = 4.76837158203125e-06f;  // 80 u = 80 * 2^-24
+constexpr int kMfmaQW = 256, kMfmaNT = 512, kMfmaTile = 1024;
+struct MfmaLds {
+    static constexpr int kA = kMfmaTile * 64;                    // target rows, 32 bf16 each
+    static constexpr int kQB = kMfmaQW * 64;                     // query rows, 32 bf16 each
+    static constexpr int kScan = kA + kQB;
+    static constexpr int kTail = 3 * kMfmaTile * 4 + 3 * 4 * kMfmaQW * 4;  // raw tile + 4 partials
+    static constexpr int kBytes = kScan > kTail ? kScan : kTail;
+};
+typedef __bf16 pcm_bf16x8 __attribute__((ext_vector_type(8)));
+
+typedef __bf16 pcm_bf16x2 __attribute__((ext_vector_type(2)));
+// (a, b) -> one dword of two round-to-nearest-even bf16 (v_cvt_pk_bf16_f32): a low, b high
+__device__ __forceinline__ unsigned cvt_bf16x2(float a, float b) {
+    return __builtin_bit_cast(unsigned, __builtin_convertvector((pcm_f2){a, b}, pcm_bf16x2));
+}
+__device__ __forceinline__ float bf_lo(unsigned v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float bf_hi(unsigned v) { return __uint_as_float(v & 0xffff0000u); }
+// dword from the 16-bit halves: low half of `lo` word (hl = 0) or its high half (hl = 1), etc.
+template <int HL, int HH>
+__device__ __forceinline__ unsigned bf_pair(unsigned lo, unsigned hi) {
+    constexpr unsigned sel = (HL ? 0x0302u : 0x0100u) | ((HH ? 0x0706u : 0x0504u) << 16);
+    return __builtin_amdgcn_perm(hi, lo, sel);
+}
+// Three-way bf16 split of (a, b): a = lo16 parts of H, M, L; b = the high parts.
+// Each level is the RNE bf16 of the remainder of the levels above; every
+// remainder is exact in fp32.
+__device__ __forceinline__ void split3x2(float a, float b, unsigned &H, unsigned &M, unsigned &L) {
+    H = cvt_bf16x2(a, b);
+    const float ra = a - bf_lo(H), rb = b - bf_hi(H);
+    M = cvt_bf16x2(ra, rb);
+    L = cvt_bf16x2(ra - bf_lo(M), rb - bf_hi(M));
+}
+// 64-target groups of the raw tile rotated by 4 (group mod 8): the rescan's
+// lanes -- one query each, chunks of stride-16 quads -- spread over the banks
+__device__ __forceinline__ int mslot(int p) { return (p & ~63) | ((p + 4 * ((p >> 6) & 7)) & 63); }
+
+template <bool kSc1>
+__device__ __forceinline__ float filt_forward_mfma(const float *__restrict__ Q, const float *__restrict__ T, int nq,
+                                                   int nt, int qbase, float *__restrict__ D, int32_t *__restrict__ I,
+                                                   unsigned char *arena) {
+    constexpr int QW = kMfmaQW, NT = kMfmaNT, W = NT / 64, TILE = kMfmaTile;
+    constexpr int kPer = TILE / NT;  // staged targets per thread
+    uint4 *sA = reinterpret_cast<uint4 *>(arena);                      // [TILE][4] x 16 B
+    uint4 *sQB = reinterpret_cast<uint4 *>(arena + MfmaLds::kA);        // [QW][4]
+    float(*sT)[TILE] = reinterpret_cast<float(*)[TILE]>(arena);         // raw x, y, z (after the scan)
+    float(*sPB)[QW] = reinterpret_cast<float(*)[QW]>(arena + 3 * TILE * 4);
+    float(*sPS)[QW] = reinterpret_cast<float(*)[QW]>(arena + 3 * TILE * 4 + 4 * QW * 4);
+    int(*sPC)[QW] = reinterpret_cast<int(*)[QW]>(arena + 3 * TILE * 4 + 8 * QW * 4);
+    __shared__ float sQx[QW], sQy[QW], sQz[QW];  // raw queries
+    __shared__ float sD[QW];
+    __shared__ int sK[QW];
+    __shared__ int sFc[QW];
+    __shared__ float sHD[2][QW];
+    __shared__ int sHK[2][QW];
+    __shared__ float sRmax[W];
+    __shared__ float sCen[4];
+    __shared__ int sList[QW];
+    __shared__ int sNList;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+
+    // ---- raw queries (thread s < QW owns query slot s) and the first tile
+    float qx = 0.f, qy = 0.f, qz = 0.f;
+    bool nonfinite = false;
+    if (tid < QW) {
+        const int qc = min(qbase + tid, nq - 1);
+        qx = pcm_ld(Q + 3 * (size_t)qc + 0);
+        qy = pcm_ld(Q + 3 * (size_t)qc + 1);
+        qz = pcm_ld(Q + 3 * (size_t)qc + 2);
+    }
+    float tv[kPer][3];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+        const int p = min(tid + r * NT, nt - 1);
+#pragma unroll
+        for (int d = 0; d < 3; ++d) tv[r][d] = pcm_ld(T + 3 * (size_t)p + d);
+    }
+    {
+        const bool live = tid < QW && qbase + tid < nq;
+        if (live) nonfinite |= !(pcm_finite(qx) && pcm_finite(qy) && pcm_finite(qz));
+        float cx = live ? qx : 0.f, cy = live ? qy : 0.f, cz = live ? qz : 0.f, cn = live ? 1.f : 0.f;
+        if (wave < QW / 64) {
+            cx = wave_sum(cx);
+            cy = wave_sum(cy);
+            cz = wave_sum(cz);
+            cn = wave_sum(cn);
+            if (lane == 0) { sRmax[wave] = cx; sHD[0][wave] = cy; sHD[1][wave] = cz; sD[wave] = cn; }
+        }
+        if (tid < QW) { sQx[tid] = qx; sQy[tid] = qy; sQz[tid] = qz; }
+        if (tid == 0) sNList = 0;
+        __syncthreads();
+        if (tid == 0) {  // fixed order over the query waves
+            float sx = 0.f, sy = 0.f, sz = 0.f, sn = 0.f;
+            for (int w = 0; w < QW / 64; ++w) { sx += sRmax[w]; sy += sHD[0][w]; sz += sHD[1][w]; sn += sD[w]; }
+            sCen[0] = sx / sn;
+            sCen[1] = sy / sn;
+            sCen[2] = sz / sn;
+        }
+        __syncthreads();
+    }
+    PCM_STAMP(1);
+#ifdef PCM_STAMPS
+    if (tid == 0 && blockIdx.x < 4096)  // shader-clock cycles beside the 100 MHz stamps (clock estimate)
+        g_pcm_stamps[(8192 + blockIdx.x) * 8 + 1] = __builtin_amdgcn_s_memtime();
+#endif
+    const float c0 = sCen[0], c1 = sCen[1], c2 = sCen[2];
+
+    // ---- rows: queries (thread s < QW) and targets (kPer per thread), 16 dwords each
+    if (tid < QW) {
+        unsigned H01, M01, L01, H2, M2, L2;
+        split3x2(qx - c0, qy - c1, H01, M01, L01);
+        split3x2(qz - c2, 0.f, H2, M2, L2);
+        // K 6d..6d+5: qh, qm, qh, ql, qh, qm; K 18..20: 1
+        const unsigned one2 = 0x3f803f80u, one0 = 0x00003f80u;
+        sQB[4 * tid + 0] = make_uint4(bf_pair<0, 0>(H01, M01), bf_pair<0, 0>(H01, L01), bf_pair<0, 0>(H01, M01),
+                                      bf_pair<1, 1>(H01, M01));
+        sQB[4 * tid + 1] = make_uint4(bf_pair<1, 1>(H01, L01), bf_pair<1, 1>(H01, M01), bf_pair<0, 0>(H2, M2),
+                                      bf_pair<0, 0>(H2, L2));
+        sQB[4 * tid + 2] = make_uint4(bf_pair<0, 0>(H2, M2), one2, one0, 0u);
+        sQB[4 * tid + 3] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    const int ntp = (nt + 63) & ~63;  // whole 64-target groups; pad rows screen as +inf
+    float rt2 = 0.f;
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+        const int p = tid + r * NT;
+        if (p < ntp) {
+            uint4 r0 = make_uint4(0u, 0u, 0u, 0u), r1 = r0, r2 = make_uint4(0u, 0x00007f80u, 0u, 0u);  // pad: K 18 (wh) = +inf
+            if (p < nt) {
+                nonfinite |= !(pcm_finite(tv[r][0]) && pcm_finite(tv[r][1]) && pcm_finite(tv[r][2]));
+                const float x = tv[r][0] - c0, y = tv[r][1] - c1, z = tv[r][2] - c2;
+                const float w = __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
+                rt2 = __builtin_fmaxf(rt2, w);
+                unsigned H01, M01, L01, H23, M23, L23;
+                split3x2(-2.f * x, -2.f * y, H01, M01, L01);
+                split3x2(-2.f * z, w, H23, M23, L23);
+                // K 6d..6d+5: uh, uh, um, uh, ul, um; K 18..20: wh, wm, wl
+                r0 = make_uint4(bf_pair<0, 0>(H01, H01), bf_pair<0, 0>(M01, H01), bf_pair<0, 0>(L01, M01),
+                                bf_pair<1, 1>(H01, H01));
+                r1 = make_uint4(bf_pair<1, 1>(M01, H01), bf_pair<1, 1>(L01, M01), bf_pair<0, 0>(H23, H23),
+                                bf_pair<0, 0>(M23, H23));
+                r2 = make_uint4(bf_pair<0, 0>(L23, M23), bf_pair<1, 1>(H23, M23), L23 >> 16, 0u);
+            }
+            sA[4 * p + 0] = r0;
+            sA[4 * p + 1] = r1;
+            sA[4 * p + 2] = r2;
+            sA[4 * p + 3] = make_uint4(0u, 0u, 0u, 0u);
+        }
+    }
+    {
+        float v = rt2;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v = __builtin_fmaxf(v, __shfl_xor(v, o, 64));
+        if (lane == 0) sRmax[wave] = v;
+    }
+    __syncthreads();
+    PCM_STAMP(2);
+
+    // ---- screen: wave (quarter, half); lane group g = lane >> 4 holds K slice 8g..8g+7
+    const int quarter = wave >> 1, half = wave & 1;
+    const int g = lane >> 4, col = lane & 15;
+    constexpr int QT = QW / 2 / 16;  // query tiles per wave
+    pcm_bf16x8 bq[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+        const uint4 v = sQB[4 * (half * (QW / 2) + qt * 16 + col) + g];
+        bq[qt] = __builtin_bit_cast(pcm_bf16x8, v);
+    }
+    float best[QT], sec[QT];
+    int bchunk[QT];
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) { best[qt] = PCM_INF; sec[qt] = PCM_INF; bchunk[qt] = 0; }
+    const int ngroups = ntp >> 6;
+    for (int gi = quarter; gi < ngroups; gi += 4) {
+        float mn[QT];
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) mn[qt] = PCM_INF;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint4 av = sA[4 * (64 * gi + 16 * i + col) + g];
+            const pcm_bf16x8 a = __builtin_bit_cast(pcm_bf16x8, av);
+#pragma unroll
+            for (int qt = 0; qt < QT; ++qt) {
+                const pcm_f4 d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bq[qt], pcm_f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                mn[qt] = __builtin_fminf(__builtin_fminf(mn[qt], d.x), d.y);
+                mn[qt] = __builtin_fminf(__builtin_fminf(mn[qt], d.z), d.w);
+            }
+        }
+        const int cid = 4 * gi + g;
+#pragma unroll
+        for (int qt = 0; qt < QT; ++qt) {
+            sec[qt] = __builtin_amdgcn_fmed3f(mn[qt], best[qt], sec[qt]);
+            if (mn[qt] < best[qt]) { best[qt] = mn[qt]; bchunk[qt] = cid; }
+        }
+    }
+    __syncthreads();  // every wave is done reading sA / sQB
+    PCM_STAMP(3);
+    // raw tile for the rescans (this thread's staged targets), partials
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+        const int p = tid + r * NT;
+        if (p < nt) { sT[0][mslot(p)] = tv[r][0]; sT[1][mslot(p)] = tv[r][1]; sT[2][mslot(p)] = tv[r][2]; }
+    }
+    // the four lane groups of a wave hold the same queries: fold them (xor 16,
+    // xor 32) so one partial per (quarter, query) goes to LDS
+#pragma unroll
+    for (int qt = 0; qt < QT; ++qt) {
+#pragma unroll
+        for (int o = 16; o <= 32; o <<= 1) {
+            const float vb = __shfl_xor(best[qt], o, 64), vs = __shfl_xor(sec[qt], o, 64);
+            const int vc = __shfl_xor(bchunk[qt], o, 64);
+            const bool better = (vb < best[qt]) | ((vb == best[qt]) & (vc < bchunk[qt]));
+            sec[qt] = __builtin_fminf(__builtin_fminf(sec[qt], vs), better ? best[qt] : vb);
+            best[qt] = better ? vb : best[qt];
+            bchunk[qt] = better ? vc : bchunk[qt];
+        }
+        if (g == 0) {
+            const int s = half * (QW / 2) + qt * 16 + col;
+            sPB[quarter][s] = best[qt];
+            sPS[quarter][s] = sec[qt];
+            sPC[quarter][s] = bchunk[qt];
+        }
+    }
+    const int any_nonfinite = __syncthreads_or(nonfinite ? 1 : 0);
+
+    float my_d = 0.f;
+    if (!any_nonfinite) {
+        // ---- merge the 16 partials; proof
+        if (tid < QW) {
+            float fb = sPB[0][tid], fs = sPS[0][tid];
+            int fc = sPC[0][tid];
+#pragma unroll
+            for (int p = 1; p < 4; ++p) {
+                const float vb = sPB[p][tid], vs = sPS[p][tid];
+                const int vc = sPC[p][tid];
+                const bool better = (vb < fb) | ((vb == fb) & (vc < fc));
+                fs = __builtin_fminf(__builtin_fminf(fs, vs), better ? fb : vb);
+                fb = better ? vb : fb;
+                fc = better ? vc : fc;
+            }
+            float rmax2 = sRmax[0];
+#pragma unroll
+            for (int w = 1; w < W; ++w) rmax2 = __builtin_fmaxf(rmax2, sRmax[w]);
+            const float x = qx - c0, y = qy - c1, z = qz - c2;
+            const float qn2 = __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
+            const float rr = __builtin_sqrtf(rmax2) + __builtin_sqrtf(qn2);
+            const float e2 = 2.f * (kFiltU80 * (rr * rr) * 1.001f + 7.888609052210118e-31f);  // + 2^-100
+            if ((fs - fb) > e2) {  // false for NaN
+                sFc[tid] = fc;
+            } else {
+                // near-tie plan, -1 - bits: quarter q is scanned whole (bit q)
+                // when its second-best chunk may lie within fb + 2E, else its
+                // best chunk alone (bit 4 + q) when that one may; every other
+                // candidate screens above fb + 2E, so lies above the answer.
+                // NaN anywhere selects the scan.
+                const float thr = fb + e2;
+                int plan = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (!(sPS[q][tid] > thr)) plan |= 1 << q;
+                    else if (!(sPB[q][tid] > thr)) plan |= 16 << q;
+                }
+                sFc[tid] = -1 - plan;
+            }
+        }
+        __syncthreads();
+        PCM_STAMP(4);
+        // ---- exact rescan of the proven chunk: thread = (query slot s, part):
+        // part p takes tiles 2p, 2p + 1 of the group, rows 4g..4g+3 (ascending)
+        {
+            const int s = tid % QW, part = tid / QW;
+            const int fc = sFc[s];
+            float hd = PCM_INF;
+            int hk = 0x7fffffff;
+            if (qbase + s < nq && fc >= 0) {
+                const float x = sQx[s], y = sQy[s], z = sQz[s];
+                const int k0 = 64 * (fc >> 2) + 32 * part + 4 * (fc & 3);
+                float tx[8], ty[8], tz[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int kk = mslot(min(k0 + 16 * (k >> 2) + (k & 3), nt - 1));
+                    tx[k] = sT[0][kk];
+                    ty[k] = sT[1][kk];
+                    tz[k] = sT[2][kk];
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int kk = k0 + 16 * (k >> 2) + (k & 3);
+                    const float d = pcm_sqd(tx[k] - x, ty[k] - y, tz[k] - z);
+                    const bool take = (d < hd) & (kk < nt);
+                    hd = take ? d : hd;
+                    hk = take ? kk : hk;
+                }
+            }
+            sHD[part][s] = hd;
+            sHK[part][s] = hk;
+        }
+        __syncthreads();
+        if (tid < QW && qbase + tid < nq) {
+            if (sFc[tid] >= 0) {
+                float d = sHD[0][tid];
+                int k = sHK[0][tid];
+                pcm_lexmin(d, k, sHD[1][tid], sHK[1][tid]);
+                sD[tid] = d;
+                sK[tid] = k;
+            } else {
+                sList[atomicAdd(&sNList, 1)] = tid;
+            }
+        }
+        __syncthreads();
+        PCM_STAMP(5);
+        // ---- near-ties: one wave per query, exact scan of the plan's
+        // candidates (64-target groups of whole quarters, single chunks)
+        const int nl = sNList;
+#ifdef PCM_STAMPS
+        if (tid == 0 && blockIdx.x < kStampSlots) {  // diagnostics: ties, whole quarters, single chunks
+            unsigned long long full = 0, single = 0;
+            for (int e = 0; e < nl; ++e) {
+                const int pl = -1 - sFc[sList[e]];
+                full += __popc(pl & 15);
+                single += __popc((pl >> 4) & 15);
+            }
+            g_pcm_stamps[blockIdx.x * 8 + 0] = (unsigned long long)nl | (full << 16) | (single << 40);
+        }
+#endif
+        for (int e = wave; e < nl; e += W) {
+            const int s = sList[e];
+            const int plan = -1 - sFc[s];
+            const float x = sQx[s], y = sQy[s], z = sQz[s];
+            float bd = PCM_INF;
+            int bk = 0x7fffffff;
+            for (int gi0 = 0; gi0 < ngroups; gi0 += 4) {  // 4 groups in flight, one candidate each per lane
+                float tx[4], ty[4], tz[4];
+                int kk[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int gi = gi0 + u, q = u;  // gi % 4 == u
+                    int k = -1;
+                    if (gi < ngroups) {
+                        if (plan & (1 << q)) {
+                            k = 64 * gi + lane;
+                        } else if ((plan & (16 << q)) && lane < 16) {
+                            const int pc = sPC[q][s];
+                            if ((pc >> 2) == gi) k = 64 * gi + 16 * (lane >> 2) + 4 * (pc & 3) + (lane & 3);
+                        }
+                    }
+                    kk[u] = (k >= 0 && k < nt) ? k : -1;
+                    const int ks = mslot(max(kk[u], 0));
+                    tx[u] = sT[0][ks];
+                    ty[u] = sT[1][ks];
+                    tz[u] = sT[2][ks];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const float d = pcm_sqd(tx[u] - x, ty[u] - y, tz[u] - z);
+                    if (kk[u] >= 0) pcm_lexmin(bd, bk, d, kk[u]);
+                }
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) pcm_lexmin(bd, bk, __shfl_xor(bd, o, 64), __shfl_xor(bk, o, 64));
+            if (lane == 0) {
+                sD[s] = bd;
+                sK[s] = bk;
+            }
+        }
+        if (nl > 0) __syncthreads();
+        PCM_STAMP(6);
+#ifdef PCM_STAMPS
+        if (tid == 0 && blockIdx.x < 4096) g_pcm_stamps[(8192 + blockIdx.x) * 8 + 6] = __builtin_amdgcn_s_memtime();
+#endif
+        if (tid < QW && qbase + tid < nq) {
+            my_d = sD[tid];
+            out_st<kSc1>(D + qbase + tid, my_d);
+            out_st<kSc1>(I + qbase + tid, (int32_t)sK[tid]);
+        }
+    } else {
+        for (int s = tid; s < QW; s += NT) {
+            const int qi = qbase + s;
+            if (qi >= nq) continue;
+            float d;
+            int idx;
+            pcm_ref_nn_scan(pcm_ld(Q + 3 * (size_t)qi + 0), pcm_ld(Q + 3 * (size_t)qi + 1),
+                            pcm_ld(Q + 3 * (size_t)qi + 2), T, nt, d, idx);
+            my_d = d;
+            out_st<kSc1>(D + qi, d);
+            out_st<kSc1>(I + qi, (int32_t)idx);
+        }
+    }
+    return my_d;
+}
+
+// ---------------------------------------------------------------------------
 // Forward kernel: direction-major workgroup numbering (as the other forward
 // forms), optional loss granule (mode 3, chamfer_loss.h).
 // ---------------------------------------------------------------------------
@@ -962,7 +1382,7 @@ __device__ __forceinline__ void poll_grad_loss(int b, int n, int m, const GradWs
     }
 }
 
-template <int W, int QPT, int C, int TILE>
+template <int W, int QPT, int C, int TILE, bool kMfma = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -970,7 +1390,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     GradWs ws, unsigned max_spins) {
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
-    constexpr int kFwd = FiltLds<W, QPT, TILE>::kBytes;
+    static_assert(!kMfma || (W == 8 && QPT == 4 && TILE == kMfmaTile), "the MFMA forward's fixed geometry");
+    constexpr int kFwd = kMfma ? MfmaLds::kBytes : FiltLds<W, QPT, TILE>::kBytes;
     constexpr int kArena = kFwd > kGradBytes ? kFwd : kGradBytes;
     static_assert(QW <= NT, "one target per thread in the gradient phase");
     __shared__ float sRed[16];
@@ -997,10 +1418,16 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int q0 = (first ? r : r - nblk1) * QW;
     const float *X1 = xyz1 + (size_t)batch * n * 3;
     const float *X2 = xyz2 + (size_t)batch * m * 3;
-    const float my_d = filt_forward<float, W, QPT, C, TILE, true>(
-        first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
-        first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
-        first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena);
+    float my_d;
+    if constexpr (kMfma)
+        my_d = filt_forward_mfma<true>(first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
+                                       first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
+                                       first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena);
+    else
+        my_d = filt_forward<float, W, QPT, C, TILE, true>(
+            first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
+            first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
+            first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena);
     PCM_STAMP2(1);
 
     // ---- workgroup partial (fixed order), write-through; drain; arrive
@@ -1132,6 +1559,7 @@ const GradVariant kGradVariants[] = {
     {chamfer_loss_grad_kernel<16, 4, 16, 1024>, 16, 4},  // 3
     {chamfer_loss_grad_kernel<8, 4, 32, 1024>, 8, 4},  // 4
     {chamfer_loss_grad_kernel<16, 4, 32, 1024>, 16, 4},  // 5
+    {chamfer_loss_grad_kernel<8, 4, 16, 1024, true>, 8, 4},  // 6: screen on the matrix cores
 };
 constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
 // tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,

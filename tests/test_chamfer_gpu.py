@@ -477,17 +477,21 @@ def test_loss_grad_matches_oracle(cuda, oracle, b, n, m, seed, dist):
         assert means[0][2] == np.float32(means[0][0] + means[0][1])
 
 
-@pytest.mark.parametrize("kind", ["grid", "near_ties", "dup_queries", "offset"])
+@pytest.mark.parametrize("kind", ["grid", "near_ties", "dup_queries", "offset", "tiny", "huge"])
 def test_loss_grad_stress(cuda, oracle, kind):
+    # every fused variant, the matrix-core screen (bf16 split, wider bound,
+    # targeted near-tie rescans) included, on clouds built to defeat the filter
+    import pcm_hip
     a, c = _stress_clouds(kind, b=3, n=1000, m=900)
     b, n, m = a.shape[0], a.shape[1], c.shape[1]
     ref = oracle.chamfer_forward(a.numpy(), c.numpy())
-    o, _, (w1, w2) = _loss_grad(cuda, a, c)
-    _assert_fwd_equal((o["d1"], o["d2"], o["i1"], o["i2"]), ref)
-    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), w1, np.float32),
-                                       np.full((b, m), w2, np.float32), ref[2], ref[3])
-    np.testing.assert_array_equal(o["g1"].view(np.int32), gr1.view(np.int32))
-    np.testing.assert_array_equal(o["g2"].view(np.int32), gr2.view(np.int32))
+    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), np.float32(1.0 / (b * n)), np.float32),
+                                       np.full((b, m), np.float32(1.0 / (b * m)), np.float32), ref[2], ref[3])
+    for v in range(pcm_hip.tune_num_chamfer_loss_grad_variants()):
+        o, _, (w1, w2) = _loss_grad(cuda, a, c, variant=v)
+        _assert_fwd_equal((o["d1"], o["d2"], o["i1"], o["i2"]), ref)
+        np.testing.assert_array_equal(o["g1"].view(np.int32), gr1.view(np.int32))
+        np.testing.assert_array_equal(o["g2"].view(np.int32), gr2.view(np.int32))
 
 
 def test_loss_grad_collapsed_cloud(cuda, oracle):
@@ -506,15 +510,17 @@ def test_loss_grad_collapsed_cloud(cuda, oracle):
 
 
 def test_loss_grad_nonfinite(cuda, oracle):
+    import pcm_hip
     a, c = _clouds(112, 2, 600, 500)
     a[0, 17, 1] = float("nan")
     c[1, 3, 0] = float("inf")
     ref = oracle.chamfer_forward(a.numpy(), c.numpy())
-    o, _, _ = _loss_grad(cuda, a, c)
-    np.testing.assert_array_equal(o["i1"], ref[2])
-    np.testing.assert_array_equal(o["i2"], ref[3])
-    np.testing.assert_array_equal(o["d1"], ref[0])
-    np.testing.assert_array_equal(o["d2"], ref[1])
+    for v in range(pcm_hip.tune_num_chamfer_loss_grad_variants()):
+        o, _, _ = _loss_grad(cuda, a, c, variant=v)
+        np.testing.assert_array_equal(o["i1"], ref[2])
+        np.testing.assert_array_equal(o["i2"], ref[3])
+        np.testing.assert_array_equal(o["d1"], ref[0])
+        np.testing.assert_array_equal(o["d2"], ref[1])
 
 
 def test_loss_grad_graph_replay_and_shared_workspace(cuda, oracle):

@@ -111,13 +111,26 @@ def run_fused(v, b, n, m, dev):
           f"{statistics.median(spread):.2f} max {max(spread):.2f} us")
     # the forward's own stamps (table's lower half, same workgroup numbering)
     lo = [[buf[i * 8 + k] for k in range(8)] for i in range(nblk - 1)]
+    if v == 6:  # the matrix-core forward stores its near-tie census in slot 0
+        nl = [r[0] & 0xffff for r in lo]
+        full = sum((r[0] >> 16) & 0xffffff for r in lo)
+        single = sum(r[0] >> 40 for r in lo)
+        print(f"  near-ties per workgroup: median {statistics.median(nl)} max {max(nl)} total {sum(nl)} "
+              f"({100.0 * sum(nl) / (64 * FUSED_QPT[v] * len(lo)):.2f}% of queries); whole quarters {full}, "
+              f"single chunks {single}")
+        cyc = [[buf[(8192 + i) * 8 + k] for k in range(8)] for i in range(nblk - 1)]
+        ghz = [(c[6] - c[1]) / ((r[6] - r[1]) * 10.0) for c, r in zip(cyc, lo) if r[6] > r[1]]
+        print(f"  shader clock over stamps 1..6: median {statistics.median(ghz):.2f} GHz, "
+              f"min {min(ghz):.2f}, max {max(ghz):.2f}")
+        for r in lo:
+            r[0] = r[1]
     for nm, k0, k1 in [("centre", 0, 1), ("stage", 1, 2), ("scan", 2, 3), ("proof", 3, 4), ("rescan", 4, 5),
                        ("ties", 5, 6)]:
         dur = [(r[k1] - r[k0]) * TICK_US for r in lo]
         print(f"  fwd {nm:7s} median {statistics.median(dur):7.2f} us  max {max(dur):7.2f}")
 
 
-FUSED_QPT = [2, 4, 2, 4, 4, 4]              # csrc/chamfer_filt.hip kGradVariants
+FUSED_QPT = [2, 4, 2, 4, 4, 4, 4]             # csrc/chamfer_filt.hip kGradVariants
 
 
 def main():

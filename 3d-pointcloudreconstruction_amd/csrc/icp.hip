@@ -35,7 +35,8 @@ namespace {
 
 constexpr int kIcpThreads = 1024;
 constexpr int kIcpWaves = kIcpThreads / 64;
-constexpr int kIcpMaxN = 4096;                 // 36 B of LDS per point (src x,y,z,w float64 + idx)
+constexpr int kIcpMaxN = 16384;                // 16 slices of <= 1024 points per pair
+constexpr int kIcpRowsLdsMax = 96 * 1024;      // rows staged in LDS for the rescans up to this size
 constexpr int kNnThreads = 256;                // one query per thread
 constexpr int kPrepThreads = 256;
 constexpr float kNnErr = 4.76837158203125e-07f;  // 2^-21
@@ -602,9 +603,9 @@ __device__ __forceinline__ void nn_screen_split(pcm_cf4 *rows, const pcm_f4 *__r
     __syncthreads();
 }
 
-template <int QPT>
+template <int QPT, bool kLdsRows>
 __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restrict__ A, const double *__restrict__ B,
-                                                          int b, int n, int K, int S,
+                                                          int b, int pair0, int n, int K, int S,
                                                           const double *__restrict__ init_pose, int max_it,
                                                           double tol, const NnHdr *__restrict__ hdr,
                                                           const pcm_f4 *__restrict__ rows_all, IcpWs ws,
@@ -612,7 +613,8 @@ __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restri
                                                           int32_t *__restrict__ iters_out) {
     extern __shared__ __align__(16) unsigned char smem[];
     pcm_f4 *sRows = reinterpret_cast<pcm_f4 *>(smem);                      // [mpad] rows, for the rescans
-    unsigned long long *mk = reinterpret_cast<unsigned long long *>(smem + (size_t)nn_mpad(n) * 16);  // [S]
+    unsigned long long *mk =
+        reinterpret_cast<unsigned long long *>(smem + (kLdsRows ? (size_t)nn_mpad(n) * 16 : 0));  // [S]
     unsigned *m2 = reinterpret_cast<unsigned *>(mk + S);                   // [S] merged d2 key
     double *sx = reinterpret_cast<double *>(m2 + ((S + 1) & ~1));
     double *sy = sx + S, *sz = sy + S, *sw = sz + S;
@@ -622,7 +624,9 @@ __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restri
     __shared__ double sT[12];
     __shared__ int sDone, sOk;
 
-    const int bi = blockIdx.x / K, k = blockIdx.x - bi * K, tid = threadIdx.x, lane = tid & 63;
+    // pairs [pair0, pair0 + gridDim.x / K) in this launch: K * pairs <= 256
+    // workgroups, all co-resident (the pair's slices wait on each other)
+    const int bl = blockIdx.x / K, k = blockIdx.x - bl * K, bi = pair0 + bl, tid = threadIdx.x, lane = tid & 63;
     const int j0 = k * S, j1 = min(n, j0 + S), ns = j1 - j0;  // this workgroup's slice
     const double *a = A + (size_t)bi * n * 3;
     const double *bb = B + (size_t)bi * n * 3;
@@ -630,8 +634,9 @@ __global__ __launch_bounds__(kIcpThreads) void icp_kernel(const double *__restri
     const int mpad = nn_mpad(n);
     const pcm_f4 *rows_g = rows_all + (size_t)bi * mpad;
     pcm_cf4 *rows = (pcm_cf4 *)(uintptr_t)rows_g;  // the screen: SGPR stream (wave-uniform)
-    const pcm_f4 *rows_v = sRows;                 // the rescans: per-lane chunks, from LDS
-    pcm_dma_to_lds(sRows, rows_g, 16 * mpad, tid >> 6, kIcpWaves);
+    // the rescans: per-lane chunks, from LDS (or global memory for large clouds)
+    const pcm_f4 *rows_v = kLdsRows ? (const pcm_f4 *)sRows : rows_g;
+    if constexpr (kLdsRows) pcm_dma_to_lds(sRows, rows_g, 16 * mpad, tid >> 6, kIcpWaves);
     const double c[3] = {hdr[bi].c[0], hdr[bi].c[1], hdr[bi].c[2]};
     const int nwq = min(kIcpWaves, (ns + 63) / 64);  // waves holding queries in the per-query loops
 
@@ -905,22 +910,33 @@ extern "C" int pcm_icp(const double *A, const double *B, int b, int n, const dou
     const int K = icp_slices(b, n);
     const int S = (n + K - 1) / K;  // points per slice (<= 1024)
     const int qpt = S <= 64 ? 1 : S <= 128 ? 2 : S <= 256 ? 4 : S <= 512 ? 8 : 16;
-    const size_t lds = (size_t)nn_mpad(n) * 16 + (size_t)S * (8 + 4 + 32) + 8;
+    const bool lds_rows = (size_t)nn_mpad(n) * 16 <= (size_t)kIcpRowsLdsMax;
+    const size_t lds = (lds_rows ? (size_t)nn_mpad(n) * 16 : 0) + (size_t)S * (8 + 4 + 32) + 8;
+    // pairs per launch: every slice of a pair must be resident while the
+    // others wait on it, so a launch holds at most 256 workgroups (one per CU)
+    const int per_launch = K <= 256 ? 256 / K : 1;
     auto launch = [&](auto kfn) -> int {
         if (lds > 64 * 1024 &&
             hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
             return PCM_ERR_LAUNCH;
-        hipLaunchKernelGGL(kfn, dim3((unsigned)(b * K)), dim3(kIcpThreads), lds, s, A, B, b, n, K, S, init_pose,
-                           max_iterations, tolerance, hdr, rows, ws, T_out, distances, iterations);
+        for (int p0 = 0; p0 < b; p0 += per_launch) {
+            const int np = b - p0 < per_launch ? b - p0 : per_launch;
+            hipLaunchKernelGGL(kfn, dim3((unsigned)(np * K)), dim3(kIcpThreads), lds, s, A, B, b, p0, n, K, S,
+                               init_pose, max_iterations, tolerance, hdr, rows, ws, T_out, distances, iterations);
+        }
         return PCM_OK;
     };
     int rc;
-    switch (qpt) {
-        case 1: rc = launch(icp_kernel<1>); break;
-        case 2: rc = launch(icp_kernel<2>); break;
-        case 4: rc = launch(icp_kernel<4>); break;
-        case 8: rc = launch(icp_kernel<8>); break;
-        default: rc = launch(icp_kernel<16>); break;
+    if (lds_rows) {
+        switch (qpt) {
+            case 1: rc = launch(icp_kernel<1, true>); break;
+            case 2: rc = launch(icp_kernel<2, true>); break;
+            case 4: rc = launch(icp_kernel<4, true>); break;
+            case 8: rc = launch(icp_kernel<8, true>); break;
+            default: rc = launch(icp_kernel<16, true>); break;
+        }
+    } else {  // above 96 KB of rows: N > 6144, so S >= 384 (QPT 8 or 16)
+        rc = qpt <= 8 ? launch(icp_kernel<8, false>) : launch(icp_kernel<16, false>);
     }
     if (rc != PCM_OK) return rc;
     return pcm_launch_status();

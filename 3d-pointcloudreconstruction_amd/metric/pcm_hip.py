@@ -32,8 +32,8 @@ EXPORTED = (
     "pcm_npy_cloud_points", "pcm_npy_load_clouds",
 )
 
-# largest cloud pcm_icp holds in LDS (csrc/icp.hip kIcpMaxN)
-ICP_MAX_POINTS = 4096
+# largest cloud pcm_icp takes (csrc/icp.hip kIcpMaxN: 16 slices of 1024 points)
+ICP_MAX_POINTS = 16384
 
 # largest cloud (points per batch element) pcm_chamfer_loss_grad runs as one
 # launch (csrc/chamfer_filt.hip kGradCap); larger clouds take forward + backward

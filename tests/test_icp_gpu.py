@@ -150,8 +150,10 @@ def test_icp_batch_matches_oracle_per_pair(icp_mod, cuda):
         np.testing.assert_allclose(dist[k], do, rtol=1e-9, atol=1e-13)
 
 
-@pytest.mark.parametrize("n", [1, 3, 255, 1025, 3072])
+@pytest.mark.parametrize("n", [1, 3, 255, 1025, 3072, 8192, 16384])
 def test_icp_sizes(icp_mod, n):
+    # above 6144 points the rescans read B's rows from global memory; 16384 =
+    # 16 slices of 1024 (the cap)
     rng = np.random.default_rng(n)
     A = rng.random((n, 3))
     B = A @ _rot(rng, 5.0).T + 0.02
@@ -160,6 +162,26 @@ def test_icp_sizes(icp_mod, n):
     assert i == io
     np.testing.assert_allclose(T, To, rtol=0, atol=1e-9)
     np.testing.assert_allclose(dist, do, rtol=1e-9, atol=1e-13)
+
+
+@pytest.mark.parametrize("b,n", [(100, 4096), (300, 200)])
+def test_icp_batch_in_launch_chunks(icp_mod, cuda, b, n):
+    # more slices than CUs: the pairs go out in several launches of at most
+    # 256 workgroups (a pair's slices wait on each other, so all must be
+    # resident); sampled pairs from every launch against the oracle
+    rng = np.random.default_rng(b + n)
+    A = rng.random((b, n, 3))
+    B = np.stack([A[k] @ _rot(rng, 3.0).T + 0.01 for k in range(b)])
+    T, dist, iters = icp_mod.icp_batch(torch.from_numpy(A).to(cuda), torch.from_numpy(B).to(cuda),
+                                       max_iterations=6, tolerance=1e-12)
+    T, dist, iters = T.cpu().numpy(), dist.cpu().numpy(), iters.cpu().numpy()
+    import pcm_hip
+    pcm_hip.icp_workspace_status(pcm_hip._nn_workspace(cuda, b, n), b, n)  # no wait timed out
+    for k in sorted({0, 1, b // 2, b - 2, b - 1}):
+        To, do, io = icp_oracle.icp(A[k], B[k], max_iterations=6, tolerance=1e-12)
+        assert iters[k] == io
+        np.testing.assert_allclose(T[k], To, rtol=0, atol=1e-9)
+        np.testing.assert_allclose(dist[k], do, rtol=1e-9, atol=1e-13)
 
 
 @pytest.mark.parametrize("kind", ["two_points", "collinear"])
@@ -210,7 +232,7 @@ def test_icp_rejects_bad_input(icp_mod, cuda):
     with pytest.raises(ValueError):
         icp_mod.icp(bad, A)
     with pytest.raises(ValueError):
-        icp_mod.icp(np.zeros((5000, 3)), np.zeros((5000, 3)))
+        icp_mod.icp(np.zeros((16385, 3)), np.zeros((16385, 3)))
     with pytest.raises(AssertionError):
         icp_mod.icp(A, A[:8])
 
@@ -218,15 +240,15 @@ def test_icp_rejects_bad_input(icp_mod, cuda):
 def test_capi_status_codes(cuda):
     import pcm_hip
     L = pcm_hip.load_library()
-    A = torch.zeros(1, 5000, 3, dtype=torch.float64, device=cuda)
+    A = torch.zeros(1, 16385, 3, dtype=torch.float64, device=cuda)
     T = torch.empty(1, 4, 4, dtype=torch.float64, device=cuda)
-    d = torch.empty(1, 5000, dtype=torch.float64, device=cuda)
+    d = torch.empty(1, 16385, dtype=torch.float64, device=cuda)
     it = torch.empty(1, dtype=torch.int32, device=cuda)
-    ws_b = L.pcm_icp_workspace_bytes(1, 5000)
+    ws_b = L.pcm_icp_workspace_bytes(1, 16385)
     ws = torch.empty(ws_b, dtype=torch.uint8, device=cuda)
     s = pcm_hip._stream(cuda)
     p = pcm_hip._ptr
-    assert L.pcm_icp(p(A), p(A), 1, 5000, None, 10, 1e-3, p(T), p(d), p(it), p(ws), ws_b, s) == -4  # UNSUPPORTED
+    assert L.pcm_icp(p(A), p(A), 1, 16385, None, 10, 1e-3, p(T), p(d), p(it), p(ws), ws_b, s) == -4  # UNSUPPORTED
     assert L.pcm_icp(p(A), p(A), 1, 16, None, 0, 1e-3, p(T), p(d), p(it), p(ws), ws_b, s) == -1    # iterations < 1
     assert L.pcm_icp(p(A), p(A), 0, 16, None, 5, 1e-3, p(T), p(d), p(it), p(ws), ws_b, s) == 0     # empty batch
     assert L.pcm_icp(p(A), p(A), 1, 16, None, 5, 1e-3, p(T), p(d), p(it), p(ws), 16, s) == -3      # workspace

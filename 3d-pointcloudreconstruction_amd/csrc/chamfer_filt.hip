@@ -495,7 +495,58 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         // barriers).  Otherwise: the workgroup cooperates, kTB queries per pass
         // (one pass over the global candidates serves them all).
         const int nl = sNList;
-        if (resident) {
+        if (resident && nl > 0 && nl <= W) {
+            // few near-ties (the usual case): each query's scan split over
+            // PW = W / nl waves (rounded down to a power of two), four
+            // candidates per lane in flight, ascending per lane; the parts
+            // merge lexicographically.  A workgroup with one near-tie used to
+            // spend ~1.9 us here, one dependent LDS round trip per candidate.
+            int PW = W;
+            while (PW * nl > W) PW >>= 1;
+            const int e = wave / PW, r = wave - e * PW;
+            if (e < nl) {
+                const int s = sList[e];
+                float x = rx[0], y = ry[0], z = rz[0];
+#pragma unroll
+                for (int qq = 1; qq < QPT; ++qq)
+                    if ((s >> 6) == qq) { x = rx[qq]; y = ry[qq]; z = rz[qq]; }
+                x = __shfl(x, s & 63, 64);
+                y = __shfl(y, s & 63, 64);
+                z = __shfl(z, s & 63, 64);
+                float bd = PCM_INF;
+                int bk = 0x7fffffff;
+                const int step = 64 * PW;
+                for (int k0 = r * 64 + lane; k0 < nt; k0 += 4 * step) {
+                    float tx[4], ty[4], tz[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int sk = slot(min(k0 + u * step, nt - 1));
+                        tx[u] = sT[0][sk];
+                        ty[u] = sT[1][sk];
+                        tz[u] = sT[2][sk];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const float d = pcm_sqd(tx[u] - x, ty[u] - y, tz[u] - z);
+                        if (k0 + u * step < nt) pcm_lexmin(bd, bk, d, k0 + u * step);
+                    }
+                }
+                pcm_wave_lexmin(bd, bk);
+                if (lane == 0) {
+                    sTD[wave] = bd;
+                    sTK[wave] = bk;
+                }
+            }
+            __syncthreads();
+            if (tid < nl) {
+                float d = sTD[tid * PW];
+                int k = sTK[tid * PW];
+                for (int w = 1; w < PW; ++w) pcm_lexmin(d, k, sTD[tid * PW + w], sTK[tid * PW + w]);
+                sD[sList[tid]] = d;
+                sK[sList[tid]] = k;
+            }
+            __syncthreads();
+        } else if (resident) {
             for (int e = wave; e < nl; e += W) {
                 const int s = sList[e];
                 float x = rx[0], y = ry[0], z = rz[0];
@@ -511,8 +562,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                     const int sk = slot(k);
                     pcm_lexmin(bd, bk, pcm_sqd(sT[0][sk] - x, sT[1][sk] - y, sT[2][sk] - z), k);
                 }
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) pcm_lexmin(bd, bk, __shfl_xor(bd, o, 64), __shfl_xor(bk, o, 64));
+                pcm_wave_lexmin(bd, bk);
                 if (lane == 0) {
                     sD[s] = bd;
                     sK[s] = bk;

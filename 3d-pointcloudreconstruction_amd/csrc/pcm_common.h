@@ -32,6 +32,28 @@ __device__ __forceinline__ void pcm_lexmin(float &d, int &k, float dv, int kv) {
     k = take ? kv : k;
 }
 
+// Wave-wide lexicographic (d, k) minimum by DPP row_shr 1/2/4/8 then
+// row_bcast 15/31 (VALU operand modifiers, no LDS round trip); the result is
+// returned wave-uniform from lane 63.  Lanes a pattern does not feed keep
+// their own pair (old = self), and a lexmin with itself is a no-op.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void pcm_lexmin_dpp_step(float &d, int &k) {
+    const float dv = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(d), __float_as_int(d), CTRL, ROWMASK,
+                                                                0xf, false));
+    const int kv = __builtin_amdgcn_update_dpp(k, k, CTRL, ROWMASK, 0xf, false);
+    pcm_lexmin(d, k, dv, kv);
+}
+__device__ __forceinline__ void pcm_wave_lexmin(float &d, int &k) {
+    pcm_lexmin_dpp_step<0x111, 0xf>(d, k);  // row_shr:1
+    pcm_lexmin_dpp_step<0x112, 0xf>(d, k);  // row_shr:2
+    pcm_lexmin_dpp_step<0x114, 0xf>(d, k);  // row_shr:4
+    pcm_lexmin_dpp_step<0x118, 0xf>(d, k);  // row_shr:8
+    pcm_lexmin_dpp_step<0x142, 0xa>(d, k);  // row_bcast:15
+    pcm_lexmin_dpp_step<0x143, 0xc>(d, k);  // row_bcast:31
+    d = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d), 63));
+    k = __builtin_amdgcn_readlane(k, 63);
+}
+
 __device__ __forceinline__ bool pcm_finite(float v) {
     return __builtin_isfinite(v);
 }

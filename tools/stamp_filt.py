@@ -127,7 +127,9 @@ def run_fused(v, b, n, m, dev):
     for nm, k0, k1 in [("centre", 0, 1), ("stage", 1, 2), ("scan", 2, 3), ("proof", 3, 4), ("rescan", 4, 5),
                        ("ties", 5, 6)]:
         dur = [(r[k1] - r[k0]) * TICK_US for r in lo]
-        print(f"  fwd {nm:7s} median {statistics.median(dur):7.2f} us  max {max(dur):7.2f}")
+        srt = sorted(dur)
+        print(f"  fwd {nm:7s} median {statistics.median(dur):7.2f} us  p90 {srt[int(0.9 * len(srt))]:7.2f}  "
+              f"max {max(dur):7.2f}  (>1 us: {sum(d > 1.0 for d in dur)} workgroups)")
 
 
 FUSED_QPT = [2, 4, 2, 4, 4, 4, 4]             # csrc/chamfer_filt.hip kGradVariants

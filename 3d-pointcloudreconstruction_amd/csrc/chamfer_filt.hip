@@ -155,7 +155,8 @@ __device__ __forceinline__ void filt_group4(float (&mn)[4], const pcm_f2 (&px)[4
 // for the loss partial.  `arena` holds FiltLds<W, QPT, TILE>::kBytes.
 template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1>
 __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const TIn *__restrict__ T, int nq, int nt, int qbase,
-                              float *__restrict__ D, int32_t *__restrict__ I, unsigned char *arena) {
+                              float *__restrict__ D, int32_t *__restrict__ I, unsigned char *arena,
+                              unsigned long long *__restrict__ Gr = nullptr, unsigned long long tag = 0) {
     static_assert(C % 4 == 0 && TILE % C == 0, "tile must hold whole chunks of 4-candidate groups");
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
@@ -648,6 +649,10 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             my_d = sD[tid];
             out_st<kSc1>(D + qbase + tid, my_d);
             out_st<kSc1>(I + qbase + tid, (int32_t)sK[tid]);
+            // data-tagged argmin granule {call tag, idx}: one 8-byte sc1 store,
+            // its own flag (no drain, no counter)
+            if (Gr) __hip_atomic_store(Gr + qbase + tid, tag | (unsigned)sK[tid], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
         }
     } else {
         for (int s = tid; s < QW; s += NT) {
@@ -660,6 +665,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             my_d = d;
             out_st<kSc1>(D + qi, d);
             out_st<kSc1>(I + qi, (int32_t)idx);
+            if (Gr) __hip_atomic_store(Gr + qi, tag | (unsigned)idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     return my_d;
@@ -1240,11 +1246,14 @@ __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, flo
 // S / A: the range's cloud and the other cloud (LDS); nq / na their sizes;
 // gs / h: 2w of the range's direction (direct term) and of the other one
 // (scatter terms); Iown / Ioth: the argmins (written by other workgroups: sc1).
-template <int NT, int QW>
-__device__ __forceinline__ void range_grad(bool dir1, int q0, int nq, int na, const float *S, const float *A,
+template <int NT, int QW, bool kGran = false>
+__device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, const float *S, const float *A,
                                            float gs, float h, const int32_t *__restrict__ Iown,
                                            const int32_t *__restrict__ Ioth, float *__restrict__ G,
-                                           unsigned char *scratch) {
+                                           unsigned char *scratch,
+                                           const unsigned long long *__restrict__ Gown = nullptr,
+                                           const unsigned long long *__restrict__ Goth = nullptr,
+                                           unsigned long long tag = 0, unsigned max_spins = 0) {
     constexpr int kPerS = (kGradCap + NT - 1) / NT;  // sources per thread
     constexpr int NW = NT / 64;
     __shared__ int sOvf[QW];   // overflowed targets (range slot)
@@ -1258,10 +1267,43 @@ __device__ __forceinline__ void range_grad(bool dir1, int q0, int nq, int na, co
     int *lst = reinterpret_cast<int *>(tab + QW * kGradSlots);     // [na] overflow source list
 
     const int jt = q0 + tid;  // this thread's target (tid < QW)
-    const int io = (tid < QW && jt < nq) ? ld_sc1(Iown + jt) : 0;
+    int io = 0;
     int isr[kPerS];
+    if constexpr (kGran) {
+        // the argmins as data-tagged granules: sweep until every one this
+        // thread needs carries the call's tag (bounded; the whole workgroup
+        // decides together), re-reading only those not yet current
+        const bool own = tid < QW && jt < nq;
+        unsigned long long go = own ? __hip_atomic_load(Gown + jt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
+        unsigned long long gr[kPerS];
 #pragma unroll
-    for (int r = 0; r < kPerS; ++r) isr[r] = ld_sc1(Ioth + min(tid + r * NT, na - 1));
+        for (int r = 0; r < kPerS; ++r)
+            gr[r] = __hip_atomic_load(Goth + min(tid + r * NT, na - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned want = (unsigned)(tag >> 32);
+        for (unsigned spins = 0;; ++spins) {
+            bool ready = (unsigned)(go >> 32) == want;
+#pragma unroll
+            for (int r = 0; r < kPerS; ++r) ready &= (unsigned)(gr[r] >> 32) == want;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (and the caller's LDS-DMA has landed)
+            if (!__syncthreads_or(ready ? 0 : 1)) break;
+            if (spins >= max_spins) return false;  // uniform: every thread saw the same vote
+            __builtin_amdgcn_s_sleep(1);
+            if (own && (unsigned)(go >> 32) != want)
+                go = __hip_atomic_load(Gown + jt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+            for (int r = 0; r < kPerS; ++r)
+                if ((unsigned)(gr[r] >> 32) != want)
+                    gr[r] = __hip_atomic_load(Goth + min(tid + r * NT, na - 1), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+        }
+        io = (int)(unsigned)go;
+#pragma unroll
+        for (int r = 0; r < kPerS; ++r) isr[r] = (int)(unsigned)gr[r];
+    } else {
+        io = (tid < QW && jt < nq) ? ld_sc1(Iown + jt) : 0;
+#pragma unroll
+        for (int r = 0; r < kPerS; ++r) isr[r] = ld_sc1(Ioth + min(tid + r * NT, na - 1));
+    }
     if (tid < QW) cnt[tid] = 0;
     if (tid == 0) sNOvf = 0;
     __syncthreads();
@@ -1357,6 +1399,7 @@ __device__ __forceinline__ void range_grad(bool dir1, int q0, int nq, int na, co
         }
         __syncthreads();
     }
+    return true;
 }
 
 // Workspace of the fused kernel (after pcm_chamfer_forward_loss's bytes, so one
@@ -1368,15 +1411,18 @@ struct GradWs {
     unsigned *epoch, *bcount, *bdepart;
     float *wpart;
     unsigned long long *gran;
+    unsigned long long *wg;  // granule hand-off: per-workgroup {tag, loss partial}
+    unsigned long long *ig;  // granule hand-off: per-point {tag, argmin}, cloud 1 [b n] then cloud 2 [b m]
 };
 constexpr int kGradErrWord = 4;  // word of the first line: non-zero after a timed-out wait (sticky)
 // each batch element's arrival and departure counters on 128-byte lines of
 // their own: with all of them in one line, the 8 adds and the polls per
 // element queue behind every other element's at the memory side
 constexpr int kCtrStride = 32;  // unsigned words
-inline size_t grad_ws_bytes(int b, long long blocks) {
+inline size_t grad_ws_bytes(int b, long long blocks, long long pts) {
     const size_t c = (size_t)b * 128, p = ((size_t)blocks * 4 + 127) / 128 * 128;
-    return 128 + 2 * c + p + (size_t)b * 16;
+    const size_t g = ((size_t)b * 16 + 127) / 128 * 128, wg = ((size_t)blocks * 8 + 127) / 128 * 128;
+    return 128 + 2 * c + p + g + wg + (size_t)pts * 8;
 }
 inline GradWs grad_ws(void *base, int b, long long blocks) {
     char *p = (char *)base;
@@ -1387,6 +1433,8 @@ inline GradWs grad_ws(void *base, int b, long long blocks) {
     w.bdepart = (unsigned *)(p + 128 + c);
     w.wpart = (float *)(p + 128 + 2 * c);
     w.gran = (unsigned long long *)((char *)w.wpart + ((size_t)blocks * 4 + 127) / 128 * 128);
+    w.wg = (unsigned long long *)((char *)w.gran + ((size_t)b * 16 + 127) / 128 * 128);
+    w.ig = (unsigned long long *)((char *)w.wg + ((size_t)blocks * 8 + 127) / 128 * 128);
     return w;
 }
 
@@ -1432,7 +1480,48 @@ __device__ __forceinline__ void poll_grad_loss(int b, int n, int m, const GradWs
     }
 }
 
-template <int W, int QPT, int C, int TILE, bool kMfma = false>
+// granule hand-off: the grid's last workgroup sweeps the b * per per-workgroup
+// {tag, partial} granules (bounded), sums them in a fixed order (lanes over
+// granules, direction by the workgroup's slot, then one wave sum each) and
+// advances the epoch
+__device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, int nblk1, const GradWs &ws,
+                                                  float *__restrict__ mean_out, unsigned max_spins) {
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    const unsigned epoch = ws.epoch[0] + 1u;
+    const int total = b * per;
+    float s1 = 0.f, s2 = 0.f;
+    bool ok = true;
+    for (int base = 0; base < total && ok; base += 64) {
+        const int i = base + lane;
+        unsigned long long x = (unsigned long long)epoch << 32;
+        for (unsigned spins = 0;; ++spins) {
+            if (i < total) x = __hip_atomic_load(ws.wg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (__all((unsigned)(x >> 32) == epoch)) break;
+            if (spins >= max_spins) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        const float v = __uint_as_float((unsigned)x);
+        if (i < total) {
+            if (i % per < nblk1) s1 += v;
+            else s2 += v;
+        }
+    }
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    if (lane == 0) {
+        if (!ok) __hip_atomic_store(ws.epoch + kGradErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = ok && ws.epoch[kGradErrWord] == 0u;
+        const float m1 = ok ? s1 / ((float)b * (float)n) : __builtin_nanf("");
+        const float m2 = ok ? s2 / ((float)b * (float)m) : __builtin_nanf("");
+        mean_out[0] = m1;
+        mean_out[1] = m2;
+        mean_out[2] = m1 + m2;
+        ws.epoch[0] = epoch;
+    }
+}
+
+template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -1453,7 +1542,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int nprod = (int)gridDim.x - 1;
     if ((int)blockIdx.x == nprod) {
         PCM_STAMP2(5);
-        poll_grad_loss(b, n, m, ws, mean_out, max_spins);
+        if constexpr (kGran) poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, max_spins);
+        else poll_grad_loss(b, n, m, ws, mean_out, max_spins);
         PCM_STAMP2(6);
         return;
     }
@@ -1468,6 +1558,47 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int q0 = (first ? r : r - nblk1) * QW;
     const float *X1 = xyz1 + (size_t)batch * n * 3;
     const float *X2 = xyz2 + (size_t)batch * m * 3;
+    if constexpr (kGran) {
+        // ---- granule hand-off (no counters): the forward publishes every
+        // argmin as a {tag, idx} granule and the workgroup's partial as a
+        // {tag, sum} granule; the gradient phase sweeps the granules it needs
+        const unsigned long long tag = (unsigned long long)(ws.epoch[0] + 1u) << 32;
+        unsigned long long *G1 = ws.ig + (size_t)batch * n, *G2 = ws.ig + (size_t)b * n + (size_t)batch * m;
+        const float my_d = filt_forward<float, W, QPT, C, TILE, false>(
+            first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
+            first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
+            first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, first ? G1 : G2, tag);
+        PCM_STAMP2(1);
+        const float s = wave_sum(my_d);
+        if (lane == 0) sRed[wave] = s;
+        __syncthreads();
+        if (tid == 0) {
+            float t = 0.f;
+            for (int w = 0; w < W; ++w) t += sRed[w];
+            __hip_atomic_store(ws.wg + bid, tag | __float_as_uint(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // the batch element's clouds for the gradient phase (the arena is free);
+        // they land during the sweep
+        pcm_dma_to_lds(arena, X1, 12 * n, wave, W);
+        pcm_dma_to_lds(arena + 12 * kGradCap, X2, 12 * m, wave, W);
+        PCM_STAMP2(2);
+        float *G = first ? grad1 + (size_t)batch * n * 3 : grad2 + (size_t)batch * m * 3;
+        const float *P1 = reinterpret_cast<const float *>(arena);
+        const float *P2 = P1 + 3 * kGradCap;
+        const float g1 = __fmul_rn(w1, 2.f), g2 = __fmul_rn(w2, 2.f);
+        const bool ok = first ? range_grad<NT, QW, true>(true, q0, n, m, P1, P2, g1, g2, nullptr, nullptr, G,
+                                                          arena + 24 * kGradCap, G1, G2, tag, max_spins)
+                              : range_grad<NT, QW, true>(false, q0, m, n, P2, P1, g2, g1, nullptr, nullptr, G,
+                                                          arena + 24 * kGradCap, G2, G1, tag, max_spins);
+        if (!ok) {  // a workgroup of this element never published: sticky error, NaN gradients
+            if (tid == 0) __hip_atomic_store(ws.epoch + kGradErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int nq = first ? n : m;
+            for (int t = tid; t < 3 * QW; t += NT)
+                if (q0 * 3 + t < 3 * nq) G[3 * q0 + t] = __builtin_nanf("");
+        }
+        PCM_STAMP2(7);
+        return;
+    }
     float my_d;
     if constexpr (kMfma)
         my_d = filt_forward_mfma<true>(first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
@@ -1610,11 +1741,13 @@ const GradVariant kGradVariants[] = {
     {chamfer_loss_grad_kernel<8, 4, 32, 1024>, 8, 4},  // 4
     {chamfer_loss_grad_kernel<16, 4, 32, 1024>, 16, 4},  // 5
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, true>, 8, 4},  // 6: screen on the matrix cores
+    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true>, 8, 4},  // 7: granule hand-off
 };
 constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
 // tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,
-// W=8 QPT=2 19.3 us, W=4 QPT=2 21.4 us
-constexpr int kDefaultGradVariant = 1;
+// W=8 QPT=2 19.3 us, W=4 QPT=2 21.4 us; round 2: variant 1 (arrival counter
+// hand-off) 16.25 us, variant 7 (the same forward, granule hand-off) 14.97 us
+constexpr int kDefaultGradVariant = 7;
 
 long long grad_blocks(const GradVariant &v, int b, int n, int m, int &nblk1, int &nblk2) {
     const int QW = 64 * v.qpt;
@@ -1647,7 +1780,8 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
     const long long blocks = grad_blocks(v, b, n, m, nblk1, nblk2);
     if (blocks > 0x7ffffffeLL) return PCM_ERR_UNSUPPORTED;
     const size_t off = pcm_chamfer_loss_ws_offset(b, n, m);
-    if (workspace_bytes < off + grad_ws_bytes(b, grad_blocks_max(b, n, m))) return PCM_ERR_WORKSPACE;
+    if (workspace_bytes < off + grad_ws_bytes(b, grad_blocks_max(b, n, m), (long long)b * (n + m)))
+        return PCM_ERR_WORKSPACE;
     const GradWs ws = grad_ws((char *)workspace + off, b, blocks);
     // + the polling workgroup (the grid's last)
     hipLaunchKernelGGL(v.k, dim3((unsigned)blocks + 1), dim3(64 * v.waves), 0, (hipStream_t)stream, xyz1, xyz2, b,
@@ -1660,7 +1794,7 @@ int pcm_chamfer_grad_err_word(void) { return kGradErrWord; }
 
 size_t pcm_chamfer_grad_ws_bytes(int b, int n, int m) {
     if (b <= 0 || n <= 0 || m <= 0) return 0;
-    return grad_ws_bytes(b, grad_blocks_max(b, n, m));
+    return grad_ws_bytes(b, grad_blocks_max(b, n, m), (long long)b * (n + m));
 }
 
 extern "C" int pcm_chamfer_loss_grad(const float *xyz1, const float *xyz2, int b, int n, int m, float w1,

@@ -51,7 +51,7 @@ GRAPH_STEPS = 10                   # steps captured per hipGraph replay
 # up in for roofline.traffic (tools/pmc_passes.sh + tools/pmc_summarize.py)
 FWD_KERNEL = "chamfer_fwd_sgpr_kernel<8, 2, 16, 3>"
 BWD_KERNEL = "chamfer_bwd_staged_kernel"
-FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024>"
+FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true>"  # the default variant (granule hand-off)
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r02", "pmc_summary.json")
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)

@@ -1098,9 +1098,10 @@ constexpr int kDefaultLossMode = 3;  // tools/tune_chamfer.py (profiles/r01): mo
 // B=8, N=M=16384 the filtered W=8 QPT=4 C=32 variant takes 344-356 us against
 // 457-471 us for the best exact-scan form; at B=32, N=M=1024 the two are level
 // (12.2 vs 12.4 us) and the SGPR form keeps the small sizes.
-inline int default_fwd_variant(int n, int m) {
-    return (long long)n * m >= (1LL << 22) ? kNumBaseFwdVariants + 3 : 8;
-}
+// Round 2 (near-tie scans split over the waves, DPP reductions): the
+// filtered W=8 QPT=4 C=32 form leads at config 2 as well -- 11.96 us against
+// 12.45 us for the SGPR form -- so it is the default at every size.
+inline int default_fwd_variant(int, int) { return kNumBaseFwdVariants + 3; }
 
 int fwd_grid(const FwdVariant &v, int b, int n, int m, int &nblk1, int &nblk2, long long &blocks) {
     const int QW = 64 * v.qpt;
@@ -1300,10 +1301,9 @@ inline const Fwd16Variant &fwd16_variant(int i) {
     return i < kNumBaseFwd16Variants ? kFwd16Variants[i] : kPcmFilt16Variants[i - kNumBaseFwd16Variants];
 }
 // tools/tune_chamfer.py on MI355X (profiles/r01): the filtered form wins once
-// a batch element has >= 4M pairs (B=8, N=M=16384); LDS-tile form below
-inline int default_fwd16_variant(int n, int m) {
-    return (long long)n * m >= (1LL << 22) ? kNumBaseFwd16Variants + 1 : 0;
-}
+// a batch element has >= 4M pairs (B=8, N=M=16384); round 2: also at B=32,
+// N=M=1024 (12.25 us against 13.46 us for the LDS-tile form), so at every size
+inline int default_fwd16_variant(int, int) { return kNumBaseFwd16Variants + 1; }
 
 int launch_fwd16(int variant, const pcm_h *xyz1, const pcm_h *xyz2, int b, int n, int m, float *dist1,
                  float *dist2, int32_t *idx1, int32_t *idx2, void *stream) {

@@ -49,7 +49,7 @@ GRAPH_STEPS = 10                   # steps captured per hipGraph replay
 # the forward kernel instance the step launches at this size (csrc/chamfer.hip
 # default_fwd_variant) and the committed rocprofv3 counter summary it is looked
 # up in for roofline.traffic (tools/pmc_passes.sh + tools/pmc_summarize.py)
-FWD_KERNEL = "chamfer_fwd_sgpr_kernel<8, 2, 16, 3>"
+FWD_KERNEL = "chamfer_fwd_filt_kernel<float, 8, 4, 32, 2048, 3>"  # default fused-loss forward
 BWD_KERNEL = "chamfer_bwd_staged_kernel"
 FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true>"  # the default variant (granule hand-off)
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r02", "pmc_summary.json")

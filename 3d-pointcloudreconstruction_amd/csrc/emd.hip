@@ -434,7 +434,6 @@ struct EmdWs {
     float *inc0;     // [b*n]
     int32_t *board;  // [b*kBoardWords]: gen, quit, jn, err (one 128-B line each)
     int32_t *ml;     // [b*n] job: miss list
-    int32_t *iclaim; // [b*n] job: per-item ticket (-g armed, g claimed)
     int32_t *idone;  // [b*n] job: per-item done generation
     int32_t *rbid;   // [b*n] job results
     float *rinc;     // [b*n]
@@ -491,8 +490,7 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__r
             const bool proven = b2 > T && (unsigned)kb < (unsigned)n;
             ws.bid0[pt] = proven ? kb : -2;  // -2: needs a full scan in the auction kernel
             ws.inc0[pt] = b1 - b2 + eps;
-            ws.iclaim[pt] = 0;  // job tickets and done words of this launch start at 0
-            ws.idone[pt] = 0;
+            ws.idone[pt] = 0;  // done words of this launch start at 0
             if (j == 0) {
                 ws.board[(size_t)batch * kBoardWords + kBoardGen] = 0;
                 ws.board[(size_t)batch * kBoardWords + kBoardQuit] = 0;
@@ -619,19 +617,16 @@ __device__ __forceinline__ void place_bid(const AState<kG> &st, int j, int kb, f
     }
 }
 
-// claim of job item i for generation g through its armed ticket (one wave)
-__device__ __forceinline__ bool claim_item(const EmdWs &ws, size_t base, int i, int g) {
-    int ok = 0;
-    if ((threadIdx.x & 63) == 0) ok = atomicCAS(ws.iclaim + base + i, -g, g) == -g;
-    return __builtin_amdgcn_readfirstlane(ok) != 0;
-}
+// Items of a job are split statically: groups of kWaves consecutive items go
+// round-robin to the master (group 0, H + 1, ...) and helpers 0 .. H - 1, one
+// item per wave of the group -- no claim atomics on anyone's critical path.
+// Owner of item i: (i / kWaves) % (H + 1), 0 = the master, r + 1 = helper r.
 
 // helper side of a job item: full scan with the snapshot prices, cache into
 // region B, result words, then the done word (sc1 throughout)
 __device__ __forceinline__ void helper_item(const EmdWs &ws, size_t base, int i, int g, const float *P,
                                             const float *Qc, const float *price, int n, float eps) {
     const int lane = threadIdx.x & 63;
-    if (!claim_item(ws, base, i, g)) return;
     const int j = __builtin_amdgcn_readfirstlane(ld_sc1(ws.ml + base + i));
     float b1, b2, T;
     int kb;
@@ -694,7 +689,10 @@ __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank
         const int jn = ld_sc1(bw + kBoardJn);
         for (int k = tid; k < n; k += kEmdThreads) sPH[k] = ld_sc1(ws.pp + base + k);
         __syncthreads();
-        for (int i = rank * kWaves + wave; i < jn; i += a.H * kWaves) helper_item(ws, base, i, g, P, Qc, sPH, n, a.eps);
+        for (int g0 = rank + 1; g0 * kWaves < jn; g0 += a.H + 1) {  // this helper's groups (owner rank + 1)
+            const int i = g0 * kWaves + wave;
+            if (i < jn) helper_item(ws, base, i, g, P, Qc, sPH, n, a.eps);
+        }
         if (a.diag == kDiagHist && tid == 0) atomicAdd(&a.stats[2 * a.iters + 12], 1);  // helper wake-ups
         last = g;
         __syncthreads();
@@ -933,23 +931,21 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         }
         if (nm > 0) {
             if (a.H > 0 && nm > a.offload_min) {
-                // publish the job: miss list, armed tickets, price snapshot, size
+                // publish the job: miss list, price snapshot, size
                 ++gen;
-                for (int i = tid; i < nm; i += kEmdThreads) {
-                    st_sc1(ws.ml + base + i, st.miss[i]);
-                    st_sc1(ws.iclaim + base + i, -gen);
-                }
+                for (int i = tid; i < nm; i += kEmdThreads) st_sc1(ws.ml + base + i, st.miss[i]);
                 for (int k = tid; k < n; k += kEmdThreads) st_sc1(ws.pp + base + k, st.price[k]);
                 if (tid == 0) st_sc1(bw + kBoardJn, nm);
                 vm_drain();
                 __syncthreads();
                 if (tid == 0) st_sc1(bw + kBoardGen, gen);
                 PCM_EMD_PHASE(4);
-                // take items from the end while the helpers start at the front;
-                // an item the master scans itself goes to region A and is
-                // marked (miss entry negated) so the collection skips it
-                for (int i = nm - 1 - wave; i >= 0; i -= kWaves) {
-                    if (!claim_item(ws, base, i, gen)) continue;
+                // the master's own groups (owner 0); an item it scans itself
+                // goes to region A and is marked (miss entry negated) so the
+                // collection skips it
+                for (int g0 = 0; g0 * kWaves < nm; g0 += a.H + 1) {
+                    const int i = g0 * kWaves + wave;
+                    if (i >= nm) break;
                     const int j = st.miss[i];
                     own_scan(j);
                     if (lane == 0) st.miss[i] = -1 - j;
@@ -1164,7 +1160,6 @@ size_t ws_layout(int b, int n, EmdWs *w, char *basep) {
     t.inc0 = (float *)take(pts * 4);
     t.board = (int32_t *)take((size_t)b * kBoardWords * 4);
     t.ml = (int32_t *)take(pts * 4);
-    t.iclaim = (int32_t *)take(pts * 4);
     t.idone = (int32_t *)take(pts * 4);
     t.rbid = (int32_t *)take(pts * 4);
     t.rinc = (float *)take(pts * 4);

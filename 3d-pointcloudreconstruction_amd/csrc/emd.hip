@@ -74,6 +74,7 @@ constexpr int kHelperMaxN = 32768;   // helpers keep a price snapshot in LDS (4 
 constexpr int kMaxHelpers = 31;
 constexpr int kBoardWords = 32;      // per batch element: gen, quit, jn, err (128-B line each group)
 constexpr int kSpinLimit = 1 << 22;  // bounded polls (sticky error word on timeout)
+constexpr int kStagePN = 1024;          // the n of the LDS-state, staged-bidder auction form
 constexpr int kDefaultOffloadMin = 24;  // misses above which an iteration is offloaded
 constexpr int kDefaultTailMax = 16;     // bidders at or below which an iteration runs in tail mode
 constexpr int kDefaultWsplit = 1;       // most waves one miss's scan is split over (2, 4: measured slower at config 3 and the training call)
@@ -354,6 +355,10 @@ __device__ __noinline__ void scan_exact(float x1, float y1, float z1, const floa
 // independently of the object.  Exact values are computed for the cached
 // entries only; if their second best does not exceed T the exact scan runs
 // instead.  Keys of objects [kbeg, kend) (a multiple of 256 long) into t.
+// Software-pipelined: the next block's coordinates and prices are loaded
+// before the current block's keys are computed, so a lone wave (one miss per
+// wave, the others at the barrier) waits on one LDS round trip per block
+// instead of several.  Same keys, same push order.
 __device__ __forceinline__ void scan_fast_keys(LaneTop &t, float x1, float y1, float z1, const float *Qc,
                                                const float *price, int kbeg, int kend) {
     const int lane = threadIdx.x & 63;
@@ -657,10 +662,10 @@ struct KArgs {
 constexpr int kDiagHist = 1, kDiagTimers = 2;
 
 // helper role: take full scans of the master's jobs until it quits
-template <bool kStage>
+template <bool kStage, int kN>
 __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank, int *smem) {
     __shared__ int sGen;
-    const int n = a.n;
+    const int n = kN > 0 ? kN : a.n;  // kN: the cloud size fixed at compile time
     const int tid = threadIdx.x, wave = tid >> 6;
     float *sQ = (float *)smem;                                       // [3n] (kStage)
     float *sPH = (float *)smem + (kStage ? 3 * (size_t)n : 0);       // [n] price snapshot
@@ -700,12 +705,12 @@ __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank
 }
 
 // master role: the auction of one batch element
-template <bool kG, bool kStage, bool kStageP>
+template <bool kG, bool kStage, bool kStageP, int kN>
 __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *smem) {
     __shared__ int sNu[2], sNm, sColl, sChainJ;
     __shared__ float sPb1[kWaves], sPb2[kWaves];  // split bids: each wave's part
     __shared__ int sPkb[kWaves];
-    const int n = a.n, iters = a.iters;
+    const int n = kN > 0 ? kN : a.n, iters = a.iters;
     const float eps = a.eps;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const size_t base = (size_t)batch * n;
@@ -762,17 +767,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     vm_drain();  // the DMA has landed
     __syncthreads();
 
-    // the master's own full scan of point j: cache region A, bid placed
-    auto own_scan = [&](int j) {
-        float b1, b2, T;
-        int kb;
-        scan_full<false>(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, C + (size_t)j * kL, b1, kb, b2, T);
-        if (lane == 0) {
-            CT[j] = T;
-            place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
-        }
-    };
-
     int gen = 0;  // jobs posted so far
     // timers (diag >= 2): cycles per phase, kept by thread 0 in LDS (not in
     // registers the whole kernel would reserve)
@@ -788,6 +782,34 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         sTm[i] += tn - sTm[12];                                           \
         sTm[12] = tn;                                                     \
     }
+    // the master's own full scan of point j: cache region A, bid placed
+    // (profiling build: wave 0's key scan, proof and exact fallback timed
+    // in slots 6, 7, 11 and the exact fallbacks counted)
+    auto own_scan = [&](int j) {
+        float b1, b2, T;
+        int kb;
+        const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
+        centry *cj = C + (size_t)j * kL;
+#ifdef PCM_STAMPS
+        LaneTop t;
+        lane_top_init(t);
+        scan_fast_keys(t, x1, y1, z1, Qc, st.price, 0, n);
+        PCM_EMD_PHASE(6);
+        const bool ok = scan_fast_finish<false>(t, x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
+        PCM_EMD_PHASE(7);
+        if (!ok) {
+            scan_exact<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
+            if (hist && lane == 0) atomicAdd(&a.stats[2 * iters + 15], 1);  // exact fallbacks
+            PCM_EMD_PHASE(11);
+        }
+#else
+        scan_full<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
+#endif
+        if (lane == 0) {
+            CT[j] = T;
+            place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
+        }
+    };
     int active = 0, chain_its = 0, tail_its = 0;
     for (int it = 0; it < iters; ++it) {
         const bool last = (it == iters - 1);
@@ -1096,12 +1118,16 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
 // Grid: b masters (blocks 0..b-1) then b*H helpers.  Helper x serves the
 // batch element on its own XCD when b % 8 == 0 (blocks x and x + 8 share one
 // under round-robin dispatch -- speed only, nothing depends on it).
+// The LDS-state form with the bidder cloud staged runs exactly n = 1024 (the
+// launcher's stage_p), so that instantiation fixes n at compile time: loop
+// bounds fold and the master spills fewer scalars.
 template <bool kG, bool kStage, bool kStageP>
 __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(KArgs a, EmdWs ws) {
     extern __shared__ __attribute__((aligned(16))) int smem[];
+    constexpr int kN = (!kG && kStageP) ? kStagePN : 0;
     const int x = (int)blockIdx.x;
     if (x < a.b) {
-        master_loop<kG, kStage, kStageP>(a, ws, x, smem);
+        master_loop<kG, kStage, kStageP, kN>(a, ws, x, smem);
         return;
     }
     const int h = x - a.b;
@@ -1115,7 +1141,7 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(KArgs a, EmdWs
         rank = h / a.b;
     }
     if (rank >= a.H) return;
-    helper_loop<kStage>(a, ws, batch, rank, smem);
+    helper_loop<kStage, kN>(a, ws, batch, rank, smem);
 }
 
 __global__ void emd_bwd_kernel(const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n,
@@ -1230,7 +1256,7 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     const bool g_state = n > kLdsStateMaxN;
     const bool stage = n <= (g_state ? kStageMaxN : kLdsStateMaxN);
     const size_t xchg = 5 * (size_t)kEmdThreads * 4;
-    const bool stage_p = n <= (g_state ? 4096 : 1024);
+    const bool stage_p = n <= (g_state ? 4096 : kStagePN);  // !g_state: n == kStagePN exactly
     const size_t m_lds = (g_state ? 0 : 44 * (size_t)n) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
                          xchg;
     const size_t h_lds = H > 0 ? (stage ? 12 * (size_t)n : 0) + 4 * (size_t)n : 0;

@@ -15,8 +15,9 @@ sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric
 sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "train"))
 import pcm_hip  # noqa: E402
 
-TIMERS = ["bids", "full-scans", "claim", "assign", "scan/publish", "exchange/own-items", "merge", "finish",
-          "chain-entry", "chain-scan", "chain-resolve", "chain-assign"]
+DIAG_WSPLIT = False
+TIMERS = ["bids", "full-scans", "claim", "assign", "scan/publish", "exchange/own-items", "keys|merge",
+          "proof|finish", "chain-entry", "chain-scan", "chain-resolve", "exact"]
 
 
 def timed(x1, x2, eps, iters, d, a, helpers, offload, wsplit=None, reps=5, tail_max=None):
@@ -50,21 +51,24 @@ def run(name, x1, x2, eps, iters, sweep):
     active = int((per[:, 0] > 0).sum())
     print(f"[{name}] B={b} N={n} eps={eps} iters={iters}: iterations with bidders {active}; "
           f"bids {int(per[:, 0].sum())}, full scans {int(per[:, 1].sum())}; offloaded jobs {misc[10]}, "
-          f"items {misc[11]}, helper wake-ups {misc[12]}")
+          f"items {misc[11]}, helper wake-ups {misc[12]}, exact fallbacks {misc[15]}")
     marks = [0, 1, 2, 5, 10, 20, 50, 100, 200, 500, 1000, 2000, 5000, iters - 1]
     print("  unassigned (sum over batch) at iter:", " ".join(f"{i}:{int(per[i, 0])}" for i in marks if i < iters))
     print("  full scans (sum over batch) at iter:", " ".join(f"{i}:{int(per[i, 1])}" for i in marks if i < iters))
     print("  auction wall per batch element (us): min %.1f max %.1f" % (min(wall) / 100.0, max(wall) / 100.0))
     st.zero_()
     slow = max(range(b), key=lambda i: wall[i])
-    st = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=dev)
-    pcm_hip.emd_forward(x1, x2, eps, iters, d, a, stats=st, diag=2 + slow)
-    torch.cuda.synchronize()
-    tm = st.cpu()[2 * iters:2 * iters + 15].tolist()
-    act = max(tm[12], 1)
-    print(f"  slowest batch element {slow}: {act} iterations ({tm[13]} tail mode, {tm[14]} chain mode); "
-          "phase cycles per iteration: " + ", ".join(f"{nm}={16.0 * v / act:.0f}" for nm, v in zip(TIMERS, tm[:12])))
-    print("  phase cycles total (M): " + ", ".join(f"{nm}={16.0 * v / 1e6:.2f}" for nm, v in zip(TIMERS, tm[:12])))
+    for ws in ((None, 4) if DIAG_WSPLIT else (None,)):
+        st = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=dev)
+        kw = {} if ws is None else {"wsplit": ws}
+        pcm_hip.emd_forward(x1, x2, eps, iters, d, a, stats=st, diag=2 + slow, **kw)
+        torch.cuda.synchronize()
+        tm = st.cpu()[2 * iters:2 * iters + 15].tolist()
+        act = max(tm[12], 1)
+        print(f"  slowest batch element {slow}{'' if ws is None else f' (wsplit={ws})'}: {act} iterations "
+              f"({tm[13]} tail mode, {tm[14]} chain mode); phase cycles per iteration: "
+              + ", ".join(f"{nm}={16.0 * v / act:.0f}" for nm, v in zip(TIMERS, tm[:12])))
+        print("  phase cycles total (M): " + ", ".join(f"{nm}={16.0 * v / 1e6:.2f}" for nm, v in zip(TIMERS, tm[:12])))
     print(f"  forward (defaults): {timed(x1, x2, eps, iters, d, a, None, None):.1f} us/call")
     for h, o in sweep:
         print(f"  forward helpers={h} offload_min={o}: {timed(x1, x2, eps, iters, d, a, h, o):.1f} us/call")
@@ -88,7 +92,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--b", type=int, default=16)
     ap.add_argument("--quick", action="store_true", help="training call + config 3 only")
+    ap.add_argument("--diag-wsplit", action="store_true", help="phase timers with wsplit=4 as well")
     args = ap.parse_args()
+    global DIAG_WSPLIT
+    DIAG_WSPLIT = args.diag_wsplit
     dev = torch.device("cuda:0")
     sweep = [(0, 0), (15, 8), (15, 16), (15, 24), (15, 48), (7, 24)]
     pred, points = generator_clouds(args.b, dev)

@@ -323,10 +323,17 @@ __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const fl
 }
 
 // ---- auction full scan, exact: key = the exact bid value.  Always exact
-// bid (the lanes' top-2 hold the global top-2); T = K*.
+// bid (the lanes' top-2 hold the global top-2); T = K*.  Out of line (the
+// rare fallback), so its results come back BY VALUE: through reference
+// parameters every caller kept b1/kb/b2/T in scratch memory, a store and a
+// dependent reload on the fast path of every full scan.
+struct ScanBid {
+    float b1, b2, T;
+    int kb;
+};
 template <bool kSc1>
-__device__ __noinline__ void scan_exact(float x1, float y1, float z1, const float *Qc, const float *price, int n,
-                                        centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T) {
+__device__ __noinline__ ScanBid scan_exact_bid(float x1, float y1, float z1, const float *Qc, const float *price,
+                                               int n, centry *__restrict__ cache) {
     const int lane = threadIdx.x & 63;
     LaneTop t;
     lane_top_init(t);
@@ -341,8 +348,19 @@ __device__ __noinline__ void scan_exact(float x1, float y1, float z1, const floa
         for (int r = 0; r < 4; ++r) lane_top_push(t, key[r], k0 + 64 * r);
     }
     bool s1, s2;
-    T = select_cache<kSc1>(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cache, s1, s2);
-    wave_top2(t.a1, t.q1, t.a2, t.q2, b1, kb, b2);
+    ScanBid r;
+    r.T = select_cache<kSc1>(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cache, s1, s2);
+    wave_top2(t.a1, t.q1, t.a2, t.q2, r.b1, r.kb, r.b2);
+    return r;
+}
+template <bool kSc1>
+__device__ __forceinline__ void scan_exact(float x1, float y1, float z1, const float *Qc, const float *price, int n,
+                                           centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T) {
+    const ScanBid r = scan_exact_bid<kSc1>(x1, y1, z1, Qc, price, n, cache);
+    b1 = r.b1;
+    kb = r.kb;
+    b2 = r.b2;
+    T = r.T;
 }
 
 // ---- auction full scan, fast: selection on an fp32 approximation

@@ -1,5 +1,10 @@
+# same-box A/B of EMD builds (tools/ab_emd.py): lib/libpcm_hip_base.so (the
+# committed source, built by hand) against the in-tree build, plus any
+# lib/libpcm_hip_v*.so variants, alternating
 L=$PWD/3d-pointcloudreconstruction_amd/lib
 for r in 1 2; do
-  PCM_HIP_LIB=$L/libpcm_hip_base.so timeout -k 10 120 python -u tools/ab_emd.py || exit 1
-  PCM_HIP_LIB=$L/libpcm_hip.so timeout -k 10 120 python -u tools/ab_emd.py || exit 1
+  for lib in $L/libpcm_hip_base.so $L/libpcm_hip_v*.so $L/libpcm_hip.so; do
+    [ -f "$lib" ] || continue
+    PCM_HIP_LIB=$lib timeout -k 10 120 python -u tools/ab_emd.py || exit 1
+  done
 done

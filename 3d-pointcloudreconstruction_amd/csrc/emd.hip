@@ -61,8 +61,9 @@
 
 namespace {
 
-constexpr int kL = 32;               // cache slots per point (unused slots: id -1)
+constexpr int kL = 64;               // cache slots per point (unused slots: id -1)
 constexpr int kSelectSteps = 8;      // bisection steps when > kL entries clear K3
+constexpr int kSectionSteps = 4;     // quarter-section steps of the reserve thresholds (1/256 of the range)
 constexpr int kSeedThreads = 256;    // 4 waves
 constexpr int kSeedPtsPerWave = 4;   // 16 points per seed workgroup
 constexpr int kSeedPts = kSeedThreads / 64 * kSeedPtsPerWave;
@@ -78,6 +79,15 @@ constexpr int kStagePN = 1024;          // the n of the LDS-state, staged-bidder
 constexpr int kDefaultOffloadMin = 24;  // misses above which an iteration is offloaded
 constexpr int kDefaultTailMax = 16;     // bidders at or below which an iteration runs in tail mode
 constexpr int kDefaultWsplit = 1;       // most waves one miss's scan is split over (2, 4: measured slower at config 3 and the training call)
+// Reserve (n == kStagePN): every object closer than a radius, built by the
+// seed at zero prices, up to kR entries of {object id, d}.  Radius^2 starts at
+// kResGrow x the cache bound's d (about 4^1.5 = 8x the cache's objects in a
+// locally uniform cloud) and shrinks by kResShrink until kR fit.  The
+// workspace keeps only the 16-bit object ids (n = 1024): the reserve bid
+// recomputes d from the LDS-staged clouds, the same pinned arithmetic.
+constexpr int kR = 256;
+constexpr float kResGrow = 6.f, kResShrink = 0.85f;
+constexpr int kResTries = 16;           // 6 * 0.85^11 < 1: the radius reaches dK (<= 128 objects inside)
 
 typedef unsigned long long centry;   // low 32 bits: object id (-1 unused), high 32: s bits
 typedef unsigned long long ckey;     // claim key: (~it) << 32 | point
@@ -322,6 +332,240 @@ __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const fl
               s2 ? value_of(d2, 0.f) : -PCM_INF, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
 }
 
+// ---- seed at n = kStagePN, one wave per point, the 16 squared distances per
+// lane kept in registers.
+//  1. dK = min over lanes of the lane's 3rd smallest d: every lane holds at
+//     most 2 objects closer than dK (<= 128 in all).
+//  2. RESERVE: every object with d < th, th starting at kResGrow * dK and
+//     shrinking towards dK until at most kR qualify.  Every other object has
+//     d >= th, so at ANY prices (p >= 0, only rising) its value is <=
+//     rT = value_of(th, 0): the cache's proof against a bound ~8x further out.
+//     Entries {id, d bits} go to R (global) and to this wave's LDS slot sR.
+//  3. CACHE: the exact nearest kL of the reserve (threshold K on d by
+//     bisection over the compacted entries, two per lane), bound
+//     T = value_of(K, 0); the iteration-0 bid is their top two.
+// rn = 0: no reserve (degenerate or non-finite cloud; the cache is then the
+// lane-top form of scan_seed).
+__device__ __forceinline__ float wave_min(float v) { return -wave_max(-v); }
+
+__device__ __forceinline__ void scan_seed_res(float x1, float y1, float z1, const float *Qc, centry *__restrict__ cache,
+                                              uint16_t *__restrict__ R, centry *sR, float &b1, int &kb, float &b2,
+                                              float &T, int &rn, float &rT) {
+    constexpr int n = kStagePN, S = n / 256;
+    const int lane = threadIdx.x & 63;
+    float dd[4 * S];
+    float m1 = PCM_INF, m2 = PCM_INF, m3 = PCM_INF;  // the lane's 3 smallest d
+#pragma unroll
+    for (int i = 0; i < 4 * S; ++i) {
+        dd[i] = sqd_to(x1, y1, z1, Qc + 3 * (size_t)(lane + 256 * (i / 4) + 64 * (i % 4)));
+        m3 = __builtin_amdgcn_fmed3f(m2, m3, dd[i]);
+        m2 = __builtin_amdgcn_fmed3f(m1, m2, dd[i]);
+        m1 = fminf(m1, dd[i]);
+    }
+    const float dK = wave_min(m3);
+    rn = 0;
+    rT = PCM_INF;
+    float th = kResGrow * dK;
+    int cnt = 0;
+    const bool ok = dK > 0.f && dK < PCM_INF;
+    if (ok) {
+#pragma unroll 1
+        for (int tr = 0; tr < kResTries; ++tr) {
+            cnt = 0;
+#pragma unroll
+            for (int i = 0; i < 4 * S; ++i) cnt += __popcll(__ballot(dd[i] < th));
+            if (cnt <= kR) break;
+            th = fmaxf(dK, kResShrink * th);
+        }
+    }
+    if (!ok || cnt > kR) {  // no reserve: the lane-top cache of scan_seed
+        scan_seed(x1, y1, z1, Qc, n, cache, b1, kb, b2, T);
+        return;
+    }
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int pos = 0;
+#pragma unroll
+    for (int i = 0; i < 4 * S; ++i) {
+        const bool in = dd[i] < th;
+        const unsigned long long m = __ballot(in);
+        if (in) {
+            const centry e = cpack(lane + 256 * (i / 4) + 64 * (i % 4), dd[i]);
+            R[pos + __popcll(m & below)] = (uint16_t)(lane + 256 * (i / 4) + 64 * (i % 4));
+            sR[pos + __popcll(m & below)] = e;
+        }
+        pos += __popcll(m);
+    }
+    rn = cnt;
+    rT = value_of(th, 0.f);
+    // sR is written by this wave's lanes and read across them: a wave's LDS
+    // accesses complete in order; the asm keeps the compiler from moving the
+    // reads above the writes
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    constexpr int RPL = kR / 64;
+    float d[RPL];
+    int k[RPL];
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        const bool h = lane + 64 * i < rn;
+        const centry e = sR[lane + 64 * i];
+        d[i] = h ? __uint_as_float((unsigned)(e >> 32)) : PCM_INF;
+        k[i] = (int)(unsigned)e;
+    }
+    auto count_below = [&](float t) {
+        int c = 0;
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) c += __popcll(__ballot(d[i] < t));
+        return c;
+    };
+    float K = th;  // rn <= kL: the whole reserve
+    if (rn > kL) {
+        // invariant: count(d < lo) <= kL < count(d < hi); quarter sections
+        // (three independent counts per step: a quarter of the dependent
+        // VALU -> SALU round trips of halving)
+        float lo = 0.f, hi = th;
+#pragma unroll 1
+        for (int step = 0; step < kSectionSteps; ++step) {
+            const float w = 0.25f * (hi - lo);
+            const float t1 = lo + w, t2 = lo + 2.f * w, t3 = lo + 3.f * w;
+            const int c1 = count_below(t1), c2 = count_below(t2), c3 = count_below(t3);
+            if (c3 <= kL) lo = t3;
+            else if (c2 <= kL) { lo = t2; hi = t3; }
+            else if (c1 <= kL) { lo = t1; hi = t2; }
+            else hi = t1;
+        }
+        K = lo;
+    }
+    float lmax = -PCM_INF;
+    float v[RPL];
+    int cpos = 0;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        const bool c = d[i] < K;
+        const unsigned long long m = __ballot(c);
+        if (c) cache[cpos + __popcll(m & below)] = cpack(k[i], __builtin_sqrtf(d[i]));
+        cpos += __popcll(m);
+        v[i] = c ? value_of(d[i], 0.f) : -PCM_INF;
+        lmax = fmaxf(lmax, v[i]);
+    }
+    if (lane < kL && lane >= cpos) cache[lane] = cpack(-1, 0.f);
+    T = value_of(K, 0.f);
+    b1 = wave_max(lmax);
+    int lk = 0x7fffffff, lc = 0;
+    float lrest = -PCM_INF;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        const bool eq = v[i] == b1;
+        lk = eq ? min(lk, k[i]) : lk;
+        lc += __popcll(__ballot(eq));
+        lrest = eq ? lrest : fmaxf(lrest, v[i]);
+    }
+    kb = wave_min_i(lk);
+    b2 = lc >= 2 ? b1 : wave_max(lrest);
+}
+
+
+// ---- reserve bid (one wave): the exact top-2 over the rn reserve entries at
+// current prices, proven when its second best exceeds rT.  Then the cache is
+// rebuilt from the reserve: the <= kL largest values (threshold K by bisection
+// as in select_cache), bound T = max(rT, K).  Returns false when not proven.
+// Results by value; the master runs it in a loop of its own (B2a), apart
+// from the full scans (B2b): inlined into the same loop body it pushed the
+// kernel past 128 VGPRs into scratch.
+typedef const __attribute__((address_space(3))) float *lds_cfp;
+struct ResBid {
+    float b1, b2, T;
+    int kb, ok;
+};
+template <typename Stamp>
+__device__ __forceinline__ ResBid reserve_bid(const uint16_t *__restrict__ R, int rn, float rT, lds_cfp price,
+                                           float x1, float y1, float z1, const float *Qc, centry *__restrict__ cache,
+                                           Stamp stamp) {
+    constexpr int RPL = kR / 64;  // reserve entries per lane: lane + 64 i
+    const int lane = threadIdx.x & 63;
+    ResBid r;
+    r.ok = 0;
+    r.T = PCM_INF;
+    bool h[RPL];
+    int k[RPL];
+    float sv[RPL], v[RPL];
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        h[i] = lane + 64 * i < rn;
+        k[i] = h[i] ? (int)R[lane + 64 * i] : 0;
+    }
+    unsigned dep = 0;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        sv[i] = __builtin_sqrtf(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k[i]));  // as the seed's d, pinned order
+        dep += (unsigned)k[i];
+    }
+    stamp(6, dep);
+    float lmax = -PCM_INF, lmin = PCM_INF;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        v[i] = h[i] ? value_from_s(sv[i], price[k[i]]) : -PCM_INF;
+        lmax = fmaxf(lmax, v[i]);
+        lmin = h[i] ? fminf(lmin, v[i]) : lmin;
+    }
+    // exact top-2 (lowest id at the best; better = best on a tie)
+    const float b1 = wave_max(lmax);
+    int lk = 0x7fffffff, lc = 0;
+    float lrest = -PCM_INF;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        const bool eq = v[i] == b1;
+        lk = eq ? min(lk, k[i]) : lk;
+        lc += __popcll(__ballot(eq));
+        lrest = eq ? lrest : fmaxf(lrest, v[i]);
+    }
+    r.b1 = b1;
+    r.kb = wave_min_i(lk);
+    r.b2 = lc >= 2 ? b1 : wave_max(lrest);
+    stamp(7, 0u);
+    if (!(r.b2 > rT)) return r;
+    auto count_above = [&](float t) {
+        int c = 0;
+#pragma unroll
+        for (int i = 0; i < RPL; ++i) c += __popcll(__ballot(v[i] > t));
+        return c;
+    };
+    float K = -PCM_INF;
+    if (rn > kL) {
+        float lo = wave_min(lmin);
+        if (count_above(lo) <= kL) {
+            K = lo;  // ties at the minimum: everything above it fits
+        } else {
+            // invariant: count(> lo) > kL >= count(> hi); quarter sections
+            float hi = b1;
+#pragma unroll 1
+            for (int step = 0; step < kSectionSteps; ++step) {
+                const float w = 0.25f * (hi - lo);
+                const float t1 = lo + w, t2 = lo + 2.f * w, t3 = lo + 3.f * w;
+                const int c1 = count_above(t1), c2 = count_above(t2), c3 = count_above(t3);
+                if (c1 <= kL) hi = t1;
+                else if (c2 <= kL) { lo = t1; hi = t2; }
+                else if (c3 <= kL) { lo = t2; hi = t3; }
+                else lo = t3;
+            }
+            K = hi;
+        }
+    }
+    stamp(11, 0u);
+    const unsigned long long below = (1ull << lane) - 1ull;
+    int pos = 0;
+#pragma unroll
+    for (int i = 0; i < RPL; ++i) {
+        const bool c = v[i] > K;
+        const unsigned long long m = __ballot(c);
+        if (c) cache[pos + __popcll(m & below)] = cpack(k[i], sv[i]);
+        pos += __popcll(m);
+    }
+    if (lane < kL && lane >= pos) cache[lane] = cpack(-1, 0.f);
+    r.T = fmaxf(rT, K);
+    r.ok = 1;
+    return r;
+}
+
 // ---- auction full scan, exact: key = the exact bid value.  Always exact
 // bid (the lanes' top-2 hold the global top-2); T = K*.  Out of line (the
 // rare fallback), so its results come back BY VALUE: through reference
@@ -461,6 +705,10 @@ struct EmdWs {
     int32_t *rbid;   // [b*n] job results
     float *rinc;     // [b*n]
     float *pp;       // [b*n] job: price snapshot
+    // reserve (n == kStagePN only, else null): seed-written, read by the master
+    uint16_t *res;   // [b*n*kR] object ids
+    float *RT;       // [b*n] reserve bound
+    int32_t *RN;     // [b*n] reserve entries (0: none)
     // master state in global memory (n > kLdsStateMaxN), per batch element n words each
     int32_t *g_ass, *g_inv, *g_max, *g_bid, *g_u0, *g_u1, *g_miss;
     float *g_price, *g_inc;
@@ -473,7 +721,7 @@ constexpr unsigned kInB = 0x7fc0b00bu;  // a quiet NaN no bound ever equals
 // 1. seed kernel: iteration-0 bids + caches, one wave per point, 16 points
 //    per workgroup, the target cloud staged in LDS (kStage)
 // ===========================================================================
-template <bool kStage>
+template <bool kStage, bool kRes>
 __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__restrict__ xyz1,
                                                                 const float *__restrict__ xyz2, int b, int n,
                                                                 float eps, EmdWs ws) {
@@ -507,7 +755,19 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__r
         const size_t pt = (size_t)batch * n + j;
         float b1, b2, T;
         int kb;
-        scan_seed(Pg[3 * j], Pg[3 * j + 1], Pg[3 * j + 2], Qc, n, ws.cache + pt * kL, b1, kb, b2, T);
+        if constexpr (kRes) {  // n == kStagePN (launch_emd)
+            int rn;
+            float rT;
+            centry *sR = reinterpret_cast<centry *>(sQs + 3 * kStagePN) + wave * kR;  // this wave's reserve copy
+            scan_seed_res(Pg[3 * j], Pg[3 * j + 1], Pg[3 * j + 2], Qc, ws.cache + pt * kL, ws.res + pt * kR, sR, b1,
+                          kb, b2, T, rn, rT);
+            if (lane == 0) {
+                ws.RN[pt] = rn;
+                ws.RT[pt] = rT;
+            }
+        } else {
+            scan_seed(Pg[3 * j], Pg[3 * j + 1], Pg[3 * j + 2], Qc, n, ws.cache + pt * kL, b1, kb, b2, T);
+        }
         if (lane == 0) {
             ws.CT[pt] = T;
             const bool proven = b2 > T && (unsigned)kb < (unsigned)n;
@@ -565,10 +825,14 @@ __device__ __forceinline__ void bid_on(const AState<kG> &st, int j, int k, float
     if (atomicMax(&st.mx[k], f2key(inc)) > 0) *coll = 1;
 }
 
+// resT/resN (reserve form, else null): a miss whose cache bound is not above
+// its reserve bound cannot be bid from the reserve (every value outside the
+// cache is <= the bound, so the reserve's second best is too): its reserve
+// is retired here and the miss goes straight to the full scan.
 template <int G, bool kG>
 __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, const centry *C, const float *CT,
                                            const centry *CB, const float *CTB, const AState<kG> &st, int *sNm,
-                                           int *coll) {
+                                           int *coll, const float *resT, int *resN) {
     static_assert(G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
     constexpr int E = kL / G;
     const int gi = threadIdx.x / G, gl = threadIdx.x % G;
@@ -624,6 +888,7 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
                 bid_on(st, j, kb, b1 - b2 + eps, coll);
             } else {
                 st.miss[atomicAdd(sNm, 1)] = j;
+                if (resN && !(tj > resT[j])) resN[j] = 0;
             }
         }
     }
@@ -767,6 +1032,12 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     // lane tops of the split scans: 5 words x 64 lanes x 16 waves
     float *xA1 = (float *)lp, *xA2 = xA1 + kEmdThreads, *xA3 = xA2 + kEmdThreads;
     int *xQ1 = (int *)(xA3 + kEmdThreads), *xQ2 = xQ1 + kEmdThreads;
+    // reserve form (n == kStagePN, LDS state): bounds and entry counts of the
+    // seed's reserves; a point's count drops to 0 once its reserve fails a proof
+    constexpr bool kRes = !kG && kN == kStagePN;
+    float *sRT = (float *)(xQ2 + kEmdThreads);  // [n] (kRes)
+    int *sRN = (int *)(sRT + n);                // [n] (kRes)
+    const bool res_on = eps >= 0.f;             // prices never fall: the reserve bounds hold
 
     if constexpr (kStage) pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kWaves);
     if constexpr (kStageP) pcm_dma_to_lds(sP, Pg, 12 * n, wave, kWaves);
@@ -780,6 +1051,10 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         st.mx[j] = f2key(0.f);  // emd_module.py:49 zero-inits max_increments
         st.claim[j] = ~0ull;
         st.U0[j] = j;           // iteration 0: every point bids
+        if constexpr (kRes) {
+            sRT[j] = ws.RT[base + j];
+            sRN[j] = res_on ? ws.RN[base + j] : 0;
+        }
     }
     if (tid == 0) { sNu[0] = n; sNu[1] = 0; sNm = 0; sColl = 0; }
     vm_drain();  // the DMA has landed
@@ -803,11 +1078,49 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     // the master's own full scan of point j: cache region A, bid placed
     // (profiling build: wave 0's key scan, proof and exact fallback timed
     // in slots 6, 7, 11 and the exact fallbacks counted)
+    // the reserve bid of miss q (kRes): two entries per lane instead of n / 64
+    // objects; on success the miss entry is cleared (-1) so B2b skips it
+    auto own_reserve = [&](int q) {
+        const int j = st.miss[q];
+        const int rn = __builtin_amdgcn_readfirstlane(sRN[j]);
+        if (rn <= 0) return;
+#ifdef PCM_STAMPS
+        PCM_EMD_PHASE(5);  // profiling build: B1 end -> wave 0's first reserve bid (slot 5), the bid (slot 4)
+#endif
+#ifdef PCM_STAMPS
+        // slots 6 (entries loaded), 7 (values + top-2), 11 (cache threshold)
+        auto stamp = [&](int i, unsigned dep) {
+            if (timers) {
+                asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(dep) : "memory");
+                const unsigned long long tn = __builtin_amdgcn_s_memtime();
+                sTm[i] += tn - sTm[12];
+                sTm[12] = tn;
+            }
+        };
+#else
+        auto stamp = [](int, unsigned) {};
+#endif
+        const ResBid rb = reserve_bid(ws.res + (base + j) * kR, rn, sRT[j], (lds_cfp)st.price, P[3 * j],
+                                      P[3 * j + 1], P[3 * j + 2], Qc, C + (size_t)j * kL, stamp);
+#ifdef PCM_STAMPS
+        PCM_EMD_PHASE(4);
+#endif
+        if (lane == 0) {
+            if (rb.ok) {
+                CT[j] = rb.T;
+                place_bid(st, j, rb.kb, rb.b1 - rb.b2 + eps, n, &sColl);
+                st.miss[q] = -1;
+                if (hist) atomicAdd(&a.stats[2 * iters + 13], 1);  // reserve bids
+            } else {
+                sRN[j] = 0;  // exhausted: j's later misses scan directly
+            }
+        }
+    };
     auto own_scan = [&](int j) {
         float b1, b2, T;
         int kb;
-        const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
         centry *cj = C + (size_t)j * kL;
+        const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
 #ifdef PCM_STAMPS
         LaneTop t;
         lane_top_init(t);
@@ -956,9 +1269,11 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             const centry *CB = ws.cacheB + base * kL;
             const float *CTB = ws.CTB + base;
             const int G = cache_bid_lanes(nu);
-            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl);
-            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl);
-            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl);
+            const float *rT = kRes ? sRT : nullptr;
+            int *rN = kRes ? sRN : nullptr;
+            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN);
+            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN);
+            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN);
         }
         __syncthreads();
         PCM_EMD_PHASE(0);
@@ -1013,7 +1328,17 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 // lane tops are merged in object order), one wave per miss else
                 const int W = (nm <= 4 && a.wmax >= 4) ? 4 : ((nm <= 8 && a.wmax >= 2) ? 2 : 1);
                 if (W == 1) {
-                    for (int q = wave; q < nm; q += kWaves) own_scan(st.miss[q]);
+                    if constexpr (kRes) {
+                        // B2a: reserve bids; B2b: full scans of the rest (the
+                        // same wave's misses: no barrier between the two)
+                        for (int q = wave; q < nm; q += kWaves) own_reserve(q);
+                        for (int q = wave; q < nm; q += kWaves) {
+                            const int j = __builtin_amdgcn_readfirstlane(st.miss[q]);
+                            if (j >= 0) own_scan(j);
+                        }
+                    } else {
+                        for (int q = wave; q < nm; q += kWaves) own_scan(st.miss[q]);
+                    }
                 } else {
                     const int q = wave / W, r = wave - q * W;
                     const bool act = q < nm;
@@ -1208,6 +1533,11 @@ size_t ws_layout(int b, int n, EmdWs *w, char *basep) {
     t.rbid = (int32_t *)take(pts * 4);
     t.rinc = (float *)take(pts * 4);
     t.pp = (float *)take(pts * 4);
+    if (n == kStagePN) {
+        t.res = (uint16_t *)take(pts * kR * sizeof(uint16_t));
+        t.RT = (float *)take(pts * 4);
+        t.RN = (int32_t *)take(pts * 4);
+    }
     if (n > kLdsStateMaxN) {
         t.g_ass = (int32_t *)take(pts * 4);
         t.g_inv = (int32_t *)take(pts * 4);
@@ -1254,17 +1584,21 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     // seed
     const bool seed_stage = n <= kStageMaxN;
     const unsigned seed_blocks = (unsigned)((size_t)b * n / kSeedPts);
-    const size_t seed_lds = seed_stage ? 12 * (size_t)n : 0;
+    const size_t seed_lds = seed_stage ? 12 * (size_t)n + (n == kStagePN ? kSeedThreads / 64 * kR * 8 : 0) : 0;
     if (seed_stage) {
         if (seed_lds > 64 * 1024 &&
-            hipFuncSetAttribute((const void *)emd_seed_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)seed_lds) != hipSuccess)
+            hipFuncSetAttribute((const void *)emd_seed_kernel<true, false>,  // n > 5461: not the reserve form
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)seed_lds) != hipSuccess)
             return PCM_ERR_LAUNCH;
-        hipLaunchKernelGGL(emd_seed_kernel<true>, dim3(seed_blocks), dim3(kSeedThreads), seed_lds, s, xyz1, xyz2,
-                           b, n, eps, ws);
+        if (n == kStagePN)
+            hipLaunchKernelGGL((emd_seed_kernel<true, true>), dim3(seed_blocks), dim3(kSeedThreads), seed_lds, s,
+                               xyz1, xyz2, b, n, eps, ws);
+        else
+            hipLaunchKernelGGL((emd_seed_kernel<true, false>), dim3(seed_blocks), dim3(kSeedThreads), seed_lds, s,
+                               xyz1, xyz2, b, n, eps, ws);
     } else {
-        hipLaunchKernelGGL(emd_seed_kernel<false>, dim3(seed_blocks), dim3(kSeedThreads), 0, s, xyz1, xyz2, b, n,
-                           eps, ws);
+        hipLaunchKernelGGL((emd_seed_kernel<false, false>), dim3(seed_blocks), dim3(kSeedThreads), 0, s, xyz1, xyz2,
+                           b, n, eps, ws);
     }
 
     // auction
@@ -1275,8 +1609,9 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     const bool stage = n <= (g_state ? kStageMaxN : kLdsStateMaxN);
     const size_t xchg = 5 * (size_t)kEmdThreads * 4;
     const bool stage_p = n <= (g_state ? 4096 : kStagePN);  // !g_state: n == kStagePN exactly
+    const bool res = !g_state && stage_p;  // n == kStagePN: the reserve form (bounds + counts in LDS)
     const size_t m_lds = (g_state ? 0 : 44 * (size_t)n) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
-                         xchg;
+                         xchg + (res ? 8 * (size_t)n : 0);
     const size_t h_lds = H > 0 ? (stage ? 12 * (size_t)n : 0) + 4 * (size_t)n : 0;
     size_t lds = m_lds > h_lds ? m_lds : h_lds;
     // one workgroup per CU when helpers run: a master never shares its SIMDs
@@ -1315,7 +1650,8 @@ extern "C" int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int 
 // Tuning / diagnostics entry.  helpers, offload_min < 0: the defaults.
 // stats (caller zero-fills 3*iters + 16 + b int32) with diag 1: stats[2*it] +=
 // unassigned points, stats[2*it+1] += full scans (summed over the batch),
-// stats[2*iters + 10/11/12] = jobs / offloaded items / helper wake-ups; with
+// stats[2*iters + 10/11/12] = jobs / offloaded items / helper wake-ups,
+// stats[2*iters + 13] = misses bid from the reserve (no full scan); with
 // diag 2: stats[2*iters + 0..7] = batch-0 phase cycles / 16 (bids, full scans,
 // claim, assign; sub-phases 4..7), stats[2*iters + 8] = iterations with
 // bidders.  Both: stats[3*iters + 16 + i] = auction wall time of batch

@@ -108,6 +108,46 @@ def test_emd_helper_configs_match_oracle(cuda, oracle, helpers, offload_min, tai
         assert st[2 * 400 + 10] == 0
 
 
+def _reserve_cases():
+    a, c = _clouds(30, 16, 1024)
+    yield "config3", a, c, 0.005, 50
+    # duplicated targets (exact value ties inside the reserve) and a collapsed
+    # bidder cluster (every reserve drains): ties and exhausted reserves
+    g = torch.Generator().manual_seed(31)
+    a = torch.rand(4, 1024, 3, generator=g)
+    c = torch.rand(4, 1024, 3, generator=g)
+    c[:, 512:] = c[:, :512]
+    yield "dup_targets", a, c, 0.005, 200
+    a = (0.5 + 1e-3 * torch.randn(4, 1024, 3, generator=g)).contiguous()
+    yield "collapsed", a, torch.rand(4, 1024, 3, generator=g), 0.01, 300
+    a = torch.full((2, 1024, 3), 0.25)  # every bidder identical: K* ties
+    yield "identical", a, torch.rand(2, 1024, 3, generator=g), 0.005, 100
+
+
+@pytest.mark.parametrize("case", ["config3", "dup_targets", "collapsed", "identical"])
+def test_emd_reserve_bids_match_oracle(cuda, oracle, case):
+    # n = 1024: misses of the cache are first bid from the seed's reserve
+    # (csrc/emd.hip reserve_bid); the result must equal the full-scan auction
+    import pcm_hip
+    name, a, c, eps, iters = next(x for x in _reserve_cases() if x[0] == case)
+    b, n, _ = a.shape
+    x1, x2 = a.to(cuda).contiguous(), c.to(cuda).contiguous()
+    dist = torch.empty(b, n, device=cuda)
+    ass = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    price = torch.empty(b, n, device=cuda)
+    stats = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=cuda)
+    pcm_hip.emd_forward(x1, x2, eps, iters, dist, ass, price, stats=stats)
+    torch.cuda.synchronize()
+    rd, ra, rp, _ = oracle.emd_forward(a.numpy(), c.numpy(), eps, iters, with_stats=True)
+    np.testing.assert_array_equal(ass.cpu().numpy(), ra)
+    np.testing.assert_array_equal(dist.cpu().numpy().view(np.int32), rd.view(np.int32))
+    np.testing.assert_array_equal(price.cpu().numpy().view(np.int32), rp.view(np.int32))
+    st = stats.cpu().numpy()
+    if name == "config3":
+        misses = int(st[1:2 * iters:2].sum())
+        assert st[2 * iters + 13] > 0.8 * misses, (st[2 * iters + 13], misses)
+
+
 def test_emd_generator_like_training_call(cuda, oracle):
     # loss/loss.py:23 setting on clustered predictions (the 13 ms case of round 1)
     a, c = _generator_like(21, 16, 1024)

@@ -835,6 +835,7 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
                                            int *coll, const float *resT, int *resN) {
     static_assert(G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
     constexpr int E = kL / G;
+    static_assert(E % 2 == 0, "slot pairs");
     const int gi = threadIdx.x / G, gl = threadIdx.x % G;
     for (int u0 = 0; u0 < nu; u0 += kEmdThreads / G) {
         const int u = u0 + gi;
@@ -845,12 +846,22 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
         // re-read from region B (sc1)
         float tj = CT[j];
         centry ce[E];
+        // lane gl evaluates the slot pairs 2 (gl + G e') + {0, 1}: one 16-byte
+        // load per pair (any partition of the kL slots over the group works)
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-        for (int e = 0; e < E; ++e) ce[e] = C[(size_t)j * kL + gl + G * e];
+        for (int e = 0; e < E / 2; ++e) {
+            const u64x2 w = *reinterpret_cast<const u64x2 *>(C + (size_t)j * kL + 2 * (gl + G * e));
+            ce[2 * e] = w.x;
+            ce[2 * e + 1] = w.y;
+        }
         if (__float_as_uint(tj) == kInB) {
             tj = ld_sc1(CTB + j);
 #pragma unroll
-            for (int e = 0; e < E; ++e) ce[e] = ld_sc1(CB + (size_t)j * kL + gl + G * e);
+            for (int e = 0; e < E / 2; ++e) {
+                ce[2 * e] = ld_sc1(CB + (size_t)j * kL + 2 * (gl + G * e));
+                ce[2 * e + 1] = ld_sc1(CB + (size_t)j * kL + 2 * (gl + G * e) + 1);
+            }
         }
         // values at current prices; an unused slot (k = -1) evaluates object
         // 0 and is then forced to (-inf, INT_MAX), branch-free

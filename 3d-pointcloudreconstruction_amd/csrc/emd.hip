@@ -743,13 +743,20 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__r
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const float *Pg = xyz1 + (size_t)batch * n * 3;
     const float *Qg = xyz2 + (size_t)batch * n * 3;
+    // this wave's query points, loaded (scalar) while the target cloud lands
+    const int j0 = chunk * kSeedPts + __builtin_amdgcn_readfirstlane(wave) * kSeedPtsPerWave;
+    float qp[kSeedPtsPerWave][3];
+#pragma unroll
+    for (int p = 0; p < kSeedPtsPerWave; ++p)
+#pragma unroll
+        for (int c = 0; c < 3; ++c) qp[p][c] = Pg[3 * (j0 + p) + c];
     if constexpr (kStage) {
         pcm_dma_to_lds(sQs, Qg, 12 * n, wave, kSeedThreads / 64);
         vm_drain();
         __syncthreads();
     }
     const float *Qc = kStage ? (const float *)sQs : Qg;
-    const int j0 = chunk * kSeedPts + wave * kSeedPtsPerWave;
+#pragma unroll
     for (int p = 0; p < kSeedPtsPerWave; ++p) {
         const int j = j0 + p;
         const size_t pt = (size_t)batch * n + j;
@@ -759,14 +766,14 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__r
             int rn;
             float rT;
             centry *sR = reinterpret_cast<centry *>(sQs + 3 * kStagePN) + wave * kR;  // this wave's reserve copy
-            scan_seed_res(Pg[3 * j], Pg[3 * j + 1], Pg[3 * j + 2], Qc, ws.cache + pt * kL, ws.res + pt * kR, sR, b1,
-                          kb, b2, T, rn, rT);
+            scan_seed_res(qp[p][0], qp[p][1], qp[p][2], Qc, ws.cache + pt * kL, ws.res + pt * kR, sR, b1, kb, b2,
+                          T, rn, rT);
             if (lane == 0) {
                 ws.RN[pt] = rn;
                 ws.RT[pt] = rT;
             }
         } else {
-            scan_seed(Pg[3 * j], Pg[3 * j + 1], Pg[3 * j + 2], Qc, n, ws.cache + pt * kL, b1, kb, b2, T);
+            scan_seed(qp[p][0], qp[p][1], qp[p][2], Qc, n, ws.cache + pt * kL, b1, kb, b2, T);
         }
         if (lane == 0) {
             ws.CT[pt] = T;

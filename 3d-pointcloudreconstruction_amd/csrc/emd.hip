@@ -65,7 +65,7 @@ constexpr int kL = 64;               // cache slots per point (unused slots: id 
 constexpr int kSelectSteps = 8;      // bisection steps when > kL entries clear K3
 constexpr int kSectionSteps = 4;     // quarter-section steps of the reserve thresholds (1/256 of the range)
 constexpr int kSeedThreads = 256;    // 4 waves
-constexpr int kSeedPtsPerWave = 2;   // 8 points per seed workgroup (4: 1.7 us slower seed at config 3, 8: 10 us)
+constexpr int kSeedPtsPerWave = 1;   // 4 points per seed workgroup (2: seed 2.2 us slower at config 3, 4: 3.9 us, 8: 15 us)
 constexpr int kSeedPts = kSeedThreads / 64 * kSeedPtsPerWave;
 constexpr int kEmdThreads = 1024;    // auction workgroup (16 waves)
 constexpr int kWaves = kEmdThreads / 64;

@@ -1188,6 +1188,14 @@ extern "C" int pcm_chamfer_workspace_status(const void *workspace, size_t worksp
     return (words[0] || words[1]) ? PCM_ERR_LAUNCH : PCM_OK;
 }
 
+// byte offsets in the workspace of the two sticky error words read above
+// (which = 0: the fused-loss forward's, 1: the one-launch step's), for the
+// Python wrappers' asynchronous copy (metric/pcm_hip.py _StickyWatch)
+extern "C" size_t pcm_tune_chamfer_err_offset(int which, int b, int n, int m) {
+    return which == 0 ? 4 * (size_t)pcm_loss::kErrWord
+                      : pcm_chamfer_loss_ws_offset(b, n, m) + 4 * (size_t)pcm_chamfer_grad_err_word();
+}
+
 extern "C" int pcm_chamfer_forward(const float *xyz1, const float *xyz2, int b, int n, int m,
                                    float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                    void *stream) {

@@ -1160,6 +1160,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
 // Fused loss + gradient
 // ---------------------------------------------------------------------------
 constexpr int kGradCap = 1024;   // points per cloud the per-element backward holds in LDS
+// Bound of a gradient-phase wait on the other workgroups' argmins (polls of
+// about a microsecond each): past it the workgroup computes what is missing
+// itself.  The loss poll (pcm_loss::kPollMaxSpins) waits longer: its
+// producers finish within this bound plus their local scans.
+constexpr unsigned kGradWaitSpins = 1u << 16;
 constexpr int kGradSlots = 8;    // inverse-index entries per target kept in LDS (more: ordered rescan)
 // arena of the per-element backward: both clouds (AoS floats), a count per
 // point, kGradSlots 16-bit source ids per point
@@ -1253,7 +1258,8 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                                            unsigned char *scratch,
                                            const unsigned long long *__restrict__ Gown = nullptr,
                                            const unsigned long long *__restrict__ Goth = nullptr,
-                                           unsigned long long tag = 0, unsigned max_spins = 0) {
+                                           unsigned long long tag = 0, unsigned max_spins = 0,
+                                           unsigned *slow = nullptr) {
     constexpr int kPerS = (kGradCap + NT - 1) / NT;  // sources per thread
     constexpr int NW = NT / 64;
     __shared__ int sOvf[QW];   // overflowed targets (range slot)
@@ -1286,7 +1292,33 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
             for (int r = 0; r < kPerS; ++r) ready &= (unsigned)(gr[r] >> 32) == want;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (and the caller's LDS-DMA has landed)
             if (!__syncthreads_or(ready ? 0 : 1)) break;
-            if (spins >= max_spins) return false;  // uniform: every thread saw the same vote
+            if (spins >= max_spins) {
+                // uniform (every thread saw the same vote): the workgroups
+                // that owe these argmins are not running yet (not resident,
+                // or slow).  Every argmin still missing is computed here by
+                // the reference-exact scan over the LDS-resident clouds --
+                // the value the forward publishes -- so a timeout costs time,
+                // never correctness.  max_spins == 0 (tests) recomputes all.
+                const bool all = max_spins == 0u;
+                if (own && (all || (unsigned)(go >> 32) != want)) {
+                    float d;
+                    int k;
+                    pcm_ref_nn_scan(S[3 * jt], S[3 * jt + 1], S[3 * jt + 2], A, na, d, k);
+                    go = tag | (unsigned)k;
+                }
+#pragma unroll
+                for (int r = 0; r < kPerS; ++r) {
+                    const int i = min(tid + r * NT, na - 1);
+                    if (all || (unsigned)(gr[r] >> 32) != want) {
+                        float d;
+                        int k;
+                        pcm_ref_nn_scan(A[3 * i], A[3 * i + 1], A[3 * i + 2], S, nq, d, k);
+                        gr[r] = tag | (unsigned)k;
+                    }
+                }
+                if (tid == 0) atomicAdd(slow, 1u);  // diagnostics (pcm_tune_chamfer_slow_paths)
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
             if (own && (unsigned)(go >> 32) != want)
                 go = __hip_atomic_load(Gown + jt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1414,7 +1446,8 @@ struct GradWs {
     unsigned long long *wg;  // granule hand-off: per-workgroup {tag, loss partial}
     unsigned long long *ig;  // granule hand-off: per-point {tag, argmin}, cloud 1 [b n] then cloud 2 [b m]
 };
-constexpr int kGradErrWord = 4;  // word of the first line: non-zero after a timed-out wait (sticky)
+constexpr int kGradErrWord = 4;   // word of the first line: non-zero after the loss poll timed out (sticky)
+constexpr int kGradSlowWord = 5;  // diagnostics: gradient-phase waits that timed out and computed locally
 // each batch element's arrival and departure counters on 128-byte lines of
 // their own: with all of them in one line, the 8 adds and the polls per
 // element queue behind every other element's at the memory side
@@ -1526,7 +1559,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
     float *__restrict__ mean_out, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
-    GradWs ws, unsigned max_spins) {
+    GradWs ws, unsigned max_spins, unsigned poll_spins) {
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
     static_assert(!kMfma || (W == 8 && QPT == 4 && TILE == kMfmaTile), "the MFMA forward's fixed geometry");
@@ -1542,8 +1575,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int nprod = (int)gridDim.x - 1;
     if ((int)blockIdx.x == nprod) {
         PCM_STAMP2(5);
-        if constexpr (kGran) poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, max_spins);
-        else poll_grad_loss(b, n, m, ws, mean_out, max_spins);
+        if constexpr (kGran) poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, poll_spins);
+        else poll_grad_loss(b, n, m, ws, mean_out, poll_spins);
         PCM_STAMP2(6);
         return;
     }
@@ -1587,9 +1620,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         const float *P2 = P1 + 3 * kGradCap;
         const float g1 = __fmul_rn(w1, 2.f), g2 = __fmul_rn(w2, 2.f);
         const bool ok = first ? range_grad<NT, QW, true>(true, q0, n, m, P1, P2, g1, g2, nullptr, nullptr, G,
-                                                          arena + 24 * kGradCap, G1, G2, tag, max_spins)
+                                                          arena + 24 * kGradCap, G1, G2, tag, max_spins,
+                                                          ws.epoch + kGradSlowWord)
                               : range_grad<NT, QW, true>(false, q0, m, n, P2, P1, g2, g1, nullptr, nullptr, G,
-                                                          arena + 24 * kGradCap, G2, G1, tag, max_spins);
+                                                          arena + 24 * kGradCap, G2, G1, tag, max_spins,
+                                                          ws.epoch + kGradSlowWord);
         if (!ok) {  // a workgroup of this element never published: sticky error, NaN gradients
             if (tid == 0) __hip_atomic_store(ws.epoch + kGradErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int nq = first ? n : m;
@@ -1647,7 +1682,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (old != (unsigned)per - 1) {
             for (unsigned spins = 0;; ++spins) {
                 if (ld_sc1((const int32_t *)ctr) == per) break;
-                if (spins >= max_spins) { late = 1; break; }
+                if (spins >= poll_spins) { late = 1; break; }
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -1728,7 +1763,8 @@ const int kPcmNumFilt16Variants = sizeof(kPcmFilt16Variants) / sizeof(kPcmFilt16
 // ---- fused loss + gradient: variants (tools/tune_chamfer.py) and entry points
 namespace {
 typedef void (*grad_kernel_t)(const float *, const float *, int, int, int, float, float, float *, float *,
-                              int32_t *, int32_t *, float *, float *, float *, int, int, GradWs, unsigned);
+                              int32_t *, int32_t *, float *, float *, float *, int, int, GradWs, unsigned,
+                              unsigned);
 struct GradVariant {
     grad_kernel_t k;
     int waves, qpt;
@@ -1769,7 +1805,7 @@ long long grad_blocks_max(int b, int n, int m) {
 int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, int n, int m, float w1, float w2,
                      float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out, float *grad1,
                      float *grad2, void *workspace, size_t workspace_bytes, void *stream,
-                     unsigned max_spins = pcm_loss::kPollMaxSpins) {
+                     unsigned max_spins = kGradWaitSpins, unsigned poll_spins = pcm_loss::kPollMaxSpins) {
     if (b <= 0 || n <= 0 || m <= 0) return PCM_ERR_INVALID_ARG;
     if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
     if (variant < 0 || variant >= kNumGradVariants) return PCM_ERR_INVALID_ARG;
@@ -1785,7 +1821,8 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
     const GradWs ws = grad_ws((char *)workspace + off, b, blocks);
     // + the polling workgroup (the grid's last)
     hipLaunchKernelGGL(v.k, dim3((unsigned)blocks + 1), dim3(64 * v.waves), 0, (hipStream_t)stream, xyz1, xyz2, b,
-                       n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out, grad1, grad2, nblk1, nblk2, ws, max_spins);
+                       n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out, grad1, grad2, nblk1, nblk2, ws, max_spins,
+                       poll_spins);
     return pcm_launch_status();
 }
 }  // namespace
@@ -1815,15 +1852,32 @@ extern "C" int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const 
 
 extern "C" int pcm_tune_num_chamfer_loss_grad_variants(void) { return kNumGradVariants; }
 
-// the default variant with a given bound on every wait (tests: 0 forces the
-// timeout path -- sticky error word, NaN means and gradients)
-extern "C" int pcm_tune_chamfer_loss_grad_spins(unsigned max_spins, const float *xyz1, const float *xyz2, int b,
-                                                int n, int m, float w1, float w2, float *dist1, float *dist2,
-                                                int32_t *idx1, int32_t *idx2, float *mean_out, float *gradxyz1,
-                                                float *gradxyz2, void *workspace, size_t workspace_bytes,
-                                                void *stream) {
+// the default variant with given bounds on the gradient-phase waits
+// (wait_spins; 0: every argmin recomputed locally, exact results) and on the
+// loss poll (poll_spins; 0 forces its timeout: sticky error word, NaN means)
+extern "C" int pcm_tune_chamfer_loss_grad_spins(unsigned wait_spins, unsigned poll_spins, const float *xyz1,
+                                                const float *xyz2, int b, int n, int m, float w1, float w2,
+                                                float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                                                float *mean_out, float *gradxyz1, float *gradxyz2, void *workspace,
+                                                size_t workspace_bytes, void *stream) {
     return launch_loss_grad(kDefaultGradVariant, xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out,
-                            gradxyz1, gradxyz2, workspace, workspace_bytes, stream, max_spins);
+                            gradxyz1, gradxyz2, workspace, workspace_bytes, stream, wait_spins, poll_spins);
+}
+
+// diagnostics: gradient-phase waits on `workspace` that timed out and computed
+// the missing argmins locally, summed over every call since it was zero-filled
+// (>= 0, or a negative pcm_status); synchronises `stream`
+extern "C" int pcm_tune_chamfer_slow_paths(const void *workspace, size_t workspace_bytes, int b, int n, int m,
+                                           void *stream) {
+    if (b <= 0 || n <= 0 || m <= 0) return 0;
+    if (!workspace || workspace_bytes < pcm_chamfer_loss_ws_offset(b, n, m) + pcm_chamfer_grad_ws_bytes(b, n, m))
+        return PCM_ERR_WORKSPACE;
+    unsigned v = 0;
+    const char *p = (const char *)workspace + pcm_chamfer_loss_ws_offset(b, n, m) + 4 * kGradSlowWord;
+    if (hipMemcpyAsync(&v, p, 4, hipMemcpyDeviceToHost, (hipStream_t)stream) != hipSuccess ||
+        hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
+        return PCM_ERR_LAUNCH;
+    return (int)(v & 0x7fffffffu);
 }
 
 #ifdef PCM_STAMPS

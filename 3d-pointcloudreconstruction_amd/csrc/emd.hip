@@ -674,6 +674,57 @@ __device__ __forceinline__ void part_merge(const float *pb1, const int *pkb, con
               b2);
 }
 
+// ---- the reference's order among EXACTLY equal best values (emd_cuda.cu:
+// 108-110, 136-139, 165-173).  Bid splits every 2048-object tile over
+// tpu = 1024 / ceil(nu / (n / 1024)) threads per bidder (nu: unassigned
+// points this iteration); thread r scans [r delta, (r + 1) delta) of each tile
+// in turn (delta = ceil(tile width / tpu)), keeping its first maximum, and the
+// bidder's threads are merged in thread order with strict '>'.  Among objects
+// of equal value the winner is therefore the lowest (r, tile, k): key
+// (r << 21) | k.  With tpu == 1, or n <= 2048 (one tile: r grows with k), that
+// is the lowest k -- every path below keeps the lowest k and, only when the
+// top two values are equal (a tie at the best) and the order differs, the
+// bidder's winner is re-chosen by this key.  The top-2 VALUES never depend on
+// the order.
+constexpr int kTieKBits = 21;  // object ids < 2^21 (launch_emd)
+struct TieRank {
+    int on, dfull, dlast;  // order differs from the lowest k; delta of full tiles / the last tile
+};
+__device__ __forceinline__ TieRank tie_rank(int n, int nu) {
+    TieRank t;
+    const int bc = n / 1024, upb = (nu + bc - 1) / bc;
+    const int tpu = 1024 / (upb > 0 ? upb : 1);
+    const int lastw = (n & 2047) ? (n & 2047) : 2048;
+    t.on = n > 2048 && tpu > 1;
+    t.dfull = (2048 + tpu - 1) / tpu;
+    t.dlast = (lastw + tpu - 1) / tpu;
+    return t;
+}
+__device__ __forceinline__ int tie_key(const TieRank &t, int k, int n) {
+    const int d = (k >> 11) == ((n - 1) >> 11) ? t.dlast : t.dfull;
+    return (((k & 2047) / d) << kTieKBits) | k;
+}
+// wave: the reference's winner among the objects whose exact value equals
+// b1 (every object re-evaluated: rare -- exact ties at the best)
+__device__ __noinline__ int tie_rescan(float x1, float y1, float z1, const float *Qc, const float *price, int n,
+                                       float b1, TieRank t) {
+    const int lane = threadIdx.x & 63;
+    int best = 0x7fffffff;
+    for (int k = lane; k < n; k += 64) {
+        const float v = value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), price[k]);
+        if (v == b1) best = min(best, tie_key(t, k, n));
+    }
+    return wave_min_i(best) & ((1 << kTieKBits) - 1);
+}
+template <bool kG>
+__device__ __forceinline__ int tie_fix(int kb, float b1, float b2, float x1, float y1, float z1, const float *Qc,
+                                       const float *price, int n, const TieRank &t) {
+    if constexpr (kG) {
+        if (t.on && b1 == b2 && (unsigned)kb < (unsigned)n) return tie_rescan(x1, y1, z1, Qc, price, n, b1, t);
+    }
+    return kb;
+}
+
 // one wave: the full bid of point (x1, y1, z1) with a rebuilt cache
 template <bool kSc1>
 __device__ __forceinline__ void scan_full(float x1, float y1, float z1, const float *Qc, const float *price, int n,
@@ -714,7 +765,7 @@ struct EmdWs {
     float *g_price, *g_inc;
     ckey *g_claim;
 };
-constexpr int kBoardGen = 0, kBoardQuit = 8, kBoardJn = 16, kBoardErr = 24;
+constexpr int kBoardGen = 0, kBoardQuit = 8, kBoardJn = 16, kBoardNu = 20, kBoardErr = 24;
 constexpr unsigned kInB = 0x7fc0b00bu;  // a quiet NaN no bound ever equals
 
 // ===========================================================================
@@ -821,6 +872,24 @@ __device__ __forceinline__ int cache_bid_lanes(int nu) {
     return nu <= 64 ? 16 : (nu <= 256 ? 8 : 4);
 }
 
+// the reference's winner among a group's cached entries of value b1 (rare:
+// exact ties at the best, global-state form): lane gl re-reads its slots
+template <int G>
+__device__ __noinline__ int cache_tie_winner(const centry *cj, bool sc1, const float *price, float b1, TieRank tr,
+                                             int n) {
+    constexpr int E = kL / G;
+    const int gl = threadIdx.x % G;
+    int lr = 0x7fffffff;
+    for (int e = 0; e < E; ++e) {
+        const int slot = 2 * (gl + G * (e >> 1)) + (e & 1);
+        const centry c = sc1 ? ld_sc1(cj + slot) : cj[slot];
+        const int k = (int)(unsigned)c;
+        if (k < 0) continue;
+        if (value_from_s(__uint_as_float((unsigned)(c >> 32)), price[k]) == b1) lr = min(lr, tie_key(tr, k, n));
+    }
+    return group_min_i<G>(lr) & ((1 << kTieKBits) - 1);
+}
+
 // A bid on object k.  Maxima persisted from earlier iterations are <= 0
 // (0 initially, -1e9 once assigned), and with eps > 0 every increment is > 0,
 // so an old maximum above 0 means a second bid on k in this iteration: the
@@ -839,7 +908,7 @@ __device__ __forceinline__ void bid_on(const AState<kG> &st, int j, int k, float
 template <int G, bool kG>
 __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, const centry *C, const float *CT,
                                            const centry *CB, const float *CTB, const AState<kG> &st, int *sNm,
-                                           int *coll, const float *resT, int *resN) {
+                                           int *coll, const float *resT, int *resN, int n, TieRank tr) {
     static_assert(G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
     constexpr int E = kL / G;
     static_assert(E % 2 == 0, "slot pairs");
@@ -897,10 +966,19 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
             lc += eq ? 1 : 0;
             lrest = eq ? lrest : fmaxf(lrest, v[e]);
         }
-        const int kb = group_min_i<G>(lk);
+        int kb = group_min_i<G>(lk);
         const int ties = group_add_i<G>(lc);
         const float rest = group_max<G>(lrest);
         const float b2 = ties >= 2 ? b1 : rest;
+        if constexpr (kG) {
+            // a tie at the best (group-uniform): the reference's order
+            // decides.  When the bid is proven (b2 > bound) every object of
+            // value b1 is cached, so the cached entries hold the winner (out
+            // of line: the entries are re-read rather than kept live)
+            if (tr.on && ties >= 2 && b2 > tj)
+                kb = cache_tie_winner<G>(__float_as_uint(CT[j]) == kInB ? CB + (size_t)j * kL : C + (size_t)j * kL,
+                                         __float_as_uint(CT[j]) == kInB, st.price, b1, tr, n);
+        }
         if (act && gl == G - 1) {
             if (b2 > tj) {
                 bid_on(st, j, kb, b1 - b2 + eps, coll);
@@ -930,14 +1008,17 @@ __device__ __forceinline__ void place_bid(const AState<kG> &st, int j, int kb, f
 
 // helper side of a job item: full scan with the snapshot prices, cache into
 // region B, result words, then the done word (sc1 throughout)
+template <bool kG>
 __device__ __forceinline__ void helper_item(const EmdWs &ws, size_t base, int i, int g, const float *P,
-                                            const float *Qc, const float *price, int n, float eps) {
+                                            const float *Qc, const float *price, int n, float eps,
+                                            const TieRank &tr) {
     const int lane = threadIdx.x & 63;
     const int j = __builtin_amdgcn_readfirstlane(ld_sc1(ws.ml + base + i));
     float b1, b2, T;
     int kb;
     scan_full<true>(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, price, n, ws.cacheB + (base + j) * kL, b1, kb, b2,
                     T);
+    kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, price, n, tr);
     if (lane == 0) {
         st_sc1(ws.CTB + base + j, T);
         st_sc1(ws.rbid + base + i, (int)kb);
@@ -950,6 +1031,7 @@ __device__ __forceinline__ void helper_item(const EmdWs &ws, size_t base, int i,
 struct KArgs {
     const float *xyz1, *xyz2;
     int b, n, iters, H, offload_min, diag, wmax, tail_max;
+    int spin_limit;  // bound of every poll (kSpinLimit; tests force 0)
     float eps;
     float *dist;
     int32_t *ass_out;
@@ -963,7 +1045,7 @@ struct KArgs {
 constexpr int kDiagHist = 1, kDiagTimers = 2;
 
 // helper role: take full scans of the master's jobs until it quits
-template <bool kStage, int kN>
+template <bool kG, bool kStage, int kN>
 __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank, int *smem) {
     __shared__ int sGen;
     const int n = kN > 0 ? kN : a.n;  // kN: the cloud size fixed at compile time
@@ -979,8 +1061,8 @@ __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank
     int last = 0;
     for (;;) {
         if (tid == 0) {
-            int g = -1;
-            for (int spin = 0; spin < kSpinLimit; ++spin) {
+            int g = -1;  // no job within the bound: this helper leaves (the master scans what it would have)
+            for (int spin = 0; spin < a.spin_limit; ++spin) {
                 if (ld_sc1(bw + kBoardQuit)) break;
                 const int gv = ld_sc1(bw + kBoardGen);
                 if (gv != last) { g = gv; break; }
@@ -993,11 +1075,12 @@ __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank
         const int g = sGen;
         if (g < 0) return;
         const int jn = ld_sc1(bw + kBoardJn);
+        const TieRank tr = tie_rank(n, ld_sc1(bw + kBoardNu));  // the job's iteration
         for (int k = tid; k < n; k += kEmdThreads) sPH[k] = ld_sc1(ws.pp + base + k);
         __syncthreads();
         for (int g0 = rank + 1; g0 * kWaves < jn; g0 += a.H + 1) {  // this helper's groups (owner rank + 1)
             const int i = g0 * kWaves + wave;
-            if (i < jn) helper_item(ws, base, i, g, P, Qc, sPH, n, a.eps);
+            if (i < jn) helper_item<kG>(ws, base, i, g, P, Qc, sPH, n, a.eps, tr);
         }
         if (a.diag == kDiagHist && tid == 0) atomicAdd(&a.stats[2 * a.iters + 12], 1);  // helper wake-ups
         last = g;
@@ -1078,7 +1161,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     vm_drain();  // the DMA has landed
     __syncthreads();
 
-    int gen = 0;  // jobs posted so far
+    TieRank tr = tie_rank(n, n);  // the current iteration's exact-tie order
+    int gen = 0;   // jobs posted so far
+    int H = a.H;   // helpers still taking jobs (0 after a timed-out job)
     // timers (diag >= 2): cycles per phase, kept by thread 0 in LDS (not in
     // registers the whole kernel would reserve)
     __shared__ unsigned long long sTm[13];  // [12] = the previous stamp
@@ -1154,6 +1239,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
 #else
         scan_full<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
 #endif
+        kb = tie_fix<kG>(kb, b1, b2, x1, y1, z1, Qc, st.price, n, tr);
         if (lane == 0) {
             CT[j] = T;
             place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
@@ -1166,6 +1252,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         const int nu = sNu[cur];
         if (nu == 0) break;  // nothing left to bid: later iterations are no-ops
         ++active;
+        tr = tie_rank(n, nu);
         // (two named arrays, not an indexed pair: the selected pointer keeps
         // its address space and the list reads stay ds_read, not flat loads)
         const int *Ucur = cur ? st.U1 : st.U0;
@@ -1202,6 +1289,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     float b1, b2;
                     int kb;
                     part_merge(sPb1, sPkb, sPb2, kWaves, b1, kb, b2);
+                    kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, tr);
                     int next = j;  // no bid / not won: j bids again
                     if ((unsigned)kb < (unsigned)n && lane == 0) {
                         if (it == iters - 1) {
@@ -1249,6 +1337,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     float b1, b2;
                     int kb;
                     part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, 0, 1, b1, kb, b2);
+                    kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, tr);
                     if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
                 }
             } else if (q < nu) {
@@ -1267,7 +1356,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 float b1, b2;
                 int kb;
                 part_merge(sPb1 + wave, sPkb + wave, sPb2 + wave, W, b1, kb, b2);
-                if (lane == 0) place_bid(st, Ucur[q], kb, b1 - b2 + eps, n, &sColl);
+                const int j = Ucur[q];
+                kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, tr);
+                if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
             }
             __syncthreads();
             PCM_EMD_PHASE(1);
@@ -1289,9 +1380,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             const int G = cache_bid_lanes(nu);
             const float *rT = kRes ? sRT : nullptr;
             int *rN = kRes ? sRN : nullptr;
-            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN);
-            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN);
-            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN);
+            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN, n, tr);
+            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN, n, tr);
+            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN, n, tr);
         }
         __syncthreads();
         PCM_EMD_PHASE(0);
@@ -1303,12 +1394,15 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             atomicAdd(&a.stats[2 * it + 1], nm);
         }
         if (nm > 0) {
-            if (a.H > 0 && nm > a.offload_min) {
+            if (H > 0 && nm > a.offload_min) {
                 // publish the job: miss list, price snapshot, size
                 ++gen;
                 for (int i = tid; i < nm; i += kEmdThreads) st_sc1(ws.ml + base + i, st.miss[i]);
                 for (int k = tid; k < n; k += kEmdThreads) st_sc1(ws.pp + base + k, st.price[k]);
-                if (tid == 0) st_sc1(bw + kBoardJn, nm);
+                if (tid == 0) {
+                    st_sc1(bw + kBoardJn, nm);
+                    st_sc1(bw + kBoardNu, nu);
+                }
                 vm_drain();
                 __syncthreads();
                 if (tid == 0) st_sc1(bw + kBoardGen, gen);
@@ -1325,17 +1419,34 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 }
                 __syncthreads();
                 PCM_EMD_PHASE(5);
-                // collect the helpers' items once their done words show this job
+                // collect the helpers' items once their done words show this
+                // job.  An item whose done word does not arrive within the
+                // bound (a helper that is not resident, or left) keeps its
+                // miss entry: the master scans it below itself, so a timeout
+                // costs time, never correctness
+                bool late = false;
                 for (int i = tid; i < nm; i += kEmdThreads) {
                     const int j = st.miss[i];
                     if (j < 0) continue;
                     int spin = 0;
-                    while (ld_sc1(ws.idone + base + i) != gen) {
-                        __builtin_amdgcn_s_sleep(1);
-                        if (++spin > kSpinLimit) { st_sc1(bw + kBoardErr, 1); break; }
+                    while (!late && ld_sc1(ws.idone + base + i) != gen) {
+                        if (++spin > a.spin_limit) late = true;
+                        else __builtin_amdgcn_s_sleep(1);
                     }
+                    if (late) continue;
                     CT[j] = __uint_as_float(kInB);
                     place_bid(st, j, ld_sc1(ws.rbid + base + i), ld_sc1(ws.rinc + base + i), n, &sColl);
+                    st.miss[i] = -1 - j;
+                }
+                if (__syncthreads_or(late ? 1 : 0)) {
+                    // region A rebuilt for the unanswered items, bids placed;
+                    // no further jobs in this call (the word is a diagnostic)
+                    H = 0;
+                    if (tid == 0) st_sc1(bw + kBoardErr, 1);
+                    for (int i = wave; i < nm; i += kWaves) {
+                        const int j = __builtin_amdgcn_readfirstlane(st.miss[i]);
+                        if (j >= 0) own_scan(j);
+                    }
                 }
                 if (hist && tid == 0) {
                     atomicAdd(&a.stats[2 * iters + 10], 1);   // jobs
@@ -1383,6 +1494,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                         centry *cj = C + (size_t)j * kL;
                         if (!scan_fast_finish<false>(t, x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T))
                             scan_exact<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
+                        kb = tie_fix<kG>(kb, b1, b2, x1, y1, z1, Qc, st.price, n, tr);
                         if (lane == 0) {
                             CT[j] = T;
                             place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
@@ -1502,7 +1614,7 @@ __global__ __launch_bounds__(kEmdThreads) void emd_auction_kernel(KArgs a, EmdWs
         rank = h / a.b;
     }
     if (rank >= a.H) return;
-    helper_loop<kStage, kN>(a, ws, batch, rank, smem);
+    helper_loop<kG, kStage, kN>(a, ws, batch, rank, smem);
 }
 
 __global__ void emd_bwd_kernel(const float *__restrict__ xyz1, const float *__restrict__ xyz2, int n,
@@ -1580,18 +1692,25 @@ extern "C" size_t pcm_emd_workspace_bytes(int b, int n) {
 }
 
 namespace {
+// helpers per batch element: every master and helper gets a CU of its own
+// (the launch pads LDS to one workgroup per CU), sized from the device's CU
+// count (a compute partition or a CU-masked device has fewer than 256).  A
+// helper that is not resident only costs time: the master scans the items
+// it would have taken itself.
 int default_helpers(int b, int n) {
     if (n > kHelperMaxN) return 0;
-    const int h = 256 / b - 1;
+    const int h = pcm_device_cus() / b - 1;
     return h < 0 ? 0 : (h > kMaxHelpers ? kMaxHelpers : h);
 }
 
 int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters, float *dist,
                int32_t *assignment, float *price, void *workspace, size_t workspace_bytes, int helpers,
-               int offload_min, int diag, int wsplit, int tail_max, int32_t *stats, void *stream) {
+               int offload_min, int diag, int wsplit, int tail_max, int32_t *stats, void *stream,
+               int spin_limit = kSpinLimit) {
     // emd_cuda.cu:236-249 (n == m is enforced by the single n here)
     if (b < 0 || n < 0 || b > 512 || n % 1024 != 0 || iters < 1) return PCM_ERR_INVALID_ARG;
     if (b == 0 || n == 0) return PCM_OK;
+    if (n > (1 << kTieKBits)) return PCM_ERR_UNSUPPORTED;  // object ids in the tie keys
     if (!xyz1 || !xyz2 || !dist || !assignment) return PCM_ERR_INVALID_ARG;
     const size_t need = ws_layout(b, n, nullptr, nullptr);
     if (!workspace || workspace_bytes < need) return PCM_ERR_WORKSPACE;
@@ -1636,8 +1755,8 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     if (H > 0 && lds < 84 * 1024) lds = 84 * 1024;
     KArgs ka{xyz1, xyz2, b, n, iters, H, offload_min >= 0 ? offload_min : kDefaultOffloadMin,
              stats ? (diag >= kDiagTimers ? diag : kDiagHist) : 0,
-             wsplit > 0 ? wsplit : kDefaultWsplit, tail_max >= 0 ? tail_max : kDefaultTailMax, eps, dist, assignment,
-             price, stats};
+             wsplit > 0 ? wsplit : kDefaultWsplit, tail_max >= 0 ? tail_max : kDefaultTailMax,
+             spin_limit >= 0 ? spin_limit : kSpinLimit, eps, dist, assignment, price, stats};
     const unsigned grid = (unsigned)(b * (1 + H));
     auto launch = [&](auto kfn) -> int {
         if (lds > 64 * 1024 &&
@@ -1677,29 +1796,46 @@ extern "C" int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int 
 extern "C" int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
                                         float *dist, int32_t *assignment, float *price, void *workspace,
                                         size_t workspace_bytes, int helpers, int offload_min, int diag,
-                                        int wsplit, int tail_max, int32_t *stats, void *stream) {
+                                        int wsplit, int tail_max, int spin_limit, int32_t *stats, void *stream) {
     return launch_emd(xyz1, xyz2, b, n, eps, iters, dist, assignment, price, workspace, workspace_bytes, helpers,
-                      offload_min, diag, wsplit, tail_max, stats, stream);
+                      offload_min, diag, wsplit, tail_max, stats, stream, spin_limit);
 }
 
-// sticky device-side error of the last pcm_emd_forward on this workspace
-// (a poll that timed out); synchronises `stream`.  Returns PCM_OK or
-// PCM_ERR_LAUNCH.
-extern "C" int pcm_emd_workspace_status(const void *workspace, size_t workspace_bytes, int b, int n,
-                                        void *stream) {
-    if (b <= 0 || n <= 0) return PCM_OK;
+namespace {
+// batch elements of the last forward on `workspace` whose master timed out
+// on a helper job (and scanned those items itself); synchronises `stream`
+int emd_timeouts(const void *workspace, size_t workspace_bytes, int b, int n, void *stream) {
+    if (b <= 0 || n <= 0) return 0;
     if (!workspace || workspace_bytes < ws_layout(b, n, nullptr, nullptr)) return PCM_ERR_WORKSPACE;
     EmdWs ws;
     ws_layout(b, n, &ws, (char *)workspace);
+    int count = 0;
     for (int i = 0; i < b; ++i) {
         int32_t err = 0;
         if (hipMemcpyAsync(&err, ws.board + (size_t)i * kBoardWords + kBoardErr, 4, hipMemcpyDeviceToHost,
                            (hipStream_t)stream) != hipSuccess ||
             hipStreamSynchronize((hipStream_t)stream) != hipSuccess)
             return PCM_ERR_LAUNCH;
-        if (err) return PCM_ERR_LAUNCH;
+        count += err ? 1 : 0;
     }
-    return PCM_OK;
+    return count;
+}
+}  // namespace
+
+// Status of the last pcm_emd_forward on this workspace; synchronises `stream`.
+// Every wait between the auction's workgroups is bounded and a timed-out
+// helper job is scanned by the master itself, so the outputs never depend on
+// helper residency: PCM_OK unless reading the workspace fails.
+extern "C" int pcm_emd_workspace_status(const void *workspace, size_t workspace_bytes, int b, int n,
+                                        void *stream) {
+    const int t = emd_timeouts(workspace, workspace_bytes, b, n, stream);
+    return t < 0 ? t : PCM_OK;
+}
+
+// diagnostics: how many batch elements of the last forward had a helper job
+// time out (>= 0), or a negative pcm_status
+extern "C" int pcm_tune_emd_timeouts(const void *workspace, size_t workspace_bytes, int b, int n, void *stream) {
+    return emd_timeouts(workspace, workspace_bytes, b, n, stream);
 }
 
 extern "C" int pcm_emd_backward(const float *xyz1, const float *xyz2, int b, int n,

@@ -880,7 +880,7 @@ int launch_prep(const double *dst, int b, int m, void *workspace, hipStream_t s,
 // slices per pair: fill the chip (K b <= 256 one-per-CU workgroups), at least
 // 64 points each, at most 1024 (16 per lane)
 int icp_slices(int b, int n) {
-    int K = 256 / b;
+    int K = pcm_device_cus() / b;  // one workgroup per CU across the batch
     K = K < 1 ? 1 : (K > kIcpMaxSlices ? kIcpMaxSlices : K);
     const int most = (n + 63) / 64, least = (n + 1023) / 1024;
     K = K < most ? K : most;
@@ -913,8 +913,10 @@ extern "C" int pcm_icp(const double *A, const double *B, int b, int n, const dou
     const bool lds_rows = (size_t)nn_mpad(n) * 16 <= (size_t)kIcpRowsLdsMax;
     const size_t lds = (lds_rows ? (size_t)nn_mpad(n) * 16 : 0) + (size_t)S * (8 + 4 + 32) + 8;
     // pairs per launch: every slice of a pair must be resident while the
-    // others wait on it, so a launch holds at most 256 workgroups (one per CU)
-    const int per_launch = K <= 256 ? 256 / K : 1;
+    // others wait on it, so a launch holds at most one workgroup per CU of
+    // this device (256 on a whole MI355X)
+    const int cus = pcm_device_cus();
+    const int per_launch = K <= cus ? cus / K : 1;
     auto launch = [&](auto kfn) -> int {
         if (lds > 64 * 1024 &&
             hipFuncSetAttribute((const void *)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)

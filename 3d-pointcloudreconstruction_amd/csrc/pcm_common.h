@@ -133,6 +133,17 @@ __device__ __forceinline__ int pcm_xcd_remap(int i, int g) {
     return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + s;
 }
 
+// Compute units of the current device (256 on a whole MI355X; fewer on a
+// compute partition).  Grids whose workgroups wait on each other are sized
+// from it; 256 if the query fails.
+static inline int pcm_device_cus() {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+        return 256;
+    return cus;
+}
+
 static inline int pcm_launch_status() {
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? PCM_OK : PCM_ERR_LAUNCH;

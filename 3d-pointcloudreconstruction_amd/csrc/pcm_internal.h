@@ -21,10 +21,12 @@ int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const float *xyz2
                                float w2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out,
                                float *gradxyz1, float *gradxyz2, void *workspace, size_t workspace_bytes,
                                void *stream);
-int pcm_tune_chamfer_loss_grad_spins(unsigned max_spins, const float *xyz1, const float *xyz2, int b, int n, int m,
-                                     float w1, float w2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
-                                     float *mean_out, float *gradxyz1, float *gradxyz2, void *workspace,
-                                     size_t workspace_bytes, void *stream);
+int pcm_tune_chamfer_loss_grad_spins(unsigned wait_spins, unsigned poll_spins, const float *xyz1, const float *xyz2,
+                                     int b, int n, int m, float w1, float w2, float *dist1, float *dist2,
+                                     int32_t *idx1, int32_t *idx2, float *mean_out, float *gradxyz1, float *gradxyz2,
+                                     void *workspace, size_t workspace_bytes, void *stream);
+int pcm_tune_chamfer_slow_paths(const void *workspace, size_t workspace_bytes, int b, int n, int m, void *stream);
+size_t pcm_tune_chamfer_err_offset(int which, int b, int n, int m);  // sticky error words' byte offsets
 int pcm_tune_read_stamps(unsigned long long *host, int nblocks);  // profiling build only (make stamps)
 int pcm_tune_num_chamfer_f16_variants(void);
 int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
@@ -33,11 +35,15 @@ int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, const uint16
 // misses above which an iteration's full scans go to the helpers (-1 =
 // default); diag: 1 = per-iteration counts, 2 = phase timers (csrc/emd.hip);
 // wsplit: most waves a full scan is split over (1, 2, 4; <= 0 = default);
-// tail_max: bidders at or below which an iteration runs in tail mode (-1 = default, 0 = never)
+// tail_max: bidders at or below which an iteration runs in tail mode (-1 = default, 0 = never);
+// spin_limit: bound of every wait between workgroups (-1 = default; 0 forces
+// the timeout path: the master scans every offloaded item itself)
 int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n, float eps, int iters,
                              float *dist, int32_t *assignment, float *price, void *workspace,
                              size_t workspace_bytes, int helpers, int offload_min, int diag, int wsplit,
-                             int tail_max, int32_t *stats, void *stream);
+                             int tail_max, int spin_limit, int32_t *stats, void *stream);
+// batch elements of the last EMD forward whose master timed out on a helper job (>= 0)
+int pcm_tune_emd_timeouts(const void *workspace, size_t workspace_bytes, int b, int n, void *stream);
 #ifdef __cplusplus
 }
 #endif

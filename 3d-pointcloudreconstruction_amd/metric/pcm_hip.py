@@ -69,8 +69,12 @@ def load_library():
     L.pcm_chamfer_workspace_status.restype = ci
     L.pcm_chamfer_workspace_status.argtypes = [vp, cs, ci, ci, ci, vp]
     L.pcm_tune_chamfer_loss_grad_spins.restype = ci
-    L.pcm_tune_chamfer_loss_grad_spins.argtypes = [ctypes.c_uint, vp, vp, ci, ci, ci, cf, cf, vp, vp, vp, vp, vp, vp,
-                                                   vp, vp, cs, vp]
+    L.pcm_tune_chamfer_loss_grad_spins.argtypes = [ctypes.c_uint, ctypes.c_uint, vp, vp, ci, ci, ci, cf, cf, vp, vp,
+                                                   vp, vp, vp, vp, vp, vp, cs, vp]
+    L.pcm_tune_chamfer_slow_paths.restype = ci
+    L.pcm_tune_chamfer_slow_paths.argtypes = [vp, cs, ci, ci, ci, vp]
+    L.pcm_tune_chamfer_err_offset.restype = cs
+    L.pcm_tune_chamfer_err_offset.argtypes = [ci, ci, ci, ci]
     L.pcm_chamfer_forward_loss.restype = ci
     L.pcm_chamfer_forward_loss.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, cs, vp]
     L.pcm_tune_num_chamfer_variants.restype = ci
@@ -98,7 +102,10 @@ def load_library():
     L.pcm_emd_workspace_status.restype = ci
     L.pcm_emd_workspace_status.argtypes = [vp, cs, ci, ci, vp]
     L.pcm_tune_emd_forward_cfg.restype = ci
-    L.pcm_tune_emd_forward_cfg.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, vp, cs, ci, ci, ci, ci, ci, vp, vp]
+    L.pcm_tune_emd_forward_cfg.argtypes = [vp, vp, ci, ci, cf, ci, vp, vp, vp, vp, cs, ci, ci, ci, ci, ci, ci, vp,
+                                           vp]
+    L.pcm_tune_emd_timeouts.restype = ci
+    L.pcm_tune_emd_timeouts.argtypes = [vp, cs, ci, ci, vp]
     L.pcm_chamfer_loss_grad.restype = ci
     L.pcm_chamfer_loss_grad.argtypes = [vp, vp, ci, ci, ci, cf, cf, vp, vp, vp, vp, vp, vp, vp, vp, cs, vp]
     L.pcm_tune_chamfer_loss_grad.restype = ci
@@ -204,18 +211,71 @@ def chamfer_workspace(dev: torch.device, b: int, n: int, m: int) -> torch.Tensor
     return ws
 
 
+class _StickyWatch:
+    """Lagged, sync-free check of a cached fused-loss workspace's sticky error
+    words (a loss poll that timed out: NaN means from then on).  After every
+    call the two words are copied asynchronously to pinned host memory behind
+    an event; the next call on the workspace reads them once that event has
+    completed and, if either is set, re-zeroes the workspace and raises
+    PcmError, so a timeout is reported instead of silently persisting."""
+
+    def __init__(self, ws, b, n, m):
+        L = load_library()
+        self.ws = ws
+        self.offs = [int(L.pcm_tune_chamfer_err_offset(w, b, n, m)) for w in (0, 1)]
+        self.host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
+        self.event = None
+
+    def check(self):
+        if self.event is None or not self.event.query():
+            return
+        bad = bool(self.host.any())
+        self.event = None
+        if bad:
+            self.host.zero_()
+            self.ws.zero_()
+            raise PcmError("a fused Chamfer loss kernel timed out waiting on its other workgroups "
+                           "(NaN means); its workspace has been reset -- repeat the step")
+
+    def record(self):
+        for i, o in enumerate(self.offs):
+            self.host[i:i + 1].copy_(self.ws[o:o + 4].view(torch.int32), non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record()
+
+
+_watches = {}
+
+
+def _watched_workspace(dev, b, n, m):
+    """The cached workspace plus its sticky-error watch (None under graph
+    capture, where host reads and events are not part of the graph)."""
+    ws = chamfer_workspace(dev, b, n, m)
+    if torch.cuda.is_current_stream_capturing():
+        return ws, None
+    key = (ws.data_ptr(), b, n, m)
+    w = _watches.get(key)
+    if w is None:
+        w = _watches[key] = _StickyWatch(ws, b, n, m)
+    w.check()
+    return ws, w
+
+
 def chamfer_forward_loss(xyz1, xyz2, dist1, dist2, idx1, idx2, mean_out, workspace=None) -> None:
     """pcm_chamfer_forward_loss: forward + mean_out[0:2] = (mean(dist1), mean(dist2))."""
     dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2, mean_out)
     b, n, _ = xyz1.shape
     m = xyz2.shape[1]
-    if workspace is None:
-        workspace = chamfer_workspace(dev, b, n, m)
+    watch = None
     with torch.cuda.device(dev):
+        if workspace is None:
+            workspace, watch = _watched_workspace(dev, b, n, m)
         _check(load_library().pcm_chamfer_forward_loss(
             _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
             _ptr(mean_out), _ptr(workspace), workspace.numel(), _stream(dev)),
             "pcm_chamfer_forward_loss")
+        if watch is not None:
+            watch.record()
 
 
 def loss_grad_supported(xyz1, xyz2) -> bool:
@@ -234,10 +294,11 @@ def chamfer_loss_grad(xyz1, xyz2, w1, w2, dist1, dist2, idx1, idx2, mean_out, gr
     m = xyz2.shape[1]
     if mean_out.numel() < 3:
         raise ValueError("mean_out needs 3 floats")
-    if workspace is None:
-        workspace = chamfer_workspace(dev, b, n, m)
     L = load_library()
+    watch = None
     with torch.cuda.device(dev):
+        if workspace is None:
+            workspace, watch = _watched_workspace(dev, b, n, m)
         args = (_ptr(xyz1), _ptr(xyz2), b, n, m, float(w1), float(w2), _ptr(dist1), _ptr(dist2), _ptr(idx1),
                 _ptr(idx2), _ptr(mean_out), _ptr(gradxyz1), _ptr(gradxyz2), _ptr(workspace), workspace.numel(),
                 _stream(dev))
@@ -245,6 +306,8 @@ def chamfer_loss_grad(xyz1, xyz2, w1, w2, dist1, dist2, idx1, idx2, mean_out, gr
             _check(L.pcm_chamfer_loss_grad(*args), "pcm_chamfer_loss_grad")
         else:
             _check(L.pcm_tune_chamfer_loss_grad(int(variant), *args), "pcm_tune_chamfer_loss_grad")
+        if watch is not None:
+            watch.record()
 
 
 def chamfer_workspace_status(workspace, b: int, n: int, m: int) -> None:
@@ -257,18 +320,31 @@ def chamfer_workspace_status(workspace, b: int, n: int, m: int) -> None:
                "pcm_chamfer_workspace_status")
 
 
-def tune_chamfer_loss_grad_spins(max_spins, xyz1, xyz2, w1, w2, dist1, dist2, idx1, idx2, mean_out, gradxyz1,
-                                 gradxyz2, workspace) -> None:
-    """Internal: pcm_chamfer_loss_grad with every wait bounded by max_spins
-    polls (0 forces the timeout path; tests)."""
+def tune_chamfer_loss_grad_spins(wait_spins, poll_spins, xyz1, xyz2, w1, w2, dist1, dist2, idx1, idx2, mean_out,
+                                 gradxyz1, gradxyz2, workspace) -> None:
+    """Internal: pcm_chamfer_loss_grad with the gradient-phase waits bounded by
+    wait_spins polls (0: every argmin recomputed locally -- exact results) and
+    the loss poll by poll_spins (0 forces its timeout: sticky error, NaN means)."""
     dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2, mean_out, gradxyz1, gradxyz2)
     b, n, _ = xyz1.shape
     m = xyz2.shape[1]
     with torch.cuda.device(dev):
         _check(load_library().pcm_tune_chamfer_loss_grad_spins(
-            int(max_spins), _ptr(xyz1), _ptr(xyz2), b, n, m, float(w1), float(w2), _ptr(dist1), _ptr(dist2),
-            _ptr(idx1), _ptr(idx2), _ptr(mean_out), _ptr(gradxyz1), _ptr(gradxyz2), _ptr(workspace),
+            int(wait_spins), int(poll_spins), _ptr(xyz1), _ptr(xyz2), b, n, m, float(w1), float(w2), _ptr(dist1),
+            _ptr(dist2), _ptr(idx1), _ptr(idx2), _ptr(mean_out), _ptr(gradxyz1), _ptr(gradxyz2), _ptr(workspace),
             workspace.numel(), _stream(dev)), "pcm_tune_chamfer_loss_grad_spins")
+
+
+def chamfer_slow_paths(workspace, b: int, n: int, m: int) -> int:
+    """Internal: gradient-phase waits on `workspace` that timed out and computed
+    the missing argmins locally (since the workspace was zero-filled)."""
+    dev = workspace.device
+    with torch.cuda.device(dev):
+        r = int(load_library().pcm_tune_chamfer_slow_paths(_ptr(workspace), workspace.numel(), b, n, m,
+                                                           _stream(dev)))
+    if r < 0:
+        _check(r, "pcm_tune_chamfer_slow_paths")
+    return r
 
 
 def tune_num_chamfer_loss_grad_variants() -> int:
@@ -354,20 +430,22 @@ def emd_workspace(dev: torch.device, b: int, n: int) -> torch.Tensor:
 
 def emd_forward(xyz1, xyz2, eps: float, iters: int, dist, assignment, price=None,
                 workspace=None, helpers=None, offload_min=None, stats=None, diag=1, wsplit=None,
-                tail_max=None) -> None:
+                tail_max=None, spin_limit=None) -> None:
     """pcm_emd_forward; helpers / offload_min / stats select the tuning entry
     (helper workgroups per cloud, the miss count above which an iteration's
     full scans are offloaded, diagnostics of kind `diag`: 1 counts, 2 + i phase
     timers of batch element i; wsplit: waves per few-miss full scan; tail_max:
-    bidders at or below which an iteration runs in tail mode, 0 = never --
-    csrc/emd.hip pcm_tune_emd_forward_cfg) -- None = the defaults."""
+    bidders at or below which an iteration runs in tail mode, 0 = never;
+    spin_limit: bound of the waits between workgroups, 0 forces the timeout
+    path -- csrc/emd.hip pcm_tune_emd_forward_cfg) -- None = the defaults."""
     dev = _require_device(xyz1, xyz2, dist, assignment)
     b, n, _ = xyz1.shape
     ws_bytes = emd_workspace_bytes(b, n)
     if ws_bytes and (workspace is None or workspace.numel() * workspace.element_size() < ws_bytes):
         workspace = emd_workspace(dev, b, n)
     with torch.cuda.device(dev):
-        if helpers is None and offload_min is None and stats is None and wsplit is None and tail_max is None:
+        if (helpers is None and offload_min is None and stats is None and wsplit is None and tail_max is None
+                and spin_limit is None):
             _check(load_library().pcm_emd_forward(
                 _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
                 _ptr(price), _ptr(workspace), ws_bytes, _stream(dev)), "pcm_emd_forward")
@@ -378,17 +456,30 @@ def emd_forward(xyz1, xyz2, eps: float, iters: int, dist, assignment, price=None
                 _ptr(xyz1), _ptr(xyz2), b, n, float(eps), int(iters), _ptr(dist), _ptr(assignment),
                 _ptr(price), _ptr(workspace), ws_bytes, -1 if helpers is None else int(helpers),
                 -1 if offload_min is None else int(offload_min), int(diag), 0 if wsplit is None else int(wsplit),
-                -1 if tail_max is None else int(tail_max), _ptr(stats), _stream(dev)),
+                -1 if tail_max is None else int(tail_max), -1 if spin_limit is None else int(spin_limit),
+                _ptr(stats), _stream(dev)),
                 "pcm_tune_emd_forward_cfg")
 
 
 def emd_workspace_status(workspace, b: int, n: int) -> None:
-    """Raise PcmError if the last EMD forward on `workspace` hit a device-side
-    timeout (synchronises the current stream)."""
+    """Raise PcmError if reading the last EMD forward's status fails
+    (synchronises the current stream).  A helper job that timed out is not an
+    error: the master scanned those items itself (emd_timeouts counts them)."""
     dev = workspace.device
     with torch.cuda.device(dev):
         _check(load_library().pcm_emd_workspace_status(_ptr(workspace), workspace.numel(), b, n, _stream(dev)),
                "pcm_emd_workspace_status")
+
+
+def emd_timeouts(workspace, b: int, n: int) -> int:
+    """Internal: batch elements of the last EMD forward on `workspace` whose
+    master timed out on a helper job and scanned the items itself."""
+    dev = workspace.device
+    with torch.cuda.device(dev):
+        r = int(load_library().pcm_tune_emd_timeouts(_ptr(workspace), workspace.numel(), b, n, _stream(dev)))
+    if r < 0:
+        _check(r, "pcm_tune_emd_timeouts")
+    return r
 
 
 def emd_backward(xyz1, xyz2, graddist, assignment, gradxyz1) -> None:

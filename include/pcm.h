@@ -112,12 +112,15 @@ int pcm_chamfer_loss_grad(const float *xyz1, const float *xyz2, int b, int n, in
                           void *stream);
 
 /*
- * Device-side failure of the fused-loss kernels on `workspace` (the loss
- * poller or a gradient-phase wait that timed out -- workgroups that could not
- * all be resident): PCM_OK or PCM_ERR_LAUNCH.  The error is sticky: every later
- * call on that workspace reports NaN means (and the failed call's NaN
- * gradients) until the caller zero-fills the workspace again.  Synchronises
- * `stream` (it reads device memory).
+ * Device-side failure of the fused-loss kernels on `workspace`: PCM_OK or
+ * PCM_ERR_LAUNCH.  A gradient-phase wait of pcm_chamfer_loss_grad that times
+ * out (workgroups that are not resident) is NOT a failure: the waiting
+ * workgroup computes the missing argmins itself, so dist/idx/gradients are
+ * exact and only time is lost.  The failure reported here is the loss poll's
+ * own wait (a much longer bound) timing out: that call's means are NaN and the
+ * error is sticky -- every later call on that workspace reports NaN means
+ * until the caller zero-fills the workspace again (the Python wrappers detect
+ * it one call later and do that, raising PcmError).  Synchronises `stream`.
  */
 int pcm_chamfer_workspace_status(const void *workspace, size_t workspace_bytes, int b, int n, int m, void *stream);
 
@@ -159,9 +162,12 @@ size_t pcm_emd_workspace_bytes(int b, int n);
 /*
  * Auction-algorithm approximate EMD (emd_cuda.cu:23-282), deterministic:
  * bidders tying within the reference's 1e-6 window resolve to the lowest
- * point index (the reference lets a racing writer win).  Requirements as the
+ * point index (the reference lets a racing writer win).  A bidder whose best
+ * value is attained by several objects bids on the one the reference's Bid
+ * finds first (emd_cuda.cu:108-110, 136-139, 165-173: the lowest (thread
+ * range, tile, index); the lowest index whenever n <= 2048).  Requirements as the
  * reference (emd_cuda.cu:236-249): both clouds [b, n, 3] (same n), b <= 512,
- * n % 1024 == 0 (any such n); iters >= 1.  Outputs dist [b, n] (squared
+ * n % 1024 == 0 (any such n up to 2^21, else PCM_ERR_UNSUPPORTED); iters >= 1.  Outputs dist [b, n] (squared
  * distance to the assigned point) and assignment [b, n] (int32; not
  * guaranteed a bijection).  `workspace` must hold pcm_emd_workspace_bytes(b, n)
  * bytes; its content on entry is irrelevant; calls that share a workspace must
@@ -173,9 +179,12 @@ int pcm_emd_forward(const float *xyz1, const float *xyz2, int b, int n, float ep
                     void *workspace, size_t workspace_bytes, void *stream);
 
 /*
- * Device-side failure of the last pcm_emd_forward on `workspace` (a bounded
- * wait between its workgroups that timed out; the outputs are then invalid):
- * PCM_OK or PCM_ERR_LAUNCH.  Synchronises `stream` (it reads device memory).
+ * Status of the last pcm_emd_forward on `workspace`; synchronises `stream`
+ * (it reads device memory).  The auction's helper workgroups take heavy
+ * iterations' full scans; a helper job whose result does not arrive within a
+ * bounded wait (helpers not resident) is scanned by the batch element's own
+ * workgroup instead, and no further jobs are posted in that call, so the
+ * outputs never depend on residency: PCM_OK unless reading the workspace fails.
  */
 int pcm_emd_workspace_status(const void *workspace, size_t workspace_bytes, int b, int n, void *stream);
 
@@ -206,9 +215,12 @@ int pcm_emd_backward(const float *xyz1, const float *xyz2, int b, int n,
  * A prep launch writes B's float32 screening rows into `workspace`
  * (pcm_icp_workspace_bytes(b, n) bytes, content on entry irrelevant); then the
  * whole loop runs in one launch (each pair's source points split over K <= 16
- * workgroups, K b <= 256, so a batch of one pair still fills 16 CUs).  Needs
- * max_iterations >= 1 (the reference fails otherwise), 0 < n <= 4096
- * (else PCM_ERR_UNSUPPORTED).  Non-finite inputs give unspecified values (the
+ * workgroups, K b <= the device's CU count, so a batch of one pair still fills
+ * 16 CUs).  Needs
+ * max_iterations >= 1 (the reference fails otherwise), 0 < n <= 16384
+ * (else PCM_ERR_UNSUPPORTED); a batch goes out in launches of at most one
+ * workgroup per compute unit (K workgroups per pair, so a pair's slices are
+ * resident together).  Non-finite inputs give unspecified values (the
  * reference's sklearn rejects them; the Python wrapper does the same).
  */
 size_t pcm_icp_workspace_bytes(int b, int m);

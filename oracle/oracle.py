@@ -48,6 +48,10 @@ def lib():
         L.pcm_oracle_emd_forward.argtypes = [_f32p, _f32p, c_int, c_int, c_float, c_int,
                                              _f32p, _i32p, ctypes.c_void_p, ctypes.c_void_p, c_int]
         L.pcm_oracle_emd_backward.argtypes = [_f32p, _f32p, c_int, c_int, _f32p, _i32p, _f32p]
+        L.pcm_oracle_emd_values.argtypes = [_f32p, _f32p, _f32p, c_int, _f32p]
+        L.pcm_oracle_emd_bid.argtypes = [_f32p, _f32p, _f32p, c_int, c_int, _i32p, _f32p, _f32p]
+        L.pcm_oracle_emd_values.restype = None
+        L.pcm_oracle_emd_bid.restype = None
         L.pcm_oracle_num_threads.restype = c_int
         for name in ("pcm_oracle_chamfer_nn", "pcm_oracle_chamfer_forward",
                      "pcm_oracle_chamfer_backward", "pcm_oracle_emd_forward",
@@ -121,6 +125,25 @@ def emd_forward(xyz1, xyz2, eps: float, iters: int, with_stats: bool = False, nt
     if with_stats:
         return dist, ass, price, hist[:iters]
     return dist, ass
+
+
+def emd_values(p, xyz2, price):
+    """Bid's value of every object for one bidder p (emd_cuda.cu:142-146)."""
+    xyz2, price = _f32(xyz2), _f32(price)
+    v = np.zeros(xyz2.shape[0], np.float32)
+    lib().pcm_oracle_emd_values(_f32(p), xyz2, price, xyz2.shape[0], v)
+    return v
+
+
+def emd_bid(p, xyz2, price, nu):
+    """One bidder's (best_i, best, better) with nu unassigned points (the
+    reference's exact-tie order, emd_cuda.cu:95-179)."""
+    xyz2, price = _f32(xyz2), _f32(price)
+    bi = np.zeros(1, np.int32)
+    b1 = np.zeros(1, np.float32)
+    b2 = np.zeros(1, np.float32)
+    lib().pcm_oracle_emd_bid(_f32(p), xyz2, price, xyz2.shape[0], int(nu), bi, b1, b2)
+    return int(bi[0]), b1[0], b2[0]
 
 
 def emd_backward(xyz1, xyz2, graddist, assignment):

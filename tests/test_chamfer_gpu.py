@@ -620,8 +620,10 @@ def test_loss_module_no_grad_skips_gradient_kernel(cuda, oracle, monkeypatch):
 
 
 def test_loss_grad_timeout_sets_sticky_error(cuda, oracle):
-    # every wait bounded to zero polls: the timeout path must be visible
-    # (sticky error word, NaN means) and a re-zeroed workspace must recover
+    # the loss poll bounded to zero polls (and every gradient-phase wait): the
+    # poll's timeout must be visible (sticky error word, NaN means) while the
+    # gradients stay exact (the waits compute missing argmins locally), and a
+    # re-zeroed workspace must recover
     import pcm_hip
     b, n, m = 32, 1024, 1024
     a, c = _clouds(123, b, n, m)
@@ -631,24 +633,110 @@ def test_loss_grad_timeout_sets_sticky_error(cuda, oracle):
     i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
     gx1, gx2 = torch.empty_like(x1), torch.empty_like(x2)
     means = torch.empty(3, device=cuda)
+    w1, w2 = np.float32(1 / (b * n)), np.float32(1 / (b * m))
     ws = torch.zeros(pcm_hip.load_library().pcm_chamfer_workspace_bytes(b, n, m), dtype=torch.uint8, device=cuda)
-    pcm_hip.tune_chamfer_loss_grad_spins(0, x1, x2, 1 / (b * n), 1 / (b * m), d1, d2, i1, i2, means, gx1, gx2, ws)
+    pcm_hip.tune_chamfer_loss_grad_spins(0, 0, x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2, ws)
     torch.cuda.synchronize()
     with pytest.raises(pcm_hip.PcmError):
         pcm_hip.chamfer_workspace_status(ws, b, n, m)
     assert torch.isnan(means).all()
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), w1, np.float32),
+                                       np.full((b, m), w2, np.float32), ref[2], ref[3])
+    np.testing.assert_array_equal(gx1.cpu().numpy().view(np.int32), gr1.view(np.int32))
+    np.testing.assert_array_equal(gx2.cpu().numpy().view(np.int32), gr2.view(np.int32))
+    assert pcm_hip.chamfer_slow_paths(ws, b, n, m) == b * 8  # every gradient workgroup took the local path
     # sticky: a normal call on the same workspace still reports NaN
-    pcm_hip.chamfer_loss_grad(x1, x2, 1 / (b * n), 1 / (b * m), d1, d2, i1, i2, means, gx1, gx2, ws)
+    pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2, ws)
     torch.cuda.synchronize()
     assert torch.isnan(means).all()
     # re-zeroed: correct again
     ws.zero_()
-    pcm_hip.chamfer_loss_grad(x1, x2, 1 / (b * n), 1 / (b * m), d1, d2, i1, i2, means, gx1, gx2, ws)
+    pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2, ws)
     torch.cuda.synchronize()
     pcm_hip.chamfer_workspace_status(ws, b, n, m)
-    r1, r2, _, _ = oracle.chamfer_forward(a.numpy(), c.numpy())
-    ref = float(r1.astype(np.float64).mean()) + float(r2.astype(np.float64).mean())
-    np.testing.assert_allclose(means[2].item(), ref, rtol=2e-6)
+    r = float(ref[0].astype(np.float64).mean()) + float(ref[1].astype(np.float64).mean())
+    np.testing.assert_allclose(means[2].item(), r, rtol=2e-6)
+
+
+@pytest.mark.parametrize("b", [32, 128])
+def test_loss_grad_local_argmins_are_exact(cuda, oracle, b):
+    # gradient-phase waits bounded to zero: every workgroup recomputes the
+    # argmins it needs instead of waiting for the workgroups that publish them
+    # (what happens when those are not resident) -- the results must not change
+    import pcm_hip
+    n = m = 1024
+    a, c = _clouds(124 + b, b, n, m)
+    x1, x2 = a.to(cuda), c.to(cuda)
+    d1, d2 = torch.empty(b, n, device=cuda), torch.empty(b, m, device=cuda)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+    gx1, gx2 = torch.empty_like(x1), torch.empty_like(x2)
+    means = torch.empty(3, device=cuda)
+    w1, w2 = np.float32(1 / (b * n)), np.float32(1 / (b * m))
+    ws = torch.zeros(pcm_hip.load_library().pcm_chamfer_workspace_bytes(b, n, m), dtype=torch.uint8, device=cuda)
+    pcm_hip.tune_chamfer_loss_grad_spins(0, 1 << 22, x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2, ws)
+    torch.cuda.synchronize()
+    pcm_hip.chamfer_workspace_status(ws, b, n, m)
+    assert pcm_hip.chamfer_slow_paths(ws, b, n, m) == b * 8
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    _assert_fwd_equal((d1.cpu().numpy(), d2.cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()), ref)
+    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), w1, np.float32),
+                                       np.full((b, m), w2, np.float32), ref[2], ref[3])
+    np.testing.assert_array_equal(gx1.cpu().numpy().view(np.int32), gr1.view(np.int32))
+    np.testing.assert_array_equal(gx2.cpu().numpy().view(np.int32), gr2.view(np.int32))
+    r = np.array([ref[0].astype(np.float64).mean(), ref[1].astype(np.float64).mean()])
+    np.testing.assert_allclose(means.cpu().numpy()[:2], r, rtol=2e-6)
+
+
+@pytest.mark.parametrize("b", [128, 512])
+def test_loss_grad_large_batch_matches_oracle(cuda, oracle, b):
+    # train.py:36's default batch (128) and the EMD limit (512): grids of
+    # b * 8 + 1 workgroups, several residency waves of the chip
+    import pcm_hip
+    n = m = 1024
+    a, c = _clouds(130 + b, b, n, m)
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    r = np.array([ref[0].astype(np.float64).mean(), ref[1].astype(np.float64).mean()])
+    o, means, (w1, w2) = _loss_grad(cuda, a, c, reps=2)
+    _assert_fwd_equal((o["d1"], o["d2"], o["i1"], o["i2"]), ref)
+    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), w1, np.float32),
+                                       np.full((b, m), w2, np.float32), ref[2], ref[3])
+    np.testing.assert_array_equal(o["g1"].view(np.int32), gr1.view(np.int32))
+    np.testing.assert_array_equal(o["g2"].view(np.int32), gr2.view(np.int32))
+    assert np.array_equal(means[0].view(np.int32), means[1].view(np.int32))
+    np.testing.assert_allclose(means[0][:2], r, rtol=2e-6)
+    assert means[0][2] == np.float32(means[0][0] + means[0][1])
+
+
+def test_wrapper_reports_and_resets_sticky_error(cuda, oracle):
+    # the wrappers' cached workspace: a timed-out loss poll (forced here) is
+    # reported by a later wrapper call (PcmError) and the workspace re-zeroed,
+    # after which the wrapper is exact again -- never silently NaN forever
+    import pcm_hip
+    b, n, m = 4, 1024, 1024
+    a, c = _clouds(125, b, n, m)
+    x1, x2 = a.to(cuda), c.to(cuda)
+    d1, d2 = torch.empty(b, n, device=cuda), torch.empty(b, m, device=cuda)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+    gx1, gx2 = torch.empty_like(x1), torch.empty_like(x2)
+    means = torch.empty(3, device=cuda)
+    w1, w2 = 1 / (b * n), 1 / (b * m)
+    pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2)
+    ws = pcm_hip.chamfer_workspace(cuda, b, n, m)
+    pcm_hip.tune_chamfer_loss_grad_spins(1 << 16, 0, x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2, ws)
+    pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2)  # sticky: NaN
+    torch.cuda.synchronize()
+    assert torch.isnan(means).all()
+    with pytest.raises(pcm_hip.PcmError):
+        pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2)
+    pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2)
+    torch.cuda.synchronize()
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    r = float(ref[0].astype(np.float64).mean()) + float(ref[1].astype(np.float64).mean())
+    np.testing.assert_allclose(means[2].item(), r, rtol=2e-6)
+    pcm_hip.chamfer_workspace_status(ws, b, n, m)
 
 
 def test_loss_function_scales_upstream_gradient(cuda):

@@ -70,6 +70,32 @@ def test_emd_large_n_matches_oracle(cuda, oracle, b, n, eps, iters, seed):
     np.testing.assert_array_equal(price.view(np.int32), rp.view(np.int32))
 
 
+@pytest.mark.parametrize("b,n,eps,iters,seed", [
+    (2, 4096, 0.05, 400, 40),
+    (1, 8192, 0.05, 300, 41),
+    (2, 3072, 0.01, 500, 42),     # a half-width last tile (its own thread ranges)
+])
+def test_emd_exact_ties_follow_reference_order(cuda, oracle, b, n, eps, iters, seed):
+    # n > 2048: the reference splits each 2048-object tile over a bidder's
+    # threads, so among EXACTLY equal values the winner is the lowest (thread
+    # range, tile, k), not the lowest k (emd_cuda.cu:108-110, 136-139, 165-173;
+    # oracle pinned by tests/test_oracle_props.py).  Duplicated targets with
+    # bidders sitting on them make such ties at the best in many iterations.
+    g = torch.Generator().manual_seed(seed)
+    a = torch.rand(b, n, 3, generator=g)
+    c = torch.rand(b, n, 3, generator=g)
+    src = torch.randperm(n, generator=g)[: n // 4]
+    dst = torch.randperm(n, generator=g)[: n // 4]
+    c[:, dst] = c[:, src]
+    on = torch.randperm(n, generator=g)[: n // 8]
+    a[:, on] = c[:, dst[: n // 8]]
+    dist, ass, price = _run(a, c, eps, iters, cuda)
+    rd, ra, rp, _ = oracle.emd_forward(a.numpy(), c.numpy(), eps, iters, with_stats=True)
+    np.testing.assert_array_equal(ass, ra)
+    np.testing.assert_array_equal(dist.view(np.int32), rd.view(np.int32))
+    np.testing.assert_array_equal(price.view(np.int32), rp.view(np.int32))
+
+
 def _generator_like(seed, b, n):
     """Clustered predictions against uniform ground truth: the shape of a
     random-init generator's output (tests/test_train_gpu.py), where most bids
@@ -106,6 +132,39 @@ def test_emd_helper_configs_match_oracle(cuda, oracle, helpers, offload_min, tai
         assert st[2 * 400 + 10] > 0, "no job was offloaded"
     if helpers == 0:
         assert st[2 * 400 + 10] == 0
+
+
+@pytest.mark.parametrize("b,n,helpers", [(4, 1024, 15), (2, 4096, -1)])
+def test_emd_helper_timeout_is_exact(cuda, oracle, b, n, helpers):
+    # every wait between the auction's workgroups bounded to zero polls: the
+    # helpers leave at once and the master times out on every job it posts,
+    # scanning those items itself (region A) -- assignment, dist and price must
+    # not change, in the LDS-state form (n = 1024) and the workspace-state form
+    # (n = 4096); the timeout is only a diagnostic
+    import pcm_hip
+    a, c = _generator_like(25 + n, b, n)
+    x1, x2 = a.to(cuda), c.to(cuda)
+    dist = torch.empty(b, n, device=cuda)
+    ass = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    price = torch.empty(b, n, device=cuda)
+    ws = pcm_hip.emd_workspace(cuda, b, n)
+    iters = 300
+    stats = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=cuda)
+    pcm_hip.emd_forward(x1, x2, 0.05, iters, dist, ass, price, workspace=ws, helpers=helpers, offload_min=0,
+                        stats=stats, spin_limit=0)
+    torch.cuda.synchronize()
+    assert stats.cpu().numpy()[2 * iters + 10] > 0, "no job was posted"
+    assert pcm_hip.emd_timeouts(ws, b, n) > 0
+    pcm_hip.emd_workspace_status(ws, b, n)  # a timeout is not an error
+    rd, ra, rp, _ = oracle.emd_forward(a.numpy(), c.numpy(), 0.05, iters, with_stats=True)
+    np.testing.assert_array_equal(ass.cpu().numpy(), ra)
+    np.testing.assert_array_equal(dist.cpu().numpy().view(np.int32), rd.view(np.int32))
+    np.testing.assert_array_equal(price.cpu().numpy().view(np.int32), rp.view(np.int32))
+    # the same workspace, default bounds: no timeout, same result
+    pcm_hip.emd_forward(x1, x2, 0.05, iters, dist, ass, price, workspace=ws)
+    torch.cuda.synchronize()
+    assert pcm_hip.emd_timeouts(ws, b, n) == 0
+    np.testing.assert_array_equal(ass.cpu().numpy(), ra)
 
 
 def _reserve_cases():

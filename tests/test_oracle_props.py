@@ -91,3 +91,57 @@ def test_emd_backward_formula(oracle):
     g = oracle.emd_backward(a, q, gd, ass)
     ref = 2 * gd[..., None] * (a - np.take_along_axis(q, ass[..., None].astype(np.int64), axis=1))
     np.testing.assert_allclose(g, ref, rtol=1e-6, atol=1e-9)
+
+
+def _reference_bid(v, nu):
+    """emd_cuda.cu:103-176 for ONE bidder, literally: tpu threads, each scans
+    its [l, r) range of every 2048-object tile with the strict '>' top-2
+    update (:136-155), then thread 0 merges the others in thread order
+    (:165-173).  v: the bidder's values (the oracle's, emd_cuda.cu:146)."""
+    n = v.shape[0]
+    block_cnt = n // 1024
+    upb = (nu + block_cnt - 1) // block_cnt
+    tpu = 1024 // upb
+    best = [np.float32(-1e9)] * tpu
+    better = [np.float32(-1e9)] * tpu
+    best_i = [-1] * tpu
+    for k2 in range(0, n, 2048):
+        end_k = min(n, k2 + 2048) - k2
+        delta = (end_k + tpu - 1) // tpu
+        for t in range(tpu):
+            for k in range(t * delta, min((t + 1) * delta, end_k)):
+                d = v[k + k2]
+                if d > best[t]:
+                    better[t], best[t], best_i[t] = best[t], d, k + k2
+                elif d > better[t]:
+                    better[t] = d
+    b, bb, bi = best[0], better[0], best_i[0]
+    for t in range(1, tpu):
+        if best[t] > b:
+            bb = max(b, better[t])
+            b, bi = best[t], best_i[t]
+        else:
+            bb = max(bb, best[t])
+    return bi, b, bb
+
+
+@pytest.mark.parametrize("n,nu", [(4096, 1), (4096, 5), (4096, 700), (4096, 2049), (4096, 4096), (3072, 3),
+                                  (3072, 900), (8192, 17), (2048, 1), (1024, 1)])
+def test_emd_bid_tie_order_matches_reference_threads(oracle, n, nu):
+    # duplicated targets give exact value ties between objects in different
+    # tiles and thread ranges: the oracle's winner must be the reference's
+    # (lowest (thread, tile, k)), and the values its top two
+    rng = np.random.default_rng(n + nu)
+    q = rng.random((n, 3), dtype=np.float32)
+    src = rng.permutation(n)[:64]
+    q[rng.permutation(n)[:64]] = q[src]          # twins at random offsets
+    q[rng.permutation(n)[:n // 8]] = q[7]        # and a crowd of copies of object 7
+    price = np.zeros(n, np.float32)
+    price[rng.permutation(n)[:n // 4]] = np.float32(0.01)
+    for trial in range(24):
+        p = (q[7] if trial % 4 == 3 else q[src[trial]]) if trial % 2 else rng.random(3, dtype=np.float32)
+        v = oracle.emd_values(p, q, price)
+        ref = _reference_bid(v, nu)
+        got = oracle.emd_bid(p, q, price, nu)
+        assert got[0] == ref[0], (trial, got, ref)
+        assert got[1] == ref[1] and got[2] == ref[2]

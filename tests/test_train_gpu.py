@@ -59,6 +59,33 @@ def test_train_step_losses_match_oracle(cuda, oracle, epoch, channels_last):
     assert all(p.grad is None for p in step.gen.edge1.parameters())
 
 
+@pytest.mark.parametrize("epoch", [1, 31])
+def test_train_step_config4_workload_matches_oracle(cuda, oracle, epoch):
+    # BASELINE config 4 at its stated per-GPU workload: train.py:36's batch of
+    # 128 over 8 GPUs = 16 clouds, EMD at loss/loss.py:23's eps 0.05 / 3000
+    # iterations (TrainStep's defaults); epoch 1 trains on CD + EMD, epoch 31
+    # on EMD alone (train.py:162-169).  Losses equal the oracle's on the clouds
+    # the step's own forward produced.
+    import train_step as T
+    step = T.TrainStep(device=cuda, seed=3)
+    assert step.emd_eps == 0.05 and step.emd_iters == 3000
+    step.set_epoch(epoch)
+    images, points = T.synthetic_batch(16, 1024, cuda, seed=6)
+    cap = []
+    hook = step.gen.register_forward_hook(lambda m, i, o: cap.append(o[2].detach().transpose(2, 1).contiguous()))
+    logged = step(images, points, epoch).cpu().numpy()
+    hook.remove()
+    p, q = cap[0].cpu().numpy(), points.cpu().numpy()
+    d1, d2, _, _ = oracle.chamfer_forward(p, q)
+    cd = float(d1.astype(np.float64).mean() + d2.astype(np.float64).mean())
+    ed, _ = oracle.emd_forward(p, q, 0.05, 3000)
+    emd = float(np.sqrt(ed.astype(np.float64)).mean())
+    assert logged[1] == pytest.approx(cd, rel=1e-5)
+    assert logged[2] == pytest.approx(emd, rel=1e-5)
+    w = T.loss_weights(epoch, 100.0, 100.0)
+    assert logged[0] == pytest.approx(w[0] * cd + w[1] * emd, rel=1e-5)
+
+
 @pytest.mark.parametrize("iters", [50, 400])
 def test_emd_training_setting_wide_clouds(cuda, oracle, iters):
     """EMD at the training call's eps (loss/loss.py:23) on predictions spread

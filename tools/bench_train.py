@@ -23,6 +23,7 @@ import torch.distributed as dist
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "train"))
+sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric"))
 import train_step as T  # noqa: E402
 
 
@@ -95,16 +96,44 @@ def main():
     torch.cuda.synchronize()
     loss_ms = e0.elapsed_time(e1) / reps
 
+    # per-step record: each step trains the generator, so the next step's
+    # predictions -- and the EMD auction's work on them -- differ.  Events
+    # time every step (no host sync); a forward hook keeps each step's
+    # predicted clouds (one small copy) so the auction's iterations and bids
+    # per step are counted afterwards, outside the timed region.
+    caps = []
+    hook = step.gen.register_forward_hook(
+        lambda m, i, o: caps.append(o[2].detach().transpose(2, 1).contiguous()))
+    sev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    sev[0].record()
+    for i in range(args.steps):
         logged = step(images, points, args.epoch)
+        sev[i + 1].record()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    hook.remove()
+    step_ms = [sev[i].elapsed_time(sev[i + 1]) for i in range(args.steps)]
+    emd_work = []
+    import pcm_hip
+    b, n = points.shape[0], points.shape[1]
+    for pred_i in caps:
+        st = torch.zeros(3 * args.emd_iters + 16 + b, dtype=torch.int32, device=dev)
+        d = torch.empty(b, n, device=dev)
+        a_ = torch.empty(b, n, dtype=torch.int32, device=dev)
+        pcm_hip.emd_forward(pred_i, points.contiguous(), args.emd_eps, args.emd_iters, d, a_, stats=st, diag=1)
+        e0.record()
+        pcm_hip.emd_forward(pred_i, points.contiguous(), args.emd_eps, args.emd_iters, d, a_)
+        e1.record()
+        torch.cuda.synchronize()
+        h = st.cpu()[:2 * args.emd_iters].view(-1, 2)
+        emd_work.append({"iterations_with_bidders": int((h[:, 0] > 0).sum()), "bids": int(h[:, 0].sum()),
+                         "full_scans": int(h[:, 1].sum()), "emd_fwd_ms": e0.elapsed_time(e1)})
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -124,6 +153,7 @@ def main():
                        "bucket_cap_mb": args.bucket_mb,
                        "channels_last": args.channels_last},
             "phases_ms": phases, "loss_path_ms": loss_ms, "loss_path_share": loss_ms / ms,
+            "per_step": [dict(step_ms=t, **w_) for t, w_ in zip(step_ms, emd_work)],
             "last_losses": {"total": vals[0], "chamfer": vals[1], "emd": vals[2]},
         }))
     if world > 1:

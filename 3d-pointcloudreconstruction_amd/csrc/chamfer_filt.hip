@@ -1291,7 +1291,8 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
 #pragma unroll
             for (int r = 0; r < kPerS; ++r) ready &= (unsigned)(gr[r] >> 32) == want;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (and the caller's LDS-DMA has landed)
-            if (!__syncthreads_or(ready ? 0 : 1)) break;
+            const int waiting = __syncthreads_or(ready ? 0 : 1);
+            if (!waiting && max_spins != 0u) break;
             if (spins >= max_spins) {
                 // uniform (every thread saw the same vote): the workgroups
                 // that owe these argmins are not running yet (not resident,

@@ -893,12 +893,26 @@ __device__ __noinline__ int cache_tie_winner(const centry *cj, bool sc1, const f
 // A bid on object k.  Maxima persisted from earlier iterations are <= 0
 // (0 initially, -1e9 once assigned), and with eps > 0 every increment is > 0,
 // so an old maximum above 0 means a second bid on k in this iteration: the
-// claim phase is needed only when some object saw that (*coll).
+// claim phase is needed only when some object saw that (coll[0]).
+//
+// The claim phase itself is needed only when a bidder other than the maximum's
+// holder lies inside GetMax's 1e-6 window of the maximum (emd_cuda.cu:188):
+// otherwise the holder -- the bidder whose increment equals the maximum --
+// wins.  Every such pair is seen by one of its two atomicMax calls: a bidder
+// arriving after the holder gets the maximum back; a holder arriving after
+// it gets back an earlier maximum that lies between the two increments.  So
+// coll[1] is raised (conservatively, 2e-6) whenever an atomicMax returns a
+// same-iteration value that close to the caller's increment; equal
+// increments raise it too.
 template <bool kG>
 __device__ __forceinline__ void bid_on(const AState<kG> &st, int j, int k, float inc, int *coll) {
     st.bid[j] = k;
     st.inc[j] = inc;
-    if (atomicMax(&st.mx[k], f2key(inc)) > 0) *coll = 1;
+    const int old = atomicMax(&st.mx[k], f2key(inc));
+    if (old > 0) {
+        coll[0] = 1;
+        if (fabs((double)inc - (double)key2f(old)) <= 2e-6) coll[1] = 1;
+    }
 }
 
 // resT/resN (reserve form, else null): a miss whose cache bound is not above
@@ -1091,7 +1105,7 @@ __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank
 // master role: the auction of one batch element
 template <bool kG, bool kStage, bool kStageP, int kN>
 __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *smem) {
-    __shared__ int sNu[2], sNm, sColl, sChainJ;
+    __shared__ int sNu[2], sNm, sColl[2], sChainJ;  // sColl: [0] some object saw 2 bids, [1] a window contention
     __shared__ float sPb1[kWaves], sPb2[kWaves];  // split bids: each wave's part
     __shared__ int sPkb[kWaves];
     const int n = kN > 0 ? kN : a.n, iters = a.iters;
@@ -1157,7 +1171,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             sRN[j] = res_on ? ws.RN[base + j] : 0;
         }
     }
-    if (tid == 0) { sNu[0] = n; sNu[1] = 0; sNm = 0; sColl = 0; }
+    if (tid == 0) { sNu[0] = n; sNu[1] = 0; sNm = 0; sColl[0] = sColl[1] = 0; }
     vm_drain();  // the DMA has landed
     __syncthreads();
 
@@ -1211,7 +1225,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         if (lane == 0) {
             if (rb.ok) {
                 CT[j] = rb.T;
-                place_bid(st, j, rb.kb, rb.b1 - rb.b2 + eps, n, &sColl);
+                place_bid(st, j, rb.kb, rb.b1 - rb.b2 + eps, n, sColl);
                 st.miss[q] = -1;
                 if (hist) atomicAdd(&a.stats[2 * iters + 13], 1);  // reserve bids
             } else {
@@ -1242,12 +1256,15 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         kb = tie_fix<kG>(kb, b1, b2, x1, y1, z1, Qc, st.price, n, tr);
         if (lane == 0) {
             CT[j] = T;
-            place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
+            place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
         }
     };
     int active = 0, chain_its = 0, tail_its = 0;
     for (int it = 0; it < iters; ++it) {
         const bool last = (it == iters - 1);
+        // timers: this iteration's start (cycles) and B1 total so far
+        unsigned long long it_t0 = 0, it_b1 = 0;
+        if (timers) { it_t0 = __builtin_amdgcn_s_memtime(); it_b1 = sTm[0]; }
         const int cur = it & 1;
         const int nu = sNu[cur];
         if (nu == 0) break;  // nothing left to bid: later iterations are no-ops
@@ -1338,7 +1355,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     int kb;
                     part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, 0, 1, b1, kb, b2);
                     kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, tr);
-                    if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
+                    if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
                 }
             } else if (q < nu) {
                 const int j = Ucur[q];
@@ -1358,7 +1375,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 part_merge(sPb1 + wave, sPkb + wave, sPb2 + wave, W, b1, kb, b2);
                 const int j = Ucur[q];
                 kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, tr);
-                if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
+                if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
             }
             __syncthreads();
             PCM_EMD_PHASE(1);
@@ -1369,7 +1386,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 const int j = Ucur[u];
                 const int k = ws.bid0[base + j];
                 if (k >= 0) {
-                    bid_on(st, j, k, ws.inc0[base + j], &sColl);
+                    bid_on(st, j, k, ws.inc0[base + j], sColl);
                 } else {
                     st.miss[atomicAdd(&sNm, 1)] = j;
                 }
@@ -1380,9 +1397,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             const int G = cache_bid_lanes(nu);
             const float *rT = kRes ? sRT : nullptr;
             int *rN = kRes ? sRN : nullptr;
-            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN, n, tr);
-            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN, n, tr);
-            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, &sColl, rT, rN, n, tr);
+            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr);
+            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr);
+            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr);
         }
         __syncthreads();
         PCM_EMD_PHASE(0);
@@ -1435,7 +1452,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     }
                     if (late) continue;
                     CT[j] = __uint_as_float(kInB);
-                    place_bid(st, j, ld_sc1(ws.rbid + base + i), ld_sc1(ws.rinc + base + i), n, &sColl);
+                    place_bid(st, j, ld_sc1(ws.rbid + base + i), ld_sc1(ws.rinc + base + i), n, sColl);
                     st.miss[i] = -1 - j;
                 }
                 if (__syncthreads_or(late ? 1 : 0)) {
@@ -1497,7 +1514,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                         kb = tie_fix<kG>(kb, b1, b2, x1, y1, z1, Qc, st.price, n, tr);
                         if (lane == 0) {
                             CT[j] = T;
-                            place_bid(st, j, kb, b1 - b2 + eps, n, &sColl);
+                            place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
                         }
                         PCM_EMD_PHASE(7);
                     }
@@ -1512,8 +1529,11 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         //      (emd_cuda.cu:181-194); the key carries the iteration.  Skipped
         //      when every bid object has a single bidder (it then wins).
         const ckey itag = (ckey)(~(unsigned)it) << 32;
-        const bool solo = sColl == 0 && eps > 0.f;
-        if (!last && !solo) {
+        // solo: no object saw two bids; by_max: no bidder other than the
+        // maximum's holder inside the window (see bid_on) -- the holder wins
+        const bool solo = sColl[0] == 0 && eps > 0.f;
+        const bool by_max = sColl[1] == 0 && eps > 0.f;
+        if (!last && !by_max) {
             for (int u = tid; u < nu; u += kEmdThreads) {
                 const int j = Ucur[u];
                 const int k = st.bid[j];
@@ -1540,7 +1560,8 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     push = j;  // no bid: stays unassigned
                 } else if (last) {
                     st.ass[j] = k;
-                } else if (solo || st.ld_claim(k) == (itag | (unsigned)j)) {
+                } else if (solo || (by_max ? st.inc[j] == key2f(st.ld_max(k))
+                                           : st.ld_claim(k) == (itag | (unsigned)j))) {
                     const int old = st.inv[k];
                     if (old != -1) { st.ass[old] = -1; push = old; }
                     st.inv[k] = j;
@@ -1551,7 +1572,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     push = j;  // outbid
                 }
             }
-            if (tid == 0) { sNm = 0; sColl = 0; }  // read before the last barrier
+            if (tid == 0) { sNm = 0; sColl[0] = sColl[1] = 0; }  // read before the last barrier
             if (!last) {
                 const unsigned long long bal = __ballot(push >= 0);
                 int pos = 0;
@@ -1562,6 +1583,11 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         }
         __syncthreads();
         PCM_EMD_PHASE(3);
+        if (timers) {  // per iteration: cycles / 16, B1 cycles / 16, bidders
+            a.stats[2 * it] = (int)((__builtin_amdgcn_s_memtime() - it_t0) >> 4);
+            a.stats[2 * it + 1] = (int)((sTm[0] - it_b1) >> 4);
+            a.stats[2 * iters + 16 + it] = nu;
+        }
     }
 #undef PCM_EMD_PHASE
     if (a.H > 0 && tid == 0) st_sc1(bw + kBoardQuit, 1);  // helpers exit

@@ -42,8 +42,15 @@ def main():
     st = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=dev)
     pcm_hip.emd_forward(x1, x2, eps, iters, d, a, stats=st, diag=2 + slow)
     torch.cuda.synchronize()
-    tm = st.cpu()[2 * iters:2 * iters + 15].tolist()
+    stc = st.cpu()
+    tm = stc[2 * iters:2 * iters + 15].tolist()
     act = max(tm[12], 1)
+    if "--per-iter" in sys.argv:  # cycles per iteration of the slowest element (x16 units)
+        for it in range(iters):
+            nu = int(stc[2 * iters + 16 + it])
+            if nu == 0 and int(stc[2 * it]) == 0:
+                continue
+            print(f"    it {it:4d} bidders {nu:5d} cycles {16 * int(stc[2 * it]):7d} bids(B1) {16 * int(stc[2 * it + 1]):7d}")
     print(f"  slowest element {slow}: {act} iterations; cycles/iteration "
           + ", ".join(f"{nm}={16.0 * v / act:.0f}" for nm, v in zip(T.TIMERS, tm[:12])))
     print(f"  forward {T.timed(x1, x2, eps, iters, d, a, None, None, reps=20):.1f} us", flush=True)

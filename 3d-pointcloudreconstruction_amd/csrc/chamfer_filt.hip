@@ -75,11 +75,22 @@ __device__ unsigned long long g_pcm_stamps[kStampSlots * 8];
 
 // The workgroup's LDS arena: one static array per size, shared by every
 // phase of a kernel that asks for the same size.
-template <int kBytes>
+template <int kBytes, int kTag = 0>
 __device__ __forceinline__ unsigned char *lds_arena() {
     __shared__ __attribute__((aligned(16))) unsigned char arena[kBytes];
     return arena;
 }
+
+// an LDS-DMA issued by filt_forward once its first target tile is staged:
+// the copy lands while the scan runs (the scan makes no global loads)
+struct PreDma {
+    void *dst1;
+    const void *src1;
+    int bytes1;
+    void *dst2;
+    const void *src2;
+    int bytes2;
+};
 
 // Arena bytes of the filtered forward: the scan tile (u, w), then -- after the
 // scan, in the same bytes -- the raw target cloud (single-tile clouds) and the
@@ -156,7 +167,8 @@ __device__ __forceinline__ void filt_group4(float (&mn)[4], const pcm_f2 (&px)[4
 template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1>
 __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const TIn *__restrict__ T, int nq, int nt, int qbase,
                               float *__restrict__ D, int32_t *__restrict__ I, unsigned char *arena,
-                              unsigned long long *__restrict__ Gr = nullptr, unsigned long long tag = 0) {
+                              unsigned long long *__restrict__ Gr = nullptr, unsigned long long tag = 0,
+                              const PreDma *pre = nullptr) {
     static_assert(C % 4 == 0 && TILE % C == 0, "tile must hold whole chunks of 4-candidate groups");
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
@@ -293,6 +305,10 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         }
         __syncthreads();
         if (t0 == 0) PCM_STAMP(2);
+        if (t0 == 0 && pre) {
+            pcm_dma_to_lds(pre->dst1, pre->src1, pre->bytes1, wave, W);
+            pcm_dma_to_lds(pre->dst2, pre->src2, pre->bytes2, wave, W);
+        }
 
         const int nch = padded / C;
         const int gc0 = t0 / C;
@@ -408,8 +424,22 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             for (int qq = 0; qq < QPT; ++qq)
                 if (qq == wave)
                     qn2 = __builtin_fmaf(pz[qq].x, pz[qq].x, __builtin_fmaf(py[qq].x, py[qq].x, px[qq].x * px[qq].x));
-            const float rr = __builtin_sqrtf(rmax2) + __builtin_sqrtf(qn2);
-            const float e2 = 2.f * kFiltU16 * (rr * rr) * 1.001f;
+            // the bound E = 16u (|t'| + |q'|)^2 of a target t: with R = max |t'|
+            // (eR) for every target; but a target that can reach the best
+            // chunk's exact minimum d_b lies within sqrt(d_b) of q, so
+            // |t'| <= |q'| + sqrt(d_b), and d_b <= fb + |q'|^2 + eR (= db,
+            // rounded up): for every target that matters -- the best chunk's
+            // argmin included -- E <= 16u (2|q'| + sqrt(db))^2.  If the
+            // other chunks' best exceeds fb by twice the smaller bound, no
+            // target outside the best chunk can reach d_b (the ICP screen's
+            // argument, csrc/icp.hip).  Near ties: 0.12 % of random queries
+            // with eR alone.
+            const float sq = __builtin_sqrtf(qn2);
+            const float rr = __builtin_sqrtf(rmax2) + sq;
+            const float eR = kFiltU16 * (rr * rr) * 1.001f;
+            const float db = __builtin_fmaxf((fb + qn2) * 1.0001f + 2.f * eR, 0.f);
+            const float rq = 2.f * sq + __builtin_sqrtf(db);
+            const float e2 = 2.f * kFiltU16 * __builtin_fminf(rr * rr, rq * rq) * 1.001f;
             const bool proven = (fs - fb) > e2;  // false for NaN
             sFc[tid] = proven ? fc : -1;
         }
@@ -1555,7 +1585,7 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
     }
 }
 
-template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false>
+template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -1565,7 +1595,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     constexpr int NT = 64 * W;
     static_assert(!kMfma || (W == 8 && QPT == 4 && TILE == kMfmaTile), "the MFMA forward's fixed geometry");
     constexpr int kFwd = kMfma ? MfmaLds::kBytes : FiltLds<W, QPT, TILE>::kBytes;
-    constexpr int kArena = kFwd > kGradBytes ? kFwd : kGradBytes;
+    // kEarly: the gradient phase's clouds get an LDS region of their own, so
+    // their copy is issued before the scan instead of after the forward
+    constexpr int kArena = kEarly ? kFwd : (kFwd > kGradBytes ? kFwd : kGradBytes);
+    static_assert(!kEarly || kGran, "early cloud copy: granule hand-off form");
     static_assert(QW <= NT, "one target per thread in the gradient phase");
     __shared__ float sRed[16];
     __shared__ int sFlag, sLate;
@@ -1573,6 +1606,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int lane = tid & 63;
     const int wave = tid >> 6;
     unsigned char *arena = lds_arena<kArena>();
+    unsigned char *garena = kEarly ? lds_arena<kGradBytes, 1>() : arena;  // gradient phase
     const int nprod = (int)gridDim.x - 1;
     if ((int)blockIdx.x == nprod) {
         PCM_STAMP2(5);
@@ -1598,10 +1632,12 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         // {tag, sum} granule; the gradient phase sweeps the granules it needs
         const unsigned long long tag = (unsigned long long)(ws.epoch[0] + 1u) << 32;
         unsigned long long *G1 = ws.ig + (size_t)batch * n, *G2 = ws.ig + (size_t)b * n + (size_t)batch * m;
+        const PreDma pre{garena, X1, 12 * n, garena + 12 * kGradCap, X2, 12 * m};
         const float my_d = filt_forward<float, W, QPT, C, TILE, false>(
             first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
             first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
-            first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, first ? G1 : G2, tag);
+            first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, first ? G1 : G2, tag,
+            kEarly ? &pre : nullptr);
         PCM_STAMP2(1);
         const float s = wave_sum(my_d);
         if (lane == 0) sRed[wave] = s;
@@ -1612,19 +1648,21 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
             __hip_atomic_store(ws.wg + bid, tag | __float_as_uint(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         // the batch element's clouds for the gradient phase (the arena is free);
-        // they land during the sweep
-        pcm_dma_to_lds(arena, X1, 12 * n, wave, W);
-        pcm_dma_to_lds(arena + 12 * kGradCap, X2, 12 * m, wave, W);
+        // they land during the sweep (kEarly: issued before the scan)
+        if constexpr (!kEarly) {
+            pcm_dma_to_lds(arena, X1, 12 * n, wave, W);
+            pcm_dma_to_lds(arena + 12 * kGradCap, X2, 12 * m, wave, W);
+        }
         PCM_STAMP2(2);
         float *G = first ? grad1 + (size_t)batch * n * 3 : grad2 + (size_t)batch * m * 3;
-        const float *P1 = reinterpret_cast<const float *>(arena);
+        const float *P1 = reinterpret_cast<const float *>(garena);
         const float *P2 = P1 + 3 * kGradCap;
         const float g1 = __fmul_rn(w1, 2.f), g2 = __fmul_rn(w2, 2.f);
         const bool ok = first ? range_grad<NT, QW, true>(true, q0, n, m, P1, P2, g1, g2, nullptr, nullptr, G,
-                                                          arena + 24 * kGradCap, G1, G2, tag, max_spins,
+                                                          garena + 24 * kGradCap, G1, G2, tag, max_spins,
                                                           ws.epoch + kGradSlowWord)
                               : range_grad<NT, QW, true>(false, q0, m, n, P2, P1, g2, g1, nullptr, nullptr, G,
-                                                          arena + 24 * kGradCap, G2, G1, tag, max_spins,
+                                                          garena + 24 * kGradCap, G2, G1, tag, max_spins,
                                                           ws.epoch + kGradSlowWord);
         if (!ok) {  // a workgroup of this element never published: sticky error, NaN gradients
             if (tid == 0) __hip_atomic_store(ws.epoch + kGradErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1779,6 +1817,7 @@ const GradVariant kGradVariants[] = {
     {chamfer_loss_grad_kernel<16, 4, 32, 1024>, 16, 4},  // 5
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, true>, 8, 4},  // 6: screen on the matrix cores
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true>, 8, 4},  // 7: granule hand-off
+    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, true>, 8, 4},  // 8: 7 + the clouds copied during the scan
 };
 constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
 // tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,
@@ -1802,6 +1841,14 @@ long long grad_blocks_max(int b, int n, int m) {
     }
     return most;
 }
+
+// variant 8 holds ~108 KB of LDS (one workgroup per CU): the default while
+// the grid is one residency wave of the device, variant 7 (64 KB, two per CU)
+// beyond
+// variant 8 (DMA issued before the scan) measured 0.4 us slower than 7 at the
+// benchmark size (r03h: 15.4 vs 15.0 us; the early copies slow the scan more
+// than they shorten the wait), so the default stays 7 at every size
+int default_grad_variant(int, int, int) { return kDefaultGradVariant; }
 
 int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, int n, int m, float w1, float w2,
                      float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out, float *grad1,
@@ -1839,7 +1886,7 @@ extern "C" int pcm_chamfer_loss_grad(const float *xyz1, const float *xyz2, int b
                                      float w2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                      float *mean_out, float *gradxyz1, float *gradxyz2, void *workspace,
                                      size_t workspace_bytes, void *stream) {
-    return launch_loss_grad(kDefaultGradVariant, xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out,
+    return launch_loss_grad(default_grad_variant(b, n, m), xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out,
                             gradxyz1, gradxyz2, workspace, workspace_bytes, stream);
 }
 
@@ -1861,7 +1908,7 @@ extern "C" int pcm_tune_chamfer_loss_grad_spins(unsigned wait_spins, unsigned po
                                                 float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                                 float *mean_out, float *gradxyz1, float *gradxyz2, void *workspace,
                                                 size_t workspace_bytes, void *stream) {
-    return launch_loss_grad(kDefaultGradVariant, xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out,
+    return launch_loss_grad(default_grad_variant(b, n, m), xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out,
                             gradxyz1, gradxyz2, workspace, workspace_bytes, stream, wait_spins, poll_spins);
 }
 

@@ -64,12 +64,15 @@ namespace {
 constexpr int kL = 64;               // cache slots per point (unused slots: id -1)
 constexpr int kSelectSteps = 8;      // bisection steps when > kL entries clear K3
 constexpr int kSectionSteps = 4;     // quarter-section steps of the reserve thresholds (1/256 of the range)
-constexpr int kSeedThreads = 256;    // 4 waves
+#ifndef PCM_SEED_THREADS
+#define PCM_SEED_THREADS 256
+#endif
+constexpr int kSeedThreads = PCM_SEED_THREADS;  // 4 waves
 constexpr int kSeedPtsPerWave = 1;   // 4 points per seed workgroup (2: seed 2.2 us slower at config 3, 4: 3.9 us, 8: 15 us)
 constexpr int kSeedPts = kSeedThreads / 64 * kSeedPtsPerWave;
 constexpr int kEmdThreads = 1024;    // auction workgroup (16 waves)
 constexpr int kWaves = kEmdThreads / 64;
-constexpr int kLdsStateMaxN = 2048;  // master state in LDS up to here (44 B x n)
+constexpr int kLdsStateMaxN = 2048;  // master state in LDS up to here (48 B x n)
 constexpr int kStageMaxN = 8192;     // target cloud copied to LDS up to here (12 B x n)
 constexpr int kHelperMaxN = 32768;   // helpers keep a price snapshot in LDS (4 B x n)
 constexpr int kMaxHelpers = 31;
@@ -78,6 +81,10 @@ constexpr int kSpinLimit = 1 << 22;  // bounded polls (sticky error word on time
 constexpr int kStagePN = 1024;          // the n of the LDS-state, staged-bidder auction form
 constexpr int kDefaultOffloadMin = 24;  // misses above which an iteration is offloaded
 constexpr int kDefaultTailMax = 16;     // bidders at or below which an iteration runs in tail mode
+#ifndef PCM_CHAIN_W
+#define PCM_CHAIN_W 16
+#endif
+constexpr int kChainW = PCM_CHAIN_W;    // waves a chain-mode bid is split over
 constexpr int kDefaultWsplit = 1;       // most waves one miss's scan is split over (2, 4: measured slower at config 3 and the training call)
 // Reserve (n == kStagePN): every object closer than a radius, built by the
 // seed at zero prices, up to kR entries of {object id, d}.  Radius^2 starts at
@@ -135,33 +142,33 @@ __device__ __forceinline__ float value_of(float d, float price) {
     return value_from_s(__builtin_sqrtf(d), price);  // correctly rounded sqrtf
 }
 
-// ---- DPP cross-lane steps (VALU operand modifiers: no LDS crossbar round trip).
-// Lanes the DPP pattern does not feed keep their own value (old = self), so a
-// combine with it is a no-op for idempotent selections.  Hillis-Steele:
-// row_shr 1,2,4,8 leaves each 16-lane row's result in its lane 15; row_bcast
-// 15 and 31 then carry it across rows so lane 63 holds the wave's result.
-constexpr int kDppRowShr1 = 0x111, kDppRowShr2 = 0x112, kDppRowShr4 = 0x114, kDppRowShr8 = 0x118;
-constexpr int kDppRowBcast15 = 0x142, kDppRowBcast31 = 0x143;
+// ---- DPP cross-lane steps (VALU operand modifiers: no LDS crossbar round
+// trip).  Hillis-Steele: row_shr 1,2,4,8 leaves each 16-lane row's result in
+// its lane 15; row_bcast 15 and 31 then carry it across rows so lane 63 holds
+// the wave's result.
 
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ int dpp_i(int x) {
-    return __builtin_amdgcn_update_dpp(x, x, CTRL, ROWMASK, 0xf, false);
+// full-wave reductions: result returned wave-uniform (read from lane 63).
+// Each Hillis-Steele step is ONE v_{max,min}_i32_dpp: a lane the pattern
+// does not feed is not written (no bound_ctrl), so it keeps its own value --
+// an idempotent no-op.  Written as inline asm: through update_dpp + fmaxf
+// hipcc emitted a mov_dpp, a canonicalising max and the max for every step.
+// s_nop 1 before each step: a DPP read of a VGPR the previous VALU
+// instruction wrote needs two wait states (asm is not hazard-checked).
+#define PCM_WAVE_RED_STEPS(OP)                                                   \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"   \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+__device__ __forceinline__ int wave_max_i(int v) {
+    asm volatile(PCM_WAVE_RED_STEPS("v_max_i32_dpp") : "+v"(v));
+    return __builtin_amdgcn_readlane(v, 63);
 }
-template <int CTRL, int ROWMASK>
-__device__ __forceinline__ float dpp_f(float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, ROWMASK,
-                                                      0xf, false));
-}
-
-// full-wave reductions: result returned wave-uniform (read from lane 63)
+// max of the wave's finite / -inf values (a NaN counts as -inf, as fmaxf
+// skips it), through the order-preserving int key
 __device__ __forceinline__ float wave_max(float v) {
-    v = fmaxf(v, dpp_f<kDppRowShr1, 0xf>(v));
-    v = fmaxf(v, dpp_f<kDppRowShr2, 0xf>(v));
-    v = fmaxf(v, dpp_f<kDppRowShr4, 0xf>(v));
-    v = fmaxf(v, dpp_f<kDppRowShr8, 0xf>(v));
-    v = fmaxf(v, dpp_f<kDppRowBcast15, 0xa>(v));
-    v = fmaxf(v, dpp_f<kDppRowBcast31, 0xc>(v));
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+    return key2f(wave_max_i(f2key(v == v ? v : -PCM_INF)));
 }
 
 // ===========================================================================
@@ -259,12 +266,7 @@ __device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float 
 }
 
 __device__ __forceinline__ int wave_min_i(int v) {
-    v = min(v, dpp_i<kDppRowShr1, 0xf>(v));
-    v = min(v, dpp_i<kDppRowShr2, 0xf>(v));
-    v = min(v, dpp_i<kDppRowShr4, 0xf>(v));
-    v = min(v, dpp_i<kDppRowShr8, 0xf>(v));
-    v = min(v, dpp_i<kDppRowBcast15, 0xa>(v));
-    v = min(v, dpp_i<kDppRowBcast31, 0xc>(v));
+    asm volatile(PCM_WAVE_RED_STEPS("v_min_i32_dpp") : "+v"(v));
     return __builtin_amdgcn_readlane(v, 63);
 }
 
@@ -282,30 +284,44 @@ __device__ __forceinline__ void wave_top2(float v1, int k1, float v2, int k2, fl
 }
 
 // ---- all-reduce inside aligned groups of G lanes (G = 4, 8, 16) with
-// butterfly DPP permutations: every lane of the group gets the result
+// butterfly DPP permutations: every lane of the group gets the result.  Every
+// lane has a source lane in these patterns, so the permuted copy needs no
+// "old" value (mov_dpp, bound_ctrl) and hipcc folds each step into ONE
+// v_{max,min,add}_i32_dpp; float maxima go through the order-preserving int
+// key (fmaxf would add a canonicalising v_max per step).
 constexpr int kQuadXor1 = 0xB1, kQuadXor2 = 0x4E, kRowHalfMirror = 0x141, kRowMirror = 0x140;
+template <int CTRL>
+__device__ __forceinline__ int dpp_all(int x) {
+    return __builtin_amdgcn_mov_dpp(x, CTRL, 0xf, 0xf, true);
+}
+template <int G>
+__device__ __forceinline__ int group_max_i(int v) {
+    v = max(v, dpp_all<kQuadXor1>(v));
+    v = max(v, dpp_all<kQuadXor2>(v));
+    if constexpr (G >= 8) v = max(v, dpp_all<kRowHalfMirror>(v));
+    if constexpr (G >= 16) v = max(v, dpp_all<kRowMirror>(v));
+    return v;
+}
+// max over the group of finite / -inf values (a NaN counts as -inf, as fmaxf
+// skips it)
 template <int G>
 __device__ __forceinline__ float group_max(float v) {
-    v = fmaxf(v, dpp_f<kQuadXor1, 0xf>(v));
-    v = fmaxf(v, dpp_f<kQuadXor2, 0xf>(v));
-    if constexpr (G >= 8) v = fmaxf(v, dpp_f<kRowHalfMirror, 0xf>(v));
-    if constexpr (G >= 16) v = fmaxf(v, dpp_f<kRowMirror, 0xf>(v));
-    return v;
+    return key2f(group_max_i<G>(f2key(v == v ? v : -PCM_INF)));
 }
 template <int G>
 __device__ __forceinline__ int group_min_i(int v) {
-    v = min(v, dpp_i<kQuadXor1, 0xf>(v));
-    v = min(v, dpp_i<kQuadXor2, 0xf>(v));
-    if constexpr (G >= 8) v = min(v, dpp_i<kRowHalfMirror, 0xf>(v));
-    if constexpr (G >= 16) v = min(v, dpp_i<kRowMirror, 0xf>(v));
+    v = min(v, dpp_all<kQuadXor1>(v));
+    v = min(v, dpp_all<kQuadXor2>(v));
+    if constexpr (G >= 8) v = min(v, dpp_all<kRowHalfMirror>(v));
+    if constexpr (G >= 16) v = min(v, dpp_all<kRowMirror>(v));
     return v;
 }
 template <int G>
 __device__ __forceinline__ int group_add_i(int v) {
-    v += dpp_i<kQuadXor1, 0xf>(v);
-    v += dpp_i<kQuadXor2, 0xf>(v);
-    if constexpr (G >= 8) v += dpp_i<kRowHalfMirror, 0xf>(v);
-    if constexpr (G >= 16) v += dpp_i<kRowMirror, 0xf>(v);
+    v += dpp_all<kQuadXor1>(v);
+    v += dpp_all<kQuadXor2>(v);
+    if constexpr (G >= 8) v += dpp_all<kRowHalfMirror>(v);
+    if constexpr (G >= 16) v += dpp_all<kRowMirror>(v);
     return v;
 }
 
@@ -768,6 +784,13 @@ struct EmdWs {
 constexpr int kBoardGen = 0, kBoardQuit = 8, kBoardJn = 16, kBoardNu = 20, kBoardErr = 24;
 constexpr unsigned kInB = 0x7fc0b00bu;  // a quiet NaN no bound ever equals
 
+#ifdef PCM_STAMPS
+// profiling build: the XCD (XCC_ID) that ran each batch element's first seed
+// workgroup ([i]) and its auction master ([512 + i])
+__device__ int g_emd_xcc[1024];
+__device__ __forceinline__ int pcm_xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15; }
+#endif
+
 // ===========================================================================
 // 1. seed kernel: iteration-0 bids + caches, one wave per point, 16 points
 //    per workgroup, the target cloud staged in LDS (kStage)
@@ -792,6 +815,9 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__r
         chunk = blk - batch * wgs_per_batch;
     }
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#ifdef PCM_STAMPS
+    if (chunk == 0 && threadIdx.x == 0) g_emd_xcc[batch] = pcm_xcc_id();
+#endif
     const float *Pg = xyz1 + (size_t)batch * n * 3;
     const float *Qg = xyz2 + (size_t)batch * n * 3;
     // this wave's query points, loaded (scalar) while the target cloud lands
@@ -919,10 +945,26 @@ __device__ __forceinline__ void bid_on(const AState<kG> &st, int j, int k, float
 // its reserve bound cannot be bid from the reserve (every value outside the
 // cache is <= the bound, so the reserve's second best is too): its reserve
 // is retired here and the miss goes straight to the full scan.
+// profiling build: sub-phase stamps of the first pass by thread 0 of the
+// timed element (slots 4..8 of the phase timers: bidder id, entries, values,
+// reductions, bid placed; slot 0 keeps the rest of B1)
+#ifdef PCM_STAMPS
+#define PCM_B1_STAMP(slot, dep)                                                         \
+    if (tm && threadIdx.x == 0 && u0 == 0) {                                            \
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::"v"(dep) : "memory");            \
+        const unsigned long long tn = __builtin_amdgcn_s_memtime();                     \
+        tm[slot] += tn - tm[12];                                                        \
+        tm[12] = tn;                                                                    \
+    }
+#else
+#define PCM_B1_STAMP(slot, dep)
+#endif
 template <int G, bool kG>
 __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, const centry *C, const float *CT,
                                            const centry *CB, const float *CTB, const AState<kG> &st, int *sNm,
-                                           int *coll, const float *resT, int *resN, int n, TieRank tr) {
+                                           int *coll, const float *resT, int *resN, int n, TieRank tr,
+                                           unsigned long long *tm = nullptr) {
+    (void)tm;
     static_assert(G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
     constexpr int E = kL / G;
     static_assert(E % 2 == 0, "slot pairs");
@@ -930,7 +972,9 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
     for (int u0 = 0; u0 < nu; u0 += kEmdThreads / G) {
         const int u = u0 + gi;
         const bool act = u < nu;
+        PCM_B1_STAMP(4, 0u);  // slot 4: from the barrier to the pass start
         const int j = act ? Ucur[u] : 0;
+        PCM_B1_STAMP(5, j);
         // region A (the master's own, plain, L2-resident) is loaded together
         // with the bound; a point whose cache a helper rebuilt (marker) is
         // re-read from region B (sc1)
@@ -945,6 +989,7 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
             ce[2 * e] = w.x;
             ce[2 * e + 1] = w.y;
         }
+        PCM_B1_STAMP(6, (unsigned)ce[0] ^ (unsigned)ce[E - 1] ^ __float_as_uint(tj));
         if (__float_as_uint(tj) == kInB) {
             tj = ld_sc1(CTB + j);
 #pragma unroll
@@ -968,6 +1013,7 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
             kk[e] = k & 0x7fffffff;
             lmax = fmaxf(lmax, v[e]);
         }
+        PCM_B1_STAMP(7, __float_as_uint(lmax));
         // group top-2: best = max, argbest = lowest id at best, better = best
         // on a tie else the max of the rest
         const float b1 = group_max<G>(lmax);
@@ -984,6 +1030,7 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
         const int ties = group_add_i<G>(lc);
         const float rest = group_max<G>(lrest);
         const float b2 = ties >= 2 ? b1 : rest;
+        PCM_B1_STAMP(8, __float_as_uint(b2) ^ (unsigned)kb);
         if constexpr (kG) {
             // a tie at the best (group-uniform): the reference's order
             // decides.  When the bid is proven (b2 > bound) every object of
@@ -1001,6 +1048,7 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
                 if (resN && !(tj > resT[j])) resN[j] = 0;
             }
         }
+        PCM_B1_STAMP(9, (unsigned)kb);
     }
 }
 
@@ -1116,10 +1164,13 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     const float *Qg = a.xyz2 + base * 3;
     int32_t *bw = ws.board + (size_t)batch * kBoardWords;
     centry *C = ws.cache + base * kL;
-    float *CT = ws.CT + base;
+    float *CT = ws.CT + base;  // region-A bounds (LDS copy in the LDS-state forms, below)
     const bool hist = a.diag == kDiagHist;
     // diag >= 2: timers of batch element diag - 2
     const bool timers = a.diag >= kDiagTimers && batch == a.diag - kDiagTimers && tid == 0;
+#ifdef PCM_STAMPS
+    if (tid == 0) g_emd_xcc[512 + batch] = pcm_xcc_id();
+#endif
 
     AState<kG> st;
     char *lp = (char *)smem;
@@ -1134,6 +1185,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         st.U0 = (int *)lp; lp += 4 * (size_t)n;
         st.U1 = (int *)lp; lp += 4 * (size_t)n;
         st.miss = (int *)lp; lp += 4 * (size_t)n;
+        CT = (float *)lp; lp += 4 * (size_t)n;  // the bound is read first in every cache bid: LDS, not L2
     } else {
         st.ass = ws.g_ass + base; st.inv = ws.g_inv + base; st.price = ws.g_price + base;
         st.mx = ws.g_max + base; st.claim = ws.g_claim + base; st.bid = ws.g_bid + base;
@@ -1166,6 +1218,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         st.mx[j] = f2key(0.f);  // emd_module.py:49 zero-inits max_increments
         st.claim[j] = ~0ull;
         st.U0[j] = j;           // iteration 0: every point bids
+        if constexpr (!kG) CT[j] = ws.CT[base + j];  // the seed's bounds
         if constexpr (kRes) {
             sRT[j] = ws.RT[base + j];
             sRN[j] = res_on ? ws.RN[base + j] : 0;
@@ -1280,9 +1333,12 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         // ---- chain mode: a single bidder.  Its bid can only collide with
         // itself, so every later iteration is bid -> resolve -> assign of one
         // point, and the evicted owner (if any) is the next iteration's only
-        // bidder.  Wave 0 runs the chain alone, with no workgroup barrier per
-        // iteration; the resolution is the claim/assign phases' below for
-        // one bidder (solo rule, else the 1e-6 window).
+        // bidder.  The bid is split over kChainW waves (each scans every
+        // kChainW-th 64-object chunk); wave 0 merges, resolves (solo rule,
+        // else the 1e-6 window) and assigns: two barriers per iteration and no
+        // list handling.  (One wave scanning all n objects alone took 4.3k
+        // cycles per iteration against 1.9k: the 16 dependent per-lane steps
+        // of its lane top-2 are latency-bound.)
         if (it > 0 && nu == 1 && a.tail_max > 0) {
             int j = Ucur[0];
             for (; it < iters; ++it) {
@@ -1293,11 +1349,10 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     atomicAdd(&a.stats[2 * it], 1);
                     atomicAdd(&a.stats[2 * it + 1], 1);
                 }
-                // the bid, split over the 16 waves
-                {
+                if (wave < kChainW) {
                     float b1, b2;
                     int kb;
-                    part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, wave, kWaves, b1, kb, b2);
+                    part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, wave, kChainW, b1, kb, b2);
                     if (lane == 0) { sPb1[wave] = b1; sPkb[wave] = kb; sPb2[wave] = b2; }
                 }
                 __syncthreads();
@@ -1305,7 +1360,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 if (wave == 0) {
                     float b1, b2;
                     int kb;
-                    part_merge(sPb1, sPkb, sPb2, kWaves, b1, kb, b2);
+                    part_merge(sPb1, sPkb, sPb2, kChainW, b1, kb, b2);
                     kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, tr);
                     int next = j;  // no bid / not won: j bids again
                     if ((unsigned)kb < (unsigned)n && lane == 0) {
@@ -1346,7 +1401,13 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             ++tail_its;
             // W waves per bidder (16 / the next power of two >= nu), each
             // scanning every W-th 64-object chunk; the bidder's first wave merges
+#if defined(PCM_TAILW1)
+            const int W = 1;
+#elif defined(PCM_TAIL_FILL)
+            const int W = nu <= 1 ? 4 : (nu <= 2 ? 2 : 1);  // just enough waves for the 4 SIMDs
+#else
             const int W = nu <= 1 ? 16 : (nu <= 2 ? 8 : (nu <= 4 ? 4 : (nu <= 8 ? 2 : 1)));
+#endif
             const int q = wave / W, r = wave - q * W;
             if (W == 1) {  // whole bids, one wave each (more than 8 bidders)
                 for (int u = wave; u < nu; u += kWaves) {
@@ -1397,9 +1458,10 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             const int G = cache_bid_lanes(nu);
             const float *rT = kRes ? sRT : nullptr;
             int *rN = kRes ? sRN : nullptr;
-            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr);
-            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr);
-            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr);
+            unsigned long long *tm = timers ? sTm : nullptr;
+            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
+            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
+            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
         }
         __syncthreads();
         PCM_EMD_PHASE(0);
@@ -1556,17 +1618,21 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             if (u < nu) {
                 const int j = Ucur[u];
                 const int k = st.bid[j];
+                // the owner, increment and maximum are read together (one
+                // LDS round trip instead of three dependent ones)
+                const int kc = k < 0 ? 0 : k;
+                const int old = st.inv[kc];
+                const float inc = st.inc[j];
+                const int mxk = by_max ? st.ld_max(kc) : 0;
                 if (k < 0) {
                     push = j;  // no bid: stays unassigned
                 } else if (last) {
                     st.ass[j] = k;
-                } else if (solo || (by_max ? st.inc[j] == key2f(st.ld_max(k))
-                                           : st.ld_claim(k) == (itag | (unsigned)j))) {
-                    const int old = st.inv[k];
+                } else if (solo || (by_max ? inc == key2f(mxk) : st.ld_claim(k) == (itag | (unsigned)j))) {
                     if (old != -1) { st.ass[old] = -1; push = old; }
                     st.inv[k] = j;
                     st.ass[j] = k;
-                    st.price[k] += st.inc[j];
+                    st.price[k] += inc;
                     st.mx[k] = f2key(-1e9f);
                 } else {
                     push = j;  // outbid
@@ -1773,7 +1839,7 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     const size_t xchg = 5 * (size_t)kEmdThreads * 4;
     const bool stage_p = n <= (g_state ? 4096 : kStagePN);  // !g_state: n == kStagePN exactly
     const bool res = !g_state && stage_p;  // n == kStagePN: the reserve form (bounds + counts in LDS)
-    const size_t m_lds = (g_state ? 0 : 44 * (size_t)n) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
+    const size_t m_lds = (g_state ? 0 : 48 * (size_t)n) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
                          xchg + (res ? 8 * (size_t)n : 0);
     const size_t h_lds = H > 0 ? (stage ? 12 * (size_t)n : 0) + 4 * (size_t)n : 0;
     size_t lds = m_lds > h_lds ? m_lds : h_lds;
@@ -1863,6 +1929,13 @@ extern "C" int pcm_emd_workspace_status(const void *workspace, size_t workspace_
 extern "C" int pcm_tune_emd_timeouts(const void *workspace, size_t workspace_bytes, int b, int n, void *stream) {
     return emd_timeouts(workspace, workspace_bytes, b, n, stream);
 }
+
+#ifdef PCM_STAMPS
+extern "C" int pcm_tune_emd_xcc(int *host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_emd_xcc), sizeof(int) * 1024, 0, hipMemcpyDeviceToHost) == hipSuccess
+               ? 0 : PCM_ERR_LAUNCH;
+}
+#endif
 
 extern "C" int pcm_emd_backward(const float *xyz1, const float *xyz2, int b, int n,
                                 const float *graddist, const int32_t *assignment, float *gradxyz1,

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""A/B of the one-launch Chamfer step (pcm_chamfer_loss_grad) for one build
+(PCM_HIP_LIB=...): every fused variant from 7 up, at BASELINE config 2 (B=32,
+N=M=1024), device time per launch from graph replays, interleaved rounds; each
+variant's outputs are compared bit for bit with variant 7's.  Run once per
+library in the same GPU session (tools/ab_chamfer.sh)."""
+import os
+import statistics
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric"))
+import pcm_hip  # noqa: E402
+from tune_chamfer import graph_of, time_graph_us  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    b, n, m, reps, rounds = 32, 1024, 1024, 50, 7
+    g = torch.Generator().manual_seed(0)
+    x1 = torch.rand(b, n, 3, generator=g).to(dev)
+    x2 = torch.rand(b, m, 3, generator=g).to(dev)
+    d1, d2 = torch.empty(b, n, device=dev), torch.empty(b, m, device=dev)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=dev)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=dev)
+    gx1, gx2 = torch.empty(b, n, 3, device=dev), torch.empty(b, m, 3, device=dev)
+    mo = torch.empty(3, device=dev)
+    ws = pcm_hip.chamfer_workspace(dev, b, n, m)
+    w1, w2 = 1.0 / (b * n), 1.0 / (b * m)
+    vs = list(range(7, pcm_hip.tune_num_chamfer_loss_grad_variants()))
+    out = {}
+    for v in vs:
+        pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, ws, variant=v)
+        torch.cuda.synchronize()
+        out[v] = [t.clone() for t in (d1, d2, i1, i2, gx1, gx2, mo)]
+    same = {v: all(torch.equal(a, r) for a, r in zip(out[v], out[7])) for v in vs}
+    graphs = {v: graph_of(lambda v=v: pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, ws,
+                                                                variant=v), reps) for v in vs}
+    res = {v: [] for v in vs}
+    for _ in range(rounds):
+        for v in vs:
+            res[v].append(time_graph_us(graphs[v], reps))
+    lib = os.path.basename(os.environ.get("PCM_HIP_LIB", "libpcm_hip.so"))
+    print(lib + ": " + ", ".join(f"v{v} {statistics.median(res[v]):.2f} us (min {min(res[v]):.2f}, same={same[v]})"
+                                 for v in vs), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -5,6 +5,8 @@ timers of the slowest element, plus the forward time."""
 import os
 import sys
 
+import numpy as np
+
 import torch
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -38,6 +40,13 @@ def main():
     lib = os.path.basename(os.environ.get("PCM_HIP_LIB", "libpcm_hip.so"))
     print(f"{lib}: bids {int(per[:, 0].sum())} misses {int(per[:, 1].sum())} reserve bids {misc[13]} "
           f"jobs {misc[10]}; wall us min {min(wall):.1f} med {sorted(wall)[b // 2]:.1f} max {max(wall):.1f}")
+    if "--hist" in sys.argv:  # bids / misses per iteration, summed over the batch, in bins
+        pr = per.numpy()
+        last = int(np.nonzero(pr[:, 0])[0].max()) + 1 if pr[:, 0].any() else 0
+        step = 25 if last > 200 else 1
+        for i0 in range(0, last, step):
+            seg = pr[i0:i0 + step]
+            print(f"    it {i0:5d}-{min(i0 + step, last) - 1:5d}: bids {int(seg[:, 0].sum()):7d} misses {int(seg[:, 1].sum()):7d}")
     slow = max(range(b), key=lambda i: wall[i])
     st = torch.zeros(3 * iters + 16 + b, dtype=torch.int32, device=dev)
     pcm_hip.emd_forward(x1, x2, eps, iters, d, a, stats=st, diag=2 + slow)

@@ -186,7 +186,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
     int(*sChunk)[QW] = reinterpret_cast<int(*)[QW]>(arena + 3 * TILE * 4 + 2 * W * QW * 4);
     __shared__ float sD[QW];  // final (distance, index) per query slot
     __shared__ int sK[QW];
-    __shared__ int sFc[QW];   // proven chunk, or -1 (cooperative scan)
+    __shared__ unsigned sPlan[QW];  // near-tie: chunks that can hold the answer (below)
     __shared__ float sTD[kTB * W];  // near-tie pass: per-wave partials
     __shared__ int sTK[kTB * W];
     __shared__ float sHD[PARTS][QW];
@@ -318,6 +318,12 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         constexpr int G = C / 4;
         pcm_f4 X4n, Y4n, Z4n, W4n;
         auto fetch = [&](int cc, int g) {
+#ifdef PCM_SCAN_NOLDS  // diagnostic timing build (wrong results): the scan without its LDS reads
+            if (cc != wave || g != 0) {
+                asm volatile("" : "+v"(X4n), "+v"(Y4n), "+v"(Z4n), "+v"(W4n));
+                return;
+            }
+#endif
             const int o = cc * C + 4 * g;
             X4n = *reinterpret_cast<const pcm_f4 *>(&sU[0][o]);
             Y4n = *reinterpret_cast<const pcm_f4 *>(&sU[1][o]);
@@ -338,6 +344,12 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                 // the next group's four reads stay ahead of this group's math
                 // (hipcc otherwise sinks them to their use and waits on each)
                 __builtin_amdgcn_sched_barrier(0);
+#ifdef PCM_SCAN_NOVALU  // diagnostic timing build (wrong results): the scan's reads, one fold each
+#pragma unroll
+                for (int qq = 0; qq < QPT; ++qq)
+                    mn[qq] = __builtin_amdgcn_fmed3f(mn[qq], X4.x + Y4.y, Z4.z + W4.w);
+                continue;
+#endif
                 if constexpr (QPT == 4) {
                     filt_group4(mn, px, py, pz, X4, Y4, Z4, W4);
                     continue;
@@ -393,18 +405,26 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         sChunk[wave][qq * 64 + lane] = bchunk[qq];
     }
     const int any_nonfinite = __syncthreads_or(nonfinite ? 1 : 0);
+    PCM_STAMP(4);
 
     float my_d = 0.f;
     if (!any_nonfinite) {
-        // ---- merge the waves; decide per query whether the best chunk is proven
-        if (tid < QW) {
+        // ---- one pass, one barrier: thread (s = tid mod QW, part = tid / QW)
+        // merges the waves' (best, second, chunk) of query s -- every part
+        // reaches the same verdict -- and, when the best chunk is proven,
+        // rescans its part of that chunk exactly; part 0 of a near-tie query
+        // lists it with its rescan plan instead.
+        const int s = tid % QW;
+        const int part = tid / QW;
+        bool proven = false;
+        {
             float vb[W], vs[W];
             int vc[W];
 #pragma unroll
             for (int w = 0; w < W; ++w) {  // every load first, then branch-free selects
-                vb[w] = sBest[w][tid];
-                vs[w] = sSec[w][tid];
-                vc[w] = sChunk[w][tid];
+                vb[w] = sBest[w][s];
+                vs[w] = sSec[w][s];
+                vc[w] = sChunk[w][s];
             }
             float fb = vb[0], fs = vs[0];
             int fc = vc[0];
@@ -418,12 +438,17 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             float rmax2 = sRmax[0];
 #pragma unroll
             for (int w = 1; w < W; ++w) rmax2 = __builtin_fmaxf(rmax2, sRmax[w]);
-            // this thread's register copy of query tid is qq = tid >> 6 (= wave)
-            float qn2 = 0.f;
+            // this thread's register copy of query s is qq = s >> 6
+            const int qsel = s >> 6;
+            float qn2 = 0.f, x = rx[0], y = ry[0], z = rz[0];
 #pragma unroll
             for (int qq = 0; qq < QPT; ++qq)
-                if (qq == wave)
+                if (qq == qsel) {
                     qn2 = __builtin_fmaf(pz[qq].x, pz[qq].x, __builtin_fmaf(py[qq].x, py[qq].x, px[qq].x * px[qq].x));
+                    x = rx[qq];
+                    y = ry[qq];
+                    z = rz[qq];
+                }
             // the bound E = 16u (|t'| + |q'|)^2 of a target t: with R = max |t'|
             // (eR) for every target; but a target that can reach the best
             // chunk's exact minimum d_b lies within sqrt(d_b) of q, so
@@ -440,37 +465,29 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             const float db = __builtin_fmaxf((fb + qn2) * 1.0001f + 2.f * eR, 0.f);
             const float rq = 2.f * sq + __builtin_sqrtf(db);
             const float e2 = 2.f * kFiltU16 * __builtin_fminf(rr * rr, rq * rq) * 1.001f;
-            const bool proven = (fs - fb) > e2;  // false for NaN
-            sFc[tid] = proven ? fc : -1;
-        }
-        __syncthreads();
-        PCM_STAMP(4);
-
-        // ---- exact rescan of the proven chunk: item -> (query slot s, part)
-#pragma unroll
-        for (int r = 0; r < (QW * PARTS + NT - 1) / NT; ++r) {
-            const int item = tid + r * NT;
-            if (item >= QW * PARTS) break;
-            const int s = item % QW;
-            const int part = item / QW;
-            const int fc = sFc[s];
+            proven = (fs - fb) > e2;  // false for NaN
             float hd = PCM_INF;
             int hk = 0x7fffffff;
-            if (qbase + s < nq && fc >= 0) {
-                const int qsel = (item >> 6) % QPT;
-                float x = rx[0], y = ry[0], z = rz[0];
+            if (qbase + s < nq) {
+                if (proven) {
+                    const int k0 = fc * C + part * CP;
+                    float tx[CP], ty[CP], tz[CP];  // all loads in flight at once
+                    if (resident) {
 #pragma unroll
-                for (int qq = 1; qq < QPT; ++qq)
-                    if (qsel == qq) { x = rx[qq]; y = ry[qq]; z = rz[qq]; }
-                const int k0 = fc * C + part * CP;
-                if (resident) {
-                    float tx[CP], ty[CP], tz[CP];
+                        for (int k = 0; k < CP; ++k) {
+                            const int kk = slot(min(k0 + k, nt - 1));
+                            tx[k] = sT[0][kk];
+                            ty[k] = sT[1][kk];
+                            tz[k] = sT[2][kk];
+                        }
+                    } else {
 #pragma unroll
-                    for (int k = 0; k < CP; ++k) {
-                        const int kk = slot(min(k0 + k, nt - 1));
-                        tx[k] = sT[0][kk];
-                        ty[k] = sT[1][kk];
-                        tz[k] = sT[2][kk];
+                        for (int k = 0; k < CP; ++k) {
+                            const int kk = min(k0 + k, nt - 1);
+                            tx[k] = pcm_ld(T + 3 * (size_t)kk);
+                            ty[k] = pcm_ld(T + 3 * (size_t)kk + 1);
+                            tz[k] = pcm_ld(T + 3 * (size_t)kk + 2);
+                        }
                     }
 #pragma unroll
                     for (int k = 0; k < CP; ++k) {  // ascending k: strict '<' keeps the lowest
@@ -479,107 +496,48 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                         hd = take ? d : hd;
                         hk = take ? k0 + k : hk;
                     }
-                } else {
-                    float tx[CP], ty[CP], tz[CP];  // all loads in flight at once
+                } else if (part == 0) {
+                    // near-tie plan: by the same argument only targets screened
+                    // at <= fb + e2 can reach d_b, so wave w's chunks are
+                    // rescanned all (bit W + w: its second-best chunk
+                    // qualifies) or only its best one (bit w), or not at all.
+                    // NaN keeps every bit (a full scan).
+                    unsigned plan = 0;
+                    const float thr = fb + e2;
 #pragma unroll
-                    for (int k = 0; k < CP; ++k) {
-                        const int kk = min(k0 + k, nt - 1);
-                        tx[k] = pcm_ld(T + 3 * (size_t)kk);
-                        ty[k] = pcm_ld(T + 3 * (size_t)kk + 1);
-                        tz[k] = pcm_ld(T + 3 * (size_t)kk + 2);
-                    }
-#pragma unroll
-                    for (int k = 0; k < CP; ++k) {
-                        const int kk = k0 + k;
-                        const float d = pcm_sqd(tx[k] - x, ty[k] - y, tz[k] - z);
-                        const bool take = (d < hd) & (kk < nt);
-                        hd = take ? d : hd;
-                        hk = take ? kk : hk;
-                    }
+                    for (int w = 0; w < W; ++w)
+                        plan |= !(vs[w] > thr) ? (1u << (W + w)) : (!(vb[w] > thr) ? (1u << w) : 0u);
+                    sPlan[s] = plan;
+                    sList[atomicAdd(&sNList, 1)] = s;
                 }
             }
             sHD[part][s] = hd;
             sHK[part][s] = hk;
         }
         __syncthreads();
-        if (tid < QW && qbase + tid < nq) {
-            if (sFc[tid] >= 0) {
-                float d = sHD[0][tid];
-                int k = sHK[0][tid];
-#pragma unroll
-                for (int p = 1; p < PARTS; ++p) {
-                    const float dv = sHD[p][tid];
-                    const int kv = sHK[p][tid];
-                    pcm_lexmin(d, k, dv, kv);
-                }
-                sD[tid] = d;
-                sK[tid] = k;
-            } else {
-                sList[atomicAdd(&sNList, 1)] = tid;
-            }
-        }
-        __syncthreads();
         PCM_STAMP(5);
 
-        // ---- near-ties: exact scans of the whole target cloud.  Resident
-        // cloud: one wave per query (LDS reads, one wave reduction, no
-        // barriers).  Otherwise: the workgroup cooperates, kTB queries per pass
+        // ---- near-ties.  Resident cloud: one wave per query rescans only the
+        // chunks its plan names (usually two: the best and one rival, 2C
+        // candidates instead of nt), 64 / C chunks per step, then one wave
+        // reduction; no barrier until the output phase.  Otherwise the
+        // workgroup cooperates over the whole cloud, kTB queries per pass
         // (one pass over the global candidates serves them all).
         const int nl = sNList;
-        if (resident && nl > 0 && nl <= W) {
-            // few near-ties (the usual case): each query's scan split over
-            // PW = W / nl waves (rounded down to a power of two), four
-            // candidates per lane in flight, ascending per lane; the parts
-            // merge lexicographically.  A workgroup with one near-tie used to
-            // spend ~1.9 us here, one dependent LDS round trip per candidate.
-            int PW = W;
-            while (PW * nl > W) PW >>= 1;
-            const int e = wave / PW, r = wave - e * PW;
-            if (e < nl) {
-                const int s = sList[e];
-                float x = rx[0], y = ry[0], z = rz[0];
+        if (resident) {
+            static_assert(C <= 64 && 64 % C == 0 && 64 % W == 0 && (TILE / C) % W == 0,
+                          "whole chunks per step; wave w owns the chunks c = w mod W");
+            constexpr int kCps = 64 / C;  // chunks per step
+            unsigned long long wpat = 0;  // chunk bits c = 0 mod W of one 64-chunk word
 #pragma unroll
-                for (int qq = 1; qq < QPT; ++qq)
-                    if ((s >> 6) == qq) { x = rx[qq]; y = ry[qq]; z = rz[qq]; }
-                x = __shfl(x, s & 63, 64);
-                y = __shfl(y, s & 63, 64);
-                z = __shfl(z, s & 63, 64);
-                float bd = PCM_INF;
-                int bk = 0x7fffffff;
-                const int step = 64 * PW;
-                for (int k0 = r * 64 + lane; k0 < nt; k0 += 4 * step) {
-                    float tx[4], ty[4], tz[4];
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int sk = slot(min(k0 + u * step, nt - 1));
-                        tx[u] = sT[0][sk];
-                        ty[u] = sT[1][sk];
-                        tz[u] = sT[2][sk];
-                    }
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const float d = pcm_sqd(tx[u] - x, ty[u] - y, tz[u] - z);
-                        if (k0 + u * step < nt) pcm_lexmin(bd, bk, d, k0 + u * step);
-                    }
-                }
-                pcm_wave_lexmin(bd, bk);
-                if (lane == 0) {
-                    sTD[wave] = bd;
-                    sTK[wave] = bk;
-                }
-            }
-            __syncthreads();
-            if (tid < nl) {
-                float d = sTD[tid * PW];
-                int k = sTK[tid * PW];
-                for (int w = 1; w < PW; ++w) pcm_lexmin(d, k, sTD[tid * PW + w], sTK[tid * PW + w]);
-                sD[sList[tid]] = d;
-                sK[sList[tid]] = k;
-            }
-            __syncthreads();
-        } else if (resident) {
+            for (int i = 0; i < 64; i += W) wpat |= 1ull << i;
+            const int nch = (nt + C - 1) / C;
             for (int e = wave; e < nl; e += W) {
-                const int s = sList[e];
+                const int s = __builtin_amdgcn_readfirstlane(sList[e]);
+                const unsigned plan = __builtin_amdgcn_readfirstlane(sPlan[s]);
+                int one[W];  // best chunk of each wave
+#pragma unroll
+                for (int w = 0; w < W; ++w) one[w] = __builtin_amdgcn_readfirstlane(sChunk[w][s]);
                 float x = rx[0], y = ry[0], z = rz[0];
 #pragma unroll
                 for (int qq = 1; qq < QPT; ++qq)
@@ -589,9 +547,30 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                 z = __shfl(z, s & 63, 64);
                 float bd = PCM_INF;
                 int bk = 0x7fffffff;
-                for (int k = lane; k < nt; k += 64) {
-                    const int sk = slot(k);
-                    pcm_lexmin(bd, bk, pcm_sqd(sT[0][sk] - x, sT[1][sk] - y, sT[2][sk] - z), k);
+                for (int c0 = 0; c0 < nch; c0 += 64) {
+                    unsigned long long M = 0;
+#pragma unroll
+                    for (int w = 0; w < W; ++w) {
+                        if ((plan >> (W + w)) & 1u) M |= wpat << w;
+                        else if (((plan >> w) & 1u) && one[w] >= c0 && one[w] < c0 + 64) M |= 1ull << (one[w] - c0);
+                    }
+                    if (nch - c0 < 64) M &= (1ull << (nch - c0)) - 1ull;
+                    while (M) {
+                        int ch[kCps];
+#pragma unroll
+                        for (int j = 0; j < kCps; ++j) {
+                            ch[j] = M ? c0 + __builtin_ctzll(M) : -1;
+                            M &= M - 1ull;
+                        }
+                        int c = ch[0];
+#pragma unroll
+                        for (int j = 1; j < kCps; ++j)
+                            if (lane / C == j) c = ch[j];
+                        const int k = c * C + (lane & (C - 1));
+                        const int sk = slot(min(max(k, 0), nt - 1));
+                        const float d = pcm_sqd(sT[0][sk] - x, sT[1][sk] - y, sT[2][sk] - z);
+                        if (c >= 0 && k < nt) pcm_lexmin(bd, bk, d, k);
+                    }
                 }
                 pcm_wave_lexmin(bd, bk);
                 if (lane == 0) {
@@ -674,15 +653,26 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             __syncthreads();
         }
         PCM_STAMP(6);
-        // ---- one store phase for the workgroup's outputs
+        // ---- one store phase for the workgroup's outputs (thread tid < QW is
+        // part 0 of query tid: `proven` is that query's verdict)
         if (tid < QW && qbase + tid < nq) {
-            my_d = sD[tid];
-            out_st<kSc1>(D + qbase + tid, my_d);
-            out_st<kSc1>(I + qbase + tid, (int32_t)sK[tid]);
+            float d;
+            int k;
+            if (proven) {
+                d = sHD[0][tid];
+                k = sHK[0][tid];
+#pragma unroll
+                for (int p = 1; p < PARTS; ++p) pcm_lexmin(d, k, sHD[p][tid], sHK[p][tid]);
+            } else {
+                d = sD[tid];
+                k = sK[tid];
+            }
+            my_d = d;
+            out_st<kSc1>(D + qbase + tid, d);
+            out_st<kSc1>(I + qbase + tid, (int32_t)k);
             // data-tagged argmin granule {call tag, idx}: one 8-byte sc1 store,
             // its own flag (no drain, no counter)
-            if (Gr) __hip_atomic_store(Gr + qbase + tid, tag | (unsigned)sK[tid], __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+            if (Gr) __hip_atomic_store(Gr + qbase + tid, tag | (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     } else {
         for (int s = tid; s < QW; s += NT) {

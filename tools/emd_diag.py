@@ -60,6 +60,21 @@ def main():
             if nu == 0 and int(stc[2 * it]) == 0:
                 continue
             print(f"    it {it:4d} bidders {nu:5d} cycles {16 * int(stc[2 * it]):7d} bids(B1) {16 * int(stc[2 * it + 1]):7d}")
+    if "--by-nu" in sys.argv:  # the slowest element's iteration cycles by bidder count
+        bins = [(1, 1), (2, 4), (5, 16), (17, 64), (65, 256), (257, 1 << 30)]
+        acc = {bn: [0, 0] for bn in bins}
+        for it in range(iters):
+            nu = int(stc[2 * iters + 16 + it])
+            cyc = 16 * int(stc[2 * it])
+            for bn in bins:
+                if bn[0] <= nu <= bn[1]:
+                    acc[bn][0] += 1
+                    acc[bn][1] += cyc
+        tot = sum(v[1] for v in acc.values())
+        for bn, (cnt, cyc) in acc.items():
+            if cnt:
+                print(f"    bidders {bn[0]:4d}-{min(bn[1], 99999):5d}: {cnt:5d} iterations, {cyc / 1e6:7.2f} M cycles "
+                      f"({100.0 * cyc / max(tot, 1):4.1f} %), {cyc / cnt:8.0f} per iteration")
     print(f"  slowest element {slow}: {act} iterations; cycles/iteration "
           + ", ".join(f"{nm}={16.0 * v / act:.0f}" for nm, v in zip(T.TIMERS, tm[:12])))
     print(f"  forward {T.timed(x1, x2, eps, iters, d, a, None, None, reps=20):.1f} us", flush=True)

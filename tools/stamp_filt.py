@@ -16,7 +16,8 @@ import statistics
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["PCM_HIP_LIB"] = os.path.join(REPO, "3d-pointcloudreconstruction_amd", "lib", "libpcm_hip_stamps.so")
+os.environ["PCM_HIP_LIB"] = os.environ.get(
+    "PCM_STAMPS_LIB", os.path.join(REPO, "3d-pointcloudreconstruction_amd", "lib", "libpcm_hip_stamps.so"))
 sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric"))
 import torch  # noqa: E402
 import pcm_hip  # noqa: E402

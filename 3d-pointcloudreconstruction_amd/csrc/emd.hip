@@ -81,6 +81,14 @@ constexpr int kSpinLimit = 1 << 22;  // bounded polls (sticky error word on time
 constexpr int kStagePN = 1024;          // the n of the LDS-state, staged-bidder auction form
 constexpr int kDefaultOffloadMin = 24;  // misses above which an iteration is offloaded
 constexpr int kDefaultTailMax = 16;     // bidders at or below which an iteration runs in tail mode
+// ... and up to kTailFuseMax bidders (fused tail, one wave per bidder) while
+// the last cache-bid iteration's misses were at least half its bids
+#ifndef PCM_TAIL_HI
+#define PCM_TAIL_HI 0  // off: 64 measured 2-4 % slower at the training call (r03m)
+#endif
+constexpr int kTailFuseMax = 64;
+constexpr int kTailHi = PCM_TAIL_HI;
+static_assert(kTailHi <= kTailFuseMax, "one lane per bidder in the fused resolve");
 #ifndef PCM_CHAIN_W
 #define PCM_CHAIN_W 16
 #endif
@@ -1154,8 +1162,8 @@ __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank
 template <bool kG, bool kStage, bool kStageP, int kN>
 __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *smem) {
     __shared__ int sNu[2], sNm, sColl[2], sChainJ;  // sColl: [0] some object saw 2 bids, [1] a window contention
-    __shared__ float sPb1[kWaves], sPb2[kWaves];  // split bids: each wave's part
-    __shared__ int sPkb[kWaves];
+    __shared__ float sPb1[kTailFuseMax], sPb2[kTailFuseMax];  // split bids: each part (wave or bidder)
+    __shared__ int sPkb[kTailFuseMax];
     const int n = kN > 0 ? kN : a.n, iters = a.iters;
     const float eps = a.eps;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1245,6 +1253,15 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         sTm[i] += tn - sTm[12];                                           \
         sTm[12] = tn;                                                     \
     }
+    // experiment build (PCM_TAIL_TIMERS): slots 4-7 time the fused tail
+    // iteration's scan, first barrier, resolve and second barrier instead
+#ifdef PCM_TAIL_TIMERS
+#define PCM_B2_PHASE(i)
+#define PCM_TAIL_PHASE(i) PCM_EMD_PHASE(i)
+#else
+#define PCM_B2_PHASE(i) PCM_EMD_PHASE(i)
+#define PCM_TAIL_PHASE(i)
+#endif
     // the master's own full scan of point j: cache region A, bid placed
     // (profiling build: wave 0's key scan, proof and exact fallback timed
     // in slots 6, 7, 11 and the exact fallbacks counted)
@@ -1313,6 +1330,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         }
     };
     int active = 0, chain_its = 0, tail_its = 0;
+    bool hi_miss = false;  // the last cache-bid iteration missed on at least half its bids
     for (int it = 0; it < iters; ++it) {
         const bool last = (it == iters - 1);
         // timers: this iteration's start (cycles) and B1 total so far
@@ -1397,8 +1415,10 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
 
         // ---- tail mode (few bidders; the count never grows): one wave per
         // bidder, full scan without a cache, no cache-bid phase
-        if (it > 0 && nu <= a.tail_max) {
+        const bool tail_hi = !kG && a.tail_max > 0 && nu <= kTailHi && hi_miss;
+        if (it > 0 && (nu <= a.tail_max || tail_hi)) {
             ++tail_its;
+            hi_miss = true;  // the count never grows from here
             // W waves per bidder (16 / the next power of two >= nu), each
             // scanning every W-th 64-object chunk; the bidder's first wave merges
 #if defined(PCM_TAILW1)
@@ -1409,6 +1429,99 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             const int W = nu <= 1 ? 16 : (nu <= 2 ? 8 : (nu <= 4 ? 4 : (nu <= 8 ? 2 : 1)));
 #endif
             const int q = wave / W, r = wave - q * W;
+            if (!kG && (tail_hi || nu * W <= kWaves)) {
+                // fused: every part to LDS, one barrier, then wave 0 -- lane
+                // u for bidder u -- merges the parts, places the bids,
+                // resolves them (GetMax + the 1e-6 window claim, as the C
+                // phase) and assigns (as D), and builds the next list: one
+                // barrier more, where the general path takes four.  Within
+                // one wave the LDS executes the instructions in order, so
+                // each step sees the previous one's atomics.  (n <= 2048:
+                // tie_fix is the identity here.)
+                if (nu > kWaves) {  // more bidders than waves: whole bids, one wave each
+                    for (int u = wave; u < nu; u += kWaves) {
+                        const int j = Ucur[u];
+                        float b1, b2;
+                        int kb;
+                        part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, 0, 1, b1, kb, b2);
+                        if (lane == 0) { sPb1[u] = b1; sPkb[u] = kb; sPb2[u] = b2; }
+                    }
+                } else if (q < nu) {
+                    const int j = Ucur[q];
+                    float b1, b2;
+                    int kb;
+                    part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, r, W, b1, kb, b2);
+                    if (lane == 0) { sPb1[wave] = b1; sPkb[wave] = kb; sPb2[wave] = b2; }
+                }
+                if (hist && tid == 0) {
+                    atomicAdd(&a.stats[2 * it], nu);
+                    atomicAdd(&a.stats[2 * it + 1], nu);
+                }
+                PCM_TAIL_PHASE(4);
+                __syncthreads();
+                PCM_TAIL_PHASE(5);
+                if (wave == 0) {
+                    const bool act = lane < nu;
+                    const int j = act ? Ucur[lane] : 0;
+                    // merge of the bidder's parts: best, lowest id at the
+                    // best, the multiset's second (parts never hold NaN)
+                    float b1 = -PCM_INF, b2 = -PCM_INF;
+                    int kb = 0x7fffffff;
+                    if (act) {
+                        for (int p = lane * W; p < lane * W + W; ++p) {
+                            const float p1 = sPb1[p], p2 = sPb2[p];
+                            const int pk = sPkb[p];
+                            if (p1 > b1) {
+                                b2 = fmaxf(b1, p2);
+                                b1 = p1;
+                                kb = pk;
+                            } else if (p1 == b1) {
+                                b2 = b1;
+                                kb = min(kb, pk);
+                            } else {
+                                b2 = fmaxf(b2, p1);
+                            }
+                        }
+                    }
+                    const bool bid = act && (unsigned)kb < (unsigned)n;  // else all-NaN values: no bid
+                    const float inc = b1 - b2 + eps;
+                    const ckey key = ((ckey)(~(unsigned)it) << 32) | (unsigned)j;
+                    int push = act && !bid ? j : -1;
+                    if (bid && last) st.ass[j] = kb;
+                    if (bid && !last) atomicMax(&st.mx[kb], f2key(inc));
+                    if (bid && !last) {
+                        const double bi = (double)inc, mi = (double)key2f(st.mx[kb]);
+                        if (bi - 1e-6 <= mi && mi <= bi + 1e-6) atomicMin(&st.claim[kb], key);
+                    }
+                    if (bid && !last) {
+                        if (st.claim[kb] == key) {
+                            const int old = st.inv[kb];
+                            if (old != -1) { st.ass[old] = -1; push = old; }
+                            st.inv[kb] = j;
+                            st.ass[j] = kb;
+                            st.price[kb] += inc;
+                            st.mx[kb] = f2key(-1e9f);
+                        } else {
+                            push = j;  // outbid
+                        }
+                    }
+                    if (!last) {
+                        const unsigned long long bal = __ballot(push >= 0);
+                        if (push >= 0) Unext[__popcll(bal & ((1ull << lane) - 1ull))] = push;
+                        if (lane == 0) sNu[cur ^ 1] = __popcll(bal);
+                    }
+                }
+                PCM_TAIL_PHASE(6);
+                __syncthreads();
+                PCM_TAIL_PHASE(7);
+                PCM_EMD_PHASE(1);
+                if (timers) {
+                    a.stats[2 * it] = (int)((__builtin_amdgcn_s_memtime() - it_t0) >> 4);
+                    a.stats[2 * it + 1] = 0;
+                    a.stats[2 * iters + 16 + it] = nu;
+                }
+                continue;
+            }
             if (W == 1) {  // whole bids, one wave each (more than 8 bidders)
                 for (int u = wave; u < nu; u += kWaves) {
                     const int j = Ucur[u];
@@ -1468,6 +1581,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
 
         // ---- B2: full scans of the misses, caches rebuilt
         const int nm = sNm;
+        hi_miss = 2 * nm >= nu;
         if (hist && tid == 0) {
             atomicAdd(&a.stats[2 * it], nu);
             atomicAdd(&a.stats[2 * it + 1], nm);
@@ -1485,7 +1599,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 vm_drain();
                 __syncthreads();
                 if (tid == 0) st_sc1(bw + kBoardGen, gen);
-                PCM_EMD_PHASE(4);
+                PCM_B2_PHASE(4);
                 // the master's own groups (owner 0); an item it scans itself
                 // goes to region A and is marked (miss entry negated) so the
                 // collection skips it
@@ -1497,7 +1611,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     if (lane == 0) st.miss[i] = -1 - j;
                 }
                 __syncthreads();
-                PCM_EMD_PHASE(5);
+                PCM_B2_PHASE(5);
                 // collect the helpers' items once their done words show this
                 // job.  An item whose done word does not arrive within the
                 // bound (a helper that is not resident, or left) keeps its
@@ -1559,15 +1673,15 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     if (act && r != 0) {
                         xA1[tid] = t.a1; xA2[tid] = t.a2; xA3[tid] = t.a3; xQ1[tid] = t.q1; xQ2[tid] = t.q2;
                     }
-                    PCM_EMD_PHASE(4);
+                    PCM_B2_PHASE(4);
                     __syncthreads();
-                    PCM_EMD_PHASE(5);
+                    PCM_B2_PHASE(5);
                     if (act && r == 0) {
                         for (int rr = 1; rr < W; ++rr) {
                             const int o = tid + 64 * rr;
                             lane_top_merge(t, xA1[o], xQ1[o], xA2[o], xQ2[o], xA3[o]);
                         }
-                        PCM_EMD_PHASE(6);
+                        PCM_B2_PHASE(6);
                         float b1, b2, T;
                         int kb;
                         centry *cj = C + (size_t)j * kL;
@@ -1578,7 +1692,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                             CT[j] = T;
                             place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
                         }
-                        PCM_EMD_PHASE(7);
+                        PCM_B2_PHASE(7);
                     }
                 }
             }
@@ -1656,6 +1770,8 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         }
     }
 #undef PCM_EMD_PHASE
+#undef PCM_B2_PHASE
+#undef PCM_TAIL_PHASE
     if (a.H > 0 && tid == 0) st_sc1(bw + kBoardQuit, 1);  // helpers exit
     if (a.stats && tid == 0)  // diagnostics: whole-auction wall time per batch element
         a.stats[3 * iters + 16 + batch] = (int)(__builtin_amdgcn_s_memrealtime() - t_start);

@@ -3,6 +3,7 @@
 iterations) and the training call (generator predictions, eps 0.05, 3000
 iterations), defaults only.  Run once per library (PCM_HIP_LIB=...) in the
 same GPU session, alternating, so box-to-box clock differences cancel."""
+import hashlib
 import os
 import sys
 
@@ -24,7 +25,9 @@ def main():
                                            ("train", pred, points, 0.05, 3000, 5)):
         d = torch.empty(16, 1024, device=dev)
         a = torch.empty(16, 1024, dtype=torch.int32, device=dev)
-        out.append(f"{name} {T.timed(x1, x2, eps, iters, d, a, None, None, reps=reps):.1f} us")
+        t = T.timed(x1, x2, eps, iters, d, a, None, None, reps=reps)
+        h = hashlib.md5(a.cpu().numpy().tobytes() + d.cpu().numpy().tobytes()).hexdigest()[:8]
+        out.append(f"{name} {t:.1f} us [{h}]")  # the hash: same results across builds
     print(os.path.basename(os.environ.get("PCM_HIP_LIB", "libpcm_hip.so")) + ": " + ", ".join(out), flush=True)
 
 

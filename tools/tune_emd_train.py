@@ -81,11 +81,13 @@ def run(name, x1, x2, eps, iters, sweep):
 def generator_clouds(b, dev):
     import fenet
     import train_step as T
-    gen = fenet.seeded_init(fenet.Generator(1024), 0).to(dev).train()
-    images, points = T.synthetic_batch(b, 1024, dev, seed=0)
+    # forward on the CPU: the same clouds in every process and on every box
+    # (MIOpen's convolutions are not bitwise reproducible across processes)
+    gen = fenet.seeded_init(fenet.Generator(1024), 0).train()
+    images, points = T.synthetic_batch(b, 1024, torch.device("cpu"), seed=0)
     with torch.no_grad():
         pred = gen(images)[2].transpose(2, 1).contiguous()
-    return pred, points
+    return pred.to(dev), points.to(dev)
 
 
 def main():

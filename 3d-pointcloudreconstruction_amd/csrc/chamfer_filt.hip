@@ -98,7 +98,7 @@ struct PreDma {
 template <int W, int QPT, int TILE>
 struct FiltLds {
     static constexpr int kScan = 4 * TILE * 4;
-    static constexpr int kTail = 3 * TILE * 4 + 3 * W * 64 * QPT * 4;
+    static constexpr int kTail = 4 * TILE * 4 + 3 * W * 64 * QPT * 4;
     static constexpr int kBytes = kScan > kTail ? kScan : kTail;
 };
 
@@ -108,6 +108,26 @@ template <bool kSc1, typename Tv>
 __device__ __forceinline__ void out_st(Tv *p, Tv v) {
     if constexpr (kSc1) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else *p = v;
+}
+
+// Sum over the wave with DPP steps (row_shr 1, 2, 4, 8, then row_bcast 15
+// and 31; lane 63 holds the total), returned wave-uniform.  A lane the
+// pattern does not feed keeps its value; s_nop 1: two wait states before a
+// DPP read of the previous instruction's result (asm is not hazard-checked).
+#define PCM_DPP_SUM_STEPS(OP)                                                    \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"   \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+    asm volatile(PCM_DPP_SUM_STEPS("v_add_f32_dpp") : "+v"(v));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    asm volatile(PCM_DPP_SUM_STEPS("v_add_u32_dpp") : "+v"(v));
+    return __builtin_amdgcn_readlane(v, 63);
 }
 
 // One 4-candidate group against four queries (QPT = 4): the 24 packed FMAs
@@ -180,10 +200,11 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
     constexpr int kPer = TILE / NT;  // staged points per thread per tile
     constexpr int kTB = 4;           // near-tie queries per cooperative pass
     float(*sU)[TILE] = reinterpret_cast<float(*)[TILE]>(arena);  // ux, uy, uz, w (SoA)
-    float(*sT)[TILE] = reinterpret_cast<float(*)[TILE]>(arena);  // raw x, y, z (after the scan)
-    float(*sBest)[QW] = reinterpret_cast<float(*)[QW]>(arena + 3 * TILE * 4);
-    float(*sSec)[QW] = reinterpret_cast<float(*)[QW]>(arena + 3 * TILE * 4 + W * QW * 4);
-    int(*sChunk)[QW] = reinterpret_cast<int(*)[QW]>(arena + 3 * TILE * 4 + 2 * W * QW * 4);
+    // raw (x, y, z, 0) per point after the scan: one ds_read_b128 per candidate
+    pcm_f4 *sT = reinterpret_cast<pcm_f4 *>(arena);
+    float(*sBest)[QW] = reinterpret_cast<float(*)[QW]>(arena + 4 * TILE * 4);
+    float(*sSec)[QW] = reinterpret_cast<float(*)[QW]>(arena + 4 * TILE * 4 + W * QW * 4);
+    int(*sChunk)[QW] = reinterpret_cast<int(*)[QW]>(arena + 4 * TILE * 4 + 2 * W * QW * 4);
     __shared__ float sD[QW];  // final (distance, index) per query slot
     __shared__ int sK[QW];
     __shared__ unsigned sPlan[QW];  // near-tie: chunks that can hold the answer (below)
@@ -192,7 +213,6 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
     __shared__ float sHD[PARTS][QW];
     __shared__ int sHK[PARTS][QW];
     __shared__ float sRmax[16];
-    __shared__ float sCen[4];
     __shared__ int sList[QW];
     __shared__ int sNList;
 
@@ -200,7 +220,8 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     // raw-tile slot of point p: rotated by its chunk index inside the chunk, so
-    // the rescan's lanes -- one query each, random chunks -- hit 32 banks, not 2
+    // the rescan's lanes -- one query each, random chunks -- spread over the
+    // 16 four-bank groups a ds_read_b128 lane group uses, not one
     static_assert((C & (C - 1)) == 0, "chunk is a power of two");
     auto slot = [](int p) { return (p & ~(C - 1)) | ((p + p / C) & (C - 1)); };
 
@@ -243,22 +264,12 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         }
     }
 
-    if (wave == 0) {
-        cx = wave_sum(cx);
-        cy = wave_sum(cy);
-        cz = wave_sum(cz);
-        float cn = (float)qcnt;
-        cn = wave_sum(cn);
-        if (lane == 0) {
-            sCen[0] = cx / cn;
-            sCen[1] = cy / cn;
-            sCen[2] = cz / cn;
-        }
-    }
-    if (tid == 0) sNList = 0;
-    __syncthreads();
+    if (tid == 0) sNList = 0;  // first read after the staging barrier
+    // every wave holds the same queries, so each reduces them itself (the
+    // same instructions give the same bits): no LDS round trip, no barrier
+    const float cn = (float)wave_sum_dpp(qcnt);
+    const float c0 = wave_sum_dpp(cx) / cn, c1 = wave_sum_dpp(cy) / cn, c2 = wave_sum_dpp(cz) / cn;
     PCM_STAMP(1);
-    const float c0 = sCen[0], c1 = sCen[1], c2 = sCen[2];
 
     // centred queries, splatted for the packed math
     pcm_f2 px[QPT], py[QPT], pz[QPT];
@@ -392,9 +403,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         for (int r = 0; r < kPer; ++r) {
             const int p = tid + r * NT;
             if (p < nt) {
-                sT[0][slot(p)] = tv[r][0];
-                sT[1][slot(p)] = tv[r][1];
-                sT[2][slot(p)] = tv[r][2];
+                sT[slot(p)] = pcm_f4{tv[r][0], tv[r][1], tv[r][2], 0.f};
             }
         }
     }
@@ -459,11 +468,13 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             // target outside the best chunk can reach d_b (the ICP screen's
             // argument, csrc/icp.hip).  Near ties: 0.12 % of random queries
             // with eR alone.
-            const float sq = __builtin_sqrtf(qn2);
-            const float rr = __builtin_sqrtf(rmax2) + sq;
+            // (v_sqrt_f32: within 1 ulp, far inside the 1.001 margins; the
+            // correctly rounded sqrtf is a dozen instructions more per root)
+            const float sq = __builtin_amdgcn_sqrtf(qn2);
+            const float rr = __builtin_amdgcn_sqrtf(rmax2) + sq;
             const float eR = kFiltU16 * (rr * rr) * 1.001f;
             const float db = __builtin_fmaxf((fb + qn2) * 1.0001f + 2.f * eR, 0.f);
-            const float rq = 2.f * sq + __builtin_sqrtf(db);
+            const float rq = 2.f * sq + __builtin_amdgcn_sqrtf(db);
             const float e2 = 2.f * kFiltU16 * __builtin_fminf(rr * rr, rq * rq) * 1.001f;
             proven = (fs - fb) > e2;  // false for NaN
             float hd = PCM_INF;
@@ -476,9 +487,10 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
 #pragma unroll
                         for (int k = 0; k < CP; ++k) {
                             const int kk = slot(min(k0 + k, nt - 1));
-                            tx[k] = sT[0][kk];
-                            ty[k] = sT[1][kk];
-                            tz[k] = sT[2][kk];
+                            const pcm_f4 t4 = sT[kk];
+                            tx[k] = t4.x;
+                            ty[k] = t4.y;
+                            tz[k] = t4.z;
                         }
                     } else {
 #pragma unroll
@@ -568,7 +580,8 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                             if (lane / C == j) c = ch[j];
                         const int k = c * C + (lane & (C - 1));
                         const int sk = slot(min(max(k, 0), nt - 1));
-                        const float d = pcm_sqd(sT[0][sk] - x, sT[1][sk] - y, sT[2][sk] - z);
+                        const pcm_f4 t4 = sT[sk];
+                        const float d = pcm_sqd(t4.x - x, t4.y - y, t4.z - z);
                         if (c >= 0 && k < nt) pcm_lexmin(bd, bk, d, k);
                     }
                 }

@@ -87,6 +87,14 @@ constexpr int kDefaultTailMax = 16;     // bidders at or below which an iteratio
 #define PCM_TAIL_HI 0  // off: 64 measured 2-4 % slower at the training call (r03m)
 #endif
 constexpr int kTailFuseMax = 64;
+// fused tail iterations (below): bit-exact, but measured no faster at the
+// training call (within the +-3 % call-to-call spread) and 3.5 % slower at
+// config 3, where it never runs (the master kernel's code generation moves;
+// r03o) -- a build option
+#ifndef PCM_TAILFUSE
+#define PCM_TAILFUSE 0
+#endif
+constexpr bool kTailFuse = PCM_TAILFUSE;
 constexpr int kTailHi = PCM_TAIL_HI;
 static_assert(kTailHi <= kTailFuseMax, "one lane per bidder in the fused resolve");
 #ifndef PCM_CHAIN_W
@@ -1416,7 +1424,10 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         // ---- tail mode (few bidders; the count never grows): one wave per
         // bidder, full scan without a cache, no cache-bid phase
         const bool tail_hi = !kG && a.tail_max > 0 && nu <= kTailHi && hi_miss;
-        if (it > 0 && (nu <= a.tail_max || tail_hi)) {
+        // the LDS-state form runs every tail iteration fused (below): at most
+        // kTailFuseMax bidders, one lane each
+        const int tail_cap = (kG || !kTailFuse) ? a.tail_max : min(a.tail_max, kTailFuseMax);
+        if (it > 0 && (nu <= tail_cap || tail_hi)) {
             ++tail_its;
             hi_miss = true;  // the count never grows from here
             // W waves per bidder (16 / the next power of two >= nu), each
@@ -1429,7 +1440,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             const int W = nu <= 1 ? 16 : (nu <= 2 ? 8 : (nu <= 4 ? 4 : (nu <= 8 ? 2 : 1)));
 #endif
             const int q = wave / W, r = wave - q * W;
-            if (!kG && (tail_hi || nu * W <= kWaves)) {
+            if (!kG && kTailFuse) {
                 // fused: every part to LDS, one barrier, then wave 0 -- lane
                 // u for bidder u -- merges the parts, places the bids,
                 // resolves them (GetMax + the 1e-6 window claim, as the C

@@ -56,28 +56,12 @@
 // order-preserving int encoding + atomicMax (the reference's CAS loop,
 // emd_cuda.cu:10-20).  Non-finite inputs are outside the reference's
 // contract (coordinates in [0, 1], emd_module.py:9).
-#include <type_traits>
-
 #include "pcm_common.h"
 #include "pcm_internal.h"
 
 namespace {
 
 constexpr int kL = 64;               // cache slots per point (unused slots: id -1)
-// Two tiers: the (at most) kL1 best entries at build time come first, with a
-// bound T1 on the build-time value of every later entry (T1 >= T, the bound of
-// the uncached objects).  Prices only rise, so a value never exceeds its
-// build-time value: a bid whose second best over the first slots exceeds T1
-// is exact without reading the rest of the cache.
-#ifndef PCM_L1
-#define PCM_L1 16
-#endif
-constexpr int kL1 = PCM_L1;
-#ifndef PCM_PREFETCH
-#define PCM_PREFETCH 0
-#endif
-constexpr bool kPrefetch = PCM_PREFETCH;
-constexpr int kTierSteps = 6;        // bisection steps of the tier-1 threshold
 constexpr int kSelectSteps = 8;      // bisection steps when > kL entries clear K3
 constexpr int kSectionSteps = 4;     // quarter-section steps of the reserve thresholds (1/256 of the range)
 #ifndef PCM_SEED_THREADS
@@ -88,7 +72,7 @@ constexpr int kSeedPtsPerWave = 1;   // 4 points per seed workgroup (2: seed 2.2
 constexpr int kSeedPts = kSeedThreads / 64 * kSeedPtsPerWave;
 constexpr int kEmdThreads = 1024;    // auction workgroup (16 waves)
 constexpr int kWaves = kEmdThreads / 64;
-constexpr int kLdsStateMaxN = 2048;  // master state in LDS up to here (52 B x n)
+constexpr int kLdsStateMaxN = 2048;  // master state in LDS up to here (48 B x n)
 constexpr int kStageMaxN = 8192;     // target cloud copied to LDS up to here (12 B x n)
 constexpr int kHelperMaxN = 32768;   // helpers keep a price snapshot in LDS (4 B x n)
 constexpr int kMaxHelpers = 31;
@@ -116,16 +100,7 @@ static_assert(kTailHi <= kTailFuseMax, "one lane per bidder in the fused resolve
 #ifndef PCM_CHAIN_W
 #define PCM_CHAIN_W 16
 #endif
-#ifndef PCM_CHAIN1
-#define PCM_CHAIN1 0
-#endif
 constexpr int kChainW = PCM_CHAIN_W;    // waves a chain-mode bid is split over
-constexpr bool kChain1 = PCM_CHAIN1;     // chain mode with one barrier per iteration (LDS state, eps > 0)
-static_assert(2 * kChainW <= kTailFuseMax, "double-buffered chain parts");
-#ifndef PCM_TAIL_FAST
-#define PCM_TAIL_FAST 1000
-#endif
-constexpr int kTailFastMin = PCM_TAIL_FAST;  // objects per lane from which tail parts scan on approximate keys
 constexpr int kDefaultWsplit = 1;       // most waves one miss's scan is split over (2, 4: measured slower at config 3 and the training call)
 // Reserve (n == kStagePN): every object closer than a radius, built by the
 // seed at zero prices, up to kR entries of {object id, d}.  Radius^2 starts at
@@ -273,13 +248,9 @@ __device__ __forceinline__ float entry_d(float x1, float y1, float z1, const flo
 // into cache[0..kL) (unused slots: id -1).  Returns K* (every uncached key
 // <= K*) or +inf when nothing could be cached.  s1/s2: this lane's entries
 // chosen; d1/d2: their squared distances.
-//
-// Tier 1 (K1 >= K*, every cached key above K1, at most kL1 of them) goes to
-// the first slots: every other cached key is <= K1.  K1 == K* when at most
-// kL1 entries are cached (then everything is tier 1 and T1 == T).
 template <bool kSc1>
 __device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float d2, centry *__restrict__ cache,
-                                              bool &s1, bool &s2, float &K1) {
+                                              bool &s1, bool &s2) {
     const int lane = threadIdx.x & 63;
     float Kstar = wave_max(t.a3);
     s1 = t.a1 > Kstar;
@@ -303,36 +274,10 @@ __device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float 
         m2 = __ballot(s2);
         cnt = __popcll(m1) + __popcll(m2);
     }
-    // tier 1: count(cached, > K1) <= kL1 by bisection between K* (count
-    // cnt > kL1) and the largest key (count 0)
-    K1 = Kstar;
-    unsigned long long t1a = m1, t1b = m2;
-    if (cnt > kL1) {
-        float lo = Kstar, hi = wave_max(t.a1);
-#pragma unroll 1
-        for (int step = 0; step < kTierSteps; ++step) {
-            const float mid = lo + 0.5f * (hi - lo);
-            const int c = __popcll(__ballot(s1 && t.a1 > mid)) + __popcll(__ballot(s2 && t.a2 > mid));
-            if (c > kL1) lo = mid; else hi = mid;
-        }
-        K1 = hi;
-        t1a = __ballot(s1 && t.a1 > K1);
-        t1b = __ballot(s2 && t.a2 > K1);
-    }
-    const unsigned long long t2a = m1 & ~t1a, t2b = m2 & ~t1b;
-    const int c1 = __popcll(t1a) + __popcll(t1b);
     const unsigned long long below = (1ull << lane) - 1ull;
-    const unsigned long long bit = 1ull << lane;
     if (lane < kL && lane >= cnt) st_entry<kSc1>(cache + lane, cpack(-1, 0.f));  // unused slots
-    if (s1) {
-        const int p = (t1a & bit) ? __popcll(t1a & below) : c1 + __popcll(t2a & below);
-        st_entry<kSc1>(cache + p, cpack(t.q1, __builtin_sqrtf(d1)));
-    }
-    if (s2) {
-        const int p = (t1b & bit) ? __popcll(t1a) + __popcll(t1b & below)
-                                  : c1 + __popcll(t2a) + __popcll(t2b & below);
-        st_entry<kSc1>(cache + p, cpack(t.q2, __builtin_sqrtf(d2)));
-    }
+    if (s1) st_entry<kSc1>(cache + __popcll(m1 & below), cpack(t.q1, __builtin_sqrtf(d1)));
+    if (s2) st_entry<kSc1>(cache + __popcll(m1) + __popcll(m2 & below), cpack(t.q2, __builtin_sqrtf(d2)));
     return Kstar;
 }
 
@@ -400,8 +345,7 @@ __device__ __forceinline__ int group_add_i(int v) {
 // non-increasing in d).  T = v(-K*) bounds every uncached value.  The bid is
 // exact whenever b2 > T (caller checks).
 __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const float *Qc, int n,
-                                          centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T,
-                                          float &T1) {
+                                          centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T) {
     const int lane = threadIdx.x & 63;
     LaneTop t;
     lane_top_init(t);
@@ -413,11 +357,9 @@ __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const fl
         for (int r = 0; r < 4; ++r) lane_top_push(t, key[r], k0 + 64 * r);
     }
     bool s1, s2;
-    float K1;
     const float d1 = -t.a1, d2 = -t.a2;  // negation is exact
-    const float Kstar = select_cache<false>(t, d1, d2, cache, s1, s2, K1);
+    const float Kstar = select_cache<false>(t, d1, d2, cache, s1, s2);
     T = Kstar == PCM_INF ? PCM_INF : value_of(-Kstar, 0.f);
-    T1 = K1 == PCM_INF ? PCM_INF : value_of(-K1, 0.f);  // keys -d: K1 >= K* gives T1 >= T
     wave_top2(s1 ? value_of(d1, 0.f) : -PCM_INF, s1 ? t.q1 : 0x7fffffff,
               s2 ? value_of(d2, 0.f) : -PCM_INF, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
 }
@@ -440,7 +382,7 @@ __device__ __forceinline__ float wave_min(float v) { return -wave_max(-v); }
 
 __device__ __forceinline__ void scan_seed_res(float x1, float y1, float z1, const float *Qc, centry *__restrict__ cache,
                                               uint16_t *__restrict__ R, centry *sR, float &b1, int &kb, float &b2,
-                                              float &T, float &T1, int &rn, float &rT) {
+                                              float &T, int &rn, float &rT) {
     constexpr int n = kStagePN, S = n / 256;
     const int lane = threadIdx.x & 63;
     float dd[4 * S];
@@ -469,7 +411,7 @@ __device__ __forceinline__ void scan_seed_res(float x1, float y1, float z1, cons
         }
     }
     if (!ok || cnt > kR) {  // no reserve: the lane-top cache of scan_seed
-        scan_seed(x1, y1, z1, Qc, n, cache, b1, kb, b2, T, T1);
+        scan_seed(x1, y1, z1, Qc, n, cache, b1, kb, b2, T);
         return;
     }
     const unsigned long long below = (1ull << lane) - 1ull;
@@ -507,46 +449,38 @@ __device__ __forceinline__ void scan_seed_res(float x1, float y1, float z1, cons
         for (int i = 0; i < RPL; ++i) c += __popcll(__ballot(d[i] < t));
         return c;
     };
-    // invariant: count(d < lo) <= cap < count(d < hi); quarter sections
-    // (three independent counts per step: a quarter of the dependent
-    // VALU -> SALU round trips of halving); returns lo
-    auto section = [&](float lo, float hi, int cap) {
+    float K = th;  // rn <= kL: the whole reserve
+    if (rn > kL) {
+        // invariant: count(d < lo) <= kL < count(d < hi); quarter sections
+        // (three independent counts per step: a quarter of the dependent
+        // VALU -> SALU round trips of halving)
+        float lo = 0.f, hi = th;
 #pragma unroll 1
         for (int step = 0; step < kSectionSteps; ++step) {
             const float w = 0.25f * (hi - lo);
             const float t1 = lo + w, t2 = lo + 2.f * w, t3 = lo + 3.f * w;
             const int c1 = count_below(t1), c2 = count_below(t2), c3 = count_below(t3);
-            if (c3 <= cap) lo = t3;
-            else if (c2 <= cap) { lo = t2; hi = t3; }
-            else if (c1 <= cap) { lo = t1; hi = t2; }
+            if (c3 <= kL) lo = t3;
+            else if (c2 <= kL) { lo = t2; hi = t3; }
+            else if (c1 <= kL) { lo = t1; hi = t2; }
             else hi = t1;
         }
-        return lo;
-    };
-    const float K = rn > kL ? section(0.f, th, kL) : th;  // rn <= kL: the whole reserve
-    // tier 1: the nearest (at most kL1) cached entries, d < K1 <= K
-    float K1 = K;
-    int c1 = count_below(K);
-    if (c1 > kL1) {
-        K1 = section(0.f, K, kL1);
-        c1 = count_below(K1);
+        K = lo;
     }
     float lmax = -PCM_INF;
     float v[RPL];
-    int p1 = 0, p2 = c1;
+    int cpos = 0;
 #pragma unroll
     for (int i = 0; i < RPL; ++i) {
-        const bool c = d[i] < K, in1 = d[i] < K1;
-        const unsigned long long m1 = __ballot(in1), m2 = __ballot(c && !in1);
-        if (c) cache[in1 ? p1 + __popcll(m1 & below) : p2 + __popcll(m2 & below)] = cpack(k[i], __builtin_sqrtf(d[i]));
-        p1 += __popcll(m1);
-        p2 += __popcll(m2);
+        const bool c = d[i] < K;
+        const unsigned long long m = __ballot(c);
+        if (c) cache[cpos + __popcll(m & below)] = cpack(k[i], __builtin_sqrtf(d[i]));
+        cpos += __popcll(m);
         v[i] = c ? value_of(d[i], 0.f) : -PCM_INF;
         lmax = fmaxf(lmax, v[i]);
     }
-    if (lane < kL && lane >= p2) cache[lane] = cpack(-1, 0.f);
+    if (lane < kL && lane >= cpos) cache[lane] = cpack(-1, 0.f);
     T = value_of(K, 0.f);
-    T1 = value_of(K1, 0.f);
     b1 = wave_max(lmax);
     int lk = 0x7fffffff, lc = 0;
     float lrest = -PCM_INF;
@@ -571,7 +505,7 @@ __device__ __forceinline__ void scan_seed_res(float x1, float y1, float z1, cons
 // kernel past 128 VGPRs into scratch.
 typedef const __attribute__((address_space(3))) float *lds_cfp;
 struct ResBid {
-    float b1, b2, T, T1;
+    float b1, b2, T;
     int kb, ok;
 };
 template <typename Stamp>
@@ -582,7 +516,7 @@ __device__ __forceinline__ ResBid reserve_bid(const uint16_t *__restrict__ R, in
     const int lane = threadIdx.x & 63;
     ResBid r;
     r.ok = 0;
-    r.T = r.T1 = PCM_INF;
+    r.T = PCM_INF;
     bool h[RPL];
     int k[RPL];
     float sv[RPL], v[RPL];
@@ -627,42 +561,39 @@ __device__ __forceinline__ ResBid reserve_bid(const uint16_t *__restrict__ R, in
         for (int i = 0; i < RPL; ++i) c += __popcll(__ballot(v[i] > t));
         return c;
     };
-    // invariant: count(> lo) > cap >= count(> hi); quarter sections; returns hi
-    auto section = [&](float lo, float hi, int cap) {
-#pragma unroll 1
-        for (int step = 0; step < kSectionSteps; ++step) {
-            const float w = 0.25f * (hi - lo);
-            const float t1 = lo + w, t2 = lo + 2.f * w, t3 = lo + 3.f * w;
-            const int c1 = count_above(t1), c2 = count_above(t2), c3 = count_above(t3);
-            if (c1 <= cap) hi = t1;
-            else if (c2 <= cap) { lo = t1; hi = t2; }
-            else if (c3 <= cap) { lo = t2; hi = t3; }
-            else lo = t3;
-        }
-        return hi;
-    };
-    // the cache: v > K (at most kL); tier 1: v > K1 >= K (at most kL1).
-    // Below the reserve's minimum nothing is cached, so the minimum itself
-    // serves as the lower end of both searches
-    const float vmin = wave_min(lmin);
     float K = -PCM_INF;
-    if (rn > kL) K = count_above(vmin) <= kL ? vmin : section(vmin, b1, kL);  // ties at the minimum: all above fit
-    const float lo1 = rn > kL ? K : vmin;
-    const float K1 = count_above(lo1) <= kL1 ? (rn > kL1 ? lo1 : K) : section(lo1, b1, kL1);
+    if (rn > kL) {
+        float lo = wave_min(lmin);
+        if (count_above(lo) <= kL) {
+            K = lo;  // ties at the minimum: everything above it fits
+        } else {
+            // invariant: count(> lo) > kL >= count(> hi); quarter sections
+            float hi = b1;
+#pragma unroll 1
+            for (int step = 0; step < kSectionSteps; ++step) {
+                const float w = 0.25f * (hi - lo);
+                const float t1 = lo + w, t2 = lo + 2.f * w, t3 = lo + 3.f * w;
+                const int c1 = count_above(t1), c2 = count_above(t2), c3 = count_above(t3);
+                if (c1 <= kL) hi = t1;
+                else if (c2 <= kL) { lo = t1; hi = t2; }
+                else if (c3 <= kL) { lo = t2; hi = t3; }
+                else lo = t3;
+            }
+            K = hi;
+        }
+    }
     stamp(11, 0u);
     const unsigned long long below = (1ull << lane) - 1ull;
-    int p1 = 0, p2 = count_above(K1);
+    int pos = 0;
 #pragma unroll
     for (int i = 0; i < RPL; ++i) {
-        const bool c = v[i] > K, in1 = v[i] > K1;
-        const unsigned long long m1 = __ballot(in1), m2 = __ballot(c && !in1);
-        if (c) cache[in1 ? p1 + __popcll(m1 & below) : p2 + __popcll(m2 & below)] = cpack(k[i], sv[i]);
-        p1 += __popcll(m1);
-        p2 += __popcll(m2);
+        const bool c = v[i] > K;
+        const unsigned long long m = __ballot(c);
+        if (c) cache[pos + __popcll(m & below)] = cpack(k[i], sv[i]);
+        pos += __popcll(m);
     }
-    if (lane < kL && lane >= p2) cache[lane] = cpack(-1, 0.f);
+    if (lane < kL && lane >= pos) cache[lane] = cpack(-1, 0.f);
     r.T = fmaxf(rT, K);
-    r.T1 = fmaxf(rT, K1);
     r.ok = 1;
     return r;
 }
@@ -673,7 +604,7 @@ __device__ __forceinline__ ResBid reserve_bid(const uint16_t *__restrict__ R, in
 // parameters every caller kept b1/kb/b2/T in scratch memory, a store and a
 // dependent reload on the fast path of every full scan.
 struct ScanBid {
-    float b1, b2, T, T1;
+    float b1, b2, T;
     int kb;
 };
 template <bool kSc1>
@@ -694,21 +625,18 @@ __device__ __noinline__ ScanBid scan_exact_bid(float x1, float y1, float z1, con
     }
     bool s1, s2;
     ScanBid r;
-    r.T = select_cache<kSc1>(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cache, s1, s2,
-                             r.T1);
+    r.T = select_cache<kSc1>(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cache, s1, s2);
     wave_top2(t.a1, t.q1, t.a2, t.q2, r.b1, r.kb, r.b2);
     return r;
 }
 template <bool kSc1>
 __device__ __forceinline__ void scan_exact(float x1, float y1, float z1, const float *Qc, const float *price, int n,
-                                           centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T,
-                                           float &T1) {
+                                           centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T) {
     const ScanBid r = scan_exact_bid<kSc1>(x1, y1, z1, Qc, price, n, cache);
     b1 = r.b1;
     kb = r.kb;
     b2 = r.b2;
     T = r.T;
-    T1 = r.T1;
 }
 
 // ---- auction full scan, fast: selection on an fp32 approximation
@@ -745,13 +673,11 @@ __device__ __forceinline__ void scan_fast_keys(LaneTop &t, float x1, float y1, f
 template <bool kSc1>
 __device__ __forceinline__ bool scan_fast_finish(const LaneTop &t, float x1, float y1, float z1, const float *Qc,
                                                  const float *price, int n, centry *__restrict__ cache, float &b1,
-                                                 int &kb, float &b2, float &T, float &T1) {
+                                                 int &kb, float &b2, float &T) {
     bool s1, s2;
-    float K1p;
     const float d1 = entry_d(x1, y1, z1, Qc, n, t.q1), d2 = entry_d(x1, y1, z1, Qc, n, t.q2);
-    const float Kp = select_cache<kSc1>(t, d1, d2, cache, s1, s2, K1p);
+    const float Kp = select_cache<kSc1>(t, d1, d2, cache, s1, s2);
     T = Kp + 4.f * 1.1920929e-7f * (6.f + fabsf(Kp));  // +inf stays +inf
-    T1 = K1p + 4.f * 1.1920929e-7f * (6.f + fabsf(K1p));  // the same bound on the keys <= K1' (K1' >= K')
     const float v1 = s1 ? value_of(d1, price[t.q1]) : -PCM_INF;
     const float v2 = s2 ? value_of(d2, price[t.q2]) : -PCM_INF;
     wave_top2(v1, s1 ? t.q1 : 0x7fffffff, v2, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
@@ -768,41 +694,6 @@ __device__ __forceinline__ void part_top2(float x1, float y1, float z1, const fl
     LaneTop t;
     lane_top_init(t);
     for (int k = r * 64 + lane; k < n; k += 64 * W) lane_top_push(t, value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), price[k]), k);
-    wave_top2(t.a1, t.q1, t.a2, t.q2, b1, kb, b2);
-}
-// The same part, selected on scan_fast_keys' fp32-approximate keys: every
-// lane's top-2 by key gets its exact value, and T bounds the exact value of
-// every other object of the part (scan_fast_finish's bound, from the largest
-// lane third key).  The part's exact top-2 is (b1, kb, b2) whenever the
-// merged second best exceeds every part's T; otherwise the caller rescans
-// exactly.  (Pays from ~8 objects per lane: ~10 VALU per key against ~25 for
-// an exact value.)
-__device__ __forceinline__ void part_top2_fast(float x1, float y1, float z1, const float *Qc, const float *price,
-                                               int n, int r, int W, float &b1, int &kb, float &b2, float &T) {
-    const int lane = threadIdx.x & 63;
-    LaneTop t;
-    lane_top_init(t);
-    for (int k = r * 64 + lane; k < n; k += 64 * W)
-        lane_top_push(t, (3.f - __builtin_amdgcn_sqrtf(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k))) - price[k], k);
-    const float Kp = wave_max(t.a3);
-    T = Kp == -PCM_INF ? -PCM_INF : Kp + 4.f * 1.1920929e-7f * (6.f + fabsf(Kp));
-    const bool h1 = (unsigned)t.q1 < (unsigned)n, h2 = (unsigned)t.q2 < (unsigned)n;
-    const float v1 = h1 ? value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)t.q1), price[t.q1]) : -PCM_INF;
-    const float v2 = h2 ? value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)t.q2), price[t.q2]) : -PCM_INF;
-    wave_top2(v1, h1 ? t.q1 : 0x7fffffff, v2, h2 ? t.q2 : 0x7fffffff, b1, kb, b2);
-}
-// part_top2 with up to two objects' prices patched (k1 -> p1 first, then
-// k2 -> p2): the prices of updates the LDS does not hold yet (chain mode)
-__device__ __forceinline__ void part_top2_pp(float x1, float y1, float z1, const float *Qc, const float *price, int n,
-                                             int r, int W, int k1, float p1, int k2, float p2, float &b1, int &kb,
-                                             float &b2) {
-    const int lane = threadIdx.x & 63;
-    LaneTop t;
-    lane_top_init(t);
-    for (int k = r * 64 + lane; k < n; k += 64 * W) {
-        const float p = k == k1 ? p1 : (k == k2 ? p2 : price[k]);
-        lane_top_push(t, value_of(sqd_to(x1, y1, z1, Qc + 3 * (size_t)k), p), k);
-    }
     wave_top2(t.a1, t.q1, t.a2, t.q2, b1, kb, b2);
 }
 // merge of W parts' results (lanes < W read part i's slot); the second
@@ -869,13 +760,12 @@ __device__ __forceinline__ int tie_fix(int kb, float b1, float b2, float x1, flo
 // one wave: the full bid of point (x1, y1, z1) with a rebuilt cache
 template <bool kSc1>
 __device__ __forceinline__ void scan_full(float x1, float y1, float z1, const float *Qc, const float *price, int n,
-                                          centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T,
-                                          float &T1) {
+                                          centry *__restrict__ cache, float &b1, int &kb, float &b2, float &T) {
     LaneTop t;
     lane_top_init(t);
     scan_fast_keys(t, x1, y1, z1, Qc, price, 0, n);
-    if (!scan_fast_finish<kSc1>(t, x1, y1, z1, Qc, price, n, cache, b1, kb, b2, T, T1))
-        scan_exact<kSc1>(x1, y1, z1, Qc, price, n, cache, b1, kb, b2, T, T1);
+    if (!scan_fast_finish<kSc1>(t, x1, y1, z1, Qc, price, n, cache, b1, kb, b2, T))
+        scan_exact<kSc1>(x1, y1, z1, Qc, price, n, cache, b1, kb, b2, T);
 }
 
 // ===========================================================================
@@ -888,10 +778,8 @@ __device__ __forceinline__ void scan_full(float x1, float y1, float z1, const fl
 struct EmdWs {
     centry *cache;   // [b*n*kL] region A
     float *CT;       // [b*n] cache bound (A) or the kInB marker
-    float *CT1;      // [b*n] tier-1 bound (A)
     centry *cacheB;  // [b*n*kL] region B
     float *CTB;      // [b*n] cache bound (B)
-    float *CTB1;     // [b*n] tier-1 bound (B)
     int32_t *bid0;   // [b*n] iteration-0 bid (-2: full scan needed)
     float *inc0;     // [b*n]
     int32_t *board;  // [b*kBoardWords]: gen, quit, jn, err (one 128-B line each)
@@ -965,24 +853,23 @@ __global__ __launch_bounds__(kSeedThreads) void emd_seed_kernel(const float *__r
     for (int p = 0; p < kSeedPtsPerWave; ++p) {
         const int j = j0 + p;
         const size_t pt = (size_t)batch * n + j;
-        float b1, b2, T, T1;
+        float b1, b2, T;
         int kb;
         if constexpr (kRes) {  // n == kStagePN (launch_emd)
             int rn;
             float rT;
             centry *sR = reinterpret_cast<centry *>(sQs + 3 * kStagePN) + wave * kR;  // this wave's reserve copy
             scan_seed_res(qp[p][0], qp[p][1], qp[p][2], Qc, ws.cache + pt * kL, ws.res + pt * kR, sR, b1, kb, b2,
-                          T, T1, rn, rT);
+                          T, rn, rT);
             if (lane == 0) {
                 ws.RN[pt] = rn;
                 ws.RT[pt] = rT;
             }
         } else {
-            scan_seed(qp[p][0], qp[p][1], qp[p][2], Qc, n, ws.cache + pt * kL, b1, kb, b2, T, T1);
+            scan_seed(qp[p][0], qp[p][1], qp[p][2], Qc, n, ws.cache + pt * kL, b1, kb, b2, T);
         }
         if (lane == 0) {
             ws.CT[pt] = T;
-            ws.CT1[pt] = T1;
             const bool proven = b2 > T && (unsigned)kb < (unsigned)n;
             ws.bid0[pt] = proven ? kb : -2;  // -2: needs a full scan in the auction kernel
             ws.inc0[pt] = b1 - b2 + eps;
@@ -1090,20 +977,13 @@ __device__ __forceinline__ void bid_on(const AState<kG> &st, int j, int k, float
 #endif
 template <int G, bool kG>
 __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, const centry *C, const float *CT,
-                                           const float *CT1, const centry *CB, const float *CTB, const float *CTB1,
-                                           const AState<kG> &st, int *sNm, int *coll, const float *resT, int *resN,
-                                           int n, TieRank tr, int *tier2 = nullptr,
+                                           const centry *CB, const float *CTB, const AState<kG> &st, int *sNm,
+                                           int *coll, const float *resT, int *resN, int n, TieRank tr,
                                            unsigned long long *tm = nullptr) {
     (void)tm;
     static_assert(G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
     constexpr int E = kL / G;
     static_assert(E % 2 == 0, "slot pairs");
-    // lane gl evaluates the slot pairs 2 (gl + G e') + {0, 1}: one 16-byte
-    // load per pair (any partition of the kL slots over the group works).
-    // Pairs e' < P1 cover slots [0, 2 G P1) >= [0, kL1): the first pass
-    constexpr int P1 = (kL1 + 2 * G - 1) / (2 * G), E1 = 2 * P1;
-    static_assert(E1 <= E, "first pass within the cache");
-    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     const int gi = threadIdx.x / G, gl = threadIdx.x % G;
     for (int u0 = 0; u0 < nu; u0 += kEmdThreads / G) {
         const int u = u0 + gi;
@@ -1112,101 +992,72 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
         const int j = act ? Ucur[u] : 0;
         PCM_B1_STAMP(5, j);
         // region A (the master's own, plain, L2-resident) is loaded together
-        // with the bounds; a point whose cache a helper rebuilt (marker) is
+        // with the bound; a point whose cache a helper rebuilt (marker) is
         // re-read from region B (sc1)
-        float tj = CT[j], t1j = CT1[j];
+        float tj = CT[j];
         centry ce[E];
+        // lane gl evaluates the slot pairs 2 (gl + G e') + {0, 1}: one 16-byte
+        // load per pair (any partition of the kL slots over the group works)
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
 #pragma unroll
-        for (int e = 0; e < P1; ++e) {
+        for (int e = 0; e < E / 2; ++e) {
             const u64x2 w = *reinterpret_cast<const u64x2 *>(C + (size_t)j * kL + 2 * (gl + G * e));
             ce[2 * e] = w.x;
             ce[2 * e + 1] = w.y;
         }
-        PCM_B1_STAMP(6, (unsigned)ce[0] ^ (unsigned)ce[E1 - 1] ^ __float_as_uint(tj));
-        const bool inB = __float_as_uint(tj) == kInB;
-        const centry *cj = (inB ? CB : C) + (size_t)j * kL;
-        if (inB) {
+        PCM_B1_STAMP(6, (unsigned)ce[0] ^ (unsigned)ce[E - 1] ^ __float_as_uint(tj));
+        if (__float_as_uint(tj) == kInB) {
             tj = ld_sc1(CTB + j);
-            t1j = ld_sc1(CTB1 + j);
 #pragma unroll
-            for (int e = 0; e < P1; ++e) {
-                ce[2 * e] = ld_sc1(cj + 2 * (gl + G * e));
-                ce[2 * e + 1] = ld_sc1(cj + 2 * (gl + G * e) + 1);
+            for (int e = 0; e < E / 2; ++e) {
+                ce[2 * e] = ld_sc1(CB + (size_t)j * kL + 2 * (gl + G * e));
+                ce[2 * e + 1] = ld_sc1(CB + (size_t)j * kL + 2 * (gl + G * e) + 1);
             }
         }
         // values at current prices; an unused slot (k = -1) evaluates object
         // 0 and is then forced to (-inf, INT_MAX), branch-free
         float v[E];
         int kk[E];
-        auto eval = [&](int e) {
+        float lmax = -PCM_INF;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
             const int k = (int)(unsigned)ce[e];
             const float s = __uint_as_float((unsigned)(ce[e] >> 32));
             const int neg = k >> 31;
             const float v0 = value_from_s(s, st.price[k & ~neg]);
             v[e] = __int_as_float((__float_as_int(v0) & ~neg) | (int)(0xff800000u & (unsigned)neg));
             kk[e] = k & 0x7fffffff;
-        };
-        // group top-2 over the first M entries of every lane: best = max,
-        // argbest = lowest id at best, better = best on a tie else the max of
-        // the rest
-        float b1, b2;
-        int kb, ties;
-        auto top2 = [&](auto M) {
-            float lmax = -PCM_INF;
-#pragma unroll
-            for (int e = 0; e < M.value; ++e) lmax = fmaxf(lmax, v[e]);
-            b1 = group_max<G>(lmax);
-            int lk = 0x7fffffff, lc = 0;
-            float lrest = -PCM_INF;
-#pragma unroll
-            for (int e = 0; e < M.value; ++e) {
-                const bool eq = v[e] == b1;
-                lk = eq ? min(lk, kk[e]) : lk;
-                lc += eq ? 1 : 0;
-                lrest = eq ? lrest : fmaxf(lrest, v[e]);
-            }
-            kb = group_min_i<G>(lk);
-            ties = group_add_i<G>(lc);
-            const float rest = group_max<G>(lrest);
-            b2 = ties >= 2 ? b1 : rest;
-        };
-#pragma unroll
-        for (int e = 0; e < E1; ++e) eval(e);
-        PCM_B1_STAMP(7, __float_as_uint(v[0]));
-        top2(std::integral_constant<int, E1>());
-        // every entry past the first pass is <= T1 >= T (group-uniform)
-        bool ok = b2 > t1j && b2 > tj;
-        if constexpr (E1 < E) {
-            if (act && !ok && !(t1j <= tj)) {  // the rest of the cache (T1 == T: nothing past tier 1)
-#pragma unroll
-                for (int e = P1; e < E / 2; ++e) {
-                    if (inB) {
-                        ce[2 * e] = ld_sc1(cj + 2 * (gl + G * e));
-                        ce[2 * e + 1] = ld_sc1(cj + 2 * (gl + G * e) + 1);
-                    } else {
-                        const u64x2 w = *reinterpret_cast<const u64x2 *>(cj + 2 * (gl + G * e));
-                        ce[2 * e] = w.x;
-                        ce[2 * e + 1] = w.y;
-                    }
-                }
-#pragma unroll
-                for (int e = E1; e < E; ++e) eval(e);
-                top2(std::integral_constant<int, E>());
-                ok = b2 > tj;
-                if (tier2 && gl == 0) atomicAdd(tier2, 1);
-            }
+            lmax = fmaxf(lmax, v[e]);
         }
+        PCM_B1_STAMP(7, __float_as_uint(lmax));
+        // group top-2: best = max, argbest = lowest id at best, better = best
+        // on a tie else the max of the rest
+        const float b1 = group_max<G>(lmax);
+        int lk = 0x7fffffff, lc = 0;
+        float lrest = -PCM_INF;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+            const bool eq = v[e] == b1;
+            lk = eq ? min(lk, kk[e]) : lk;
+            lc += eq ? 1 : 0;
+            lrest = eq ? lrest : fmaxf(lrest, v[e]);
+        }
+        int kb = group_min_i<G>(lk);
+        const int ties = group_add_i<G>(lc);
+        const float rest = group_max<G>(lrest);
+        const float b2 = ties >= 2 ? b1 : rest;
         PCM_B1_STAMP(8, __float_as_uint(b2) ^ (unsigned)kb);
         if constexpr (kG) {
             // a tie at the best (group-uniform): the reference's order
-            // decides.  When the bid is proven every object of value b1 is
-            // cached (in the slots evaluated), so the cached entries hold the
-            // winner (out of line: the entries are re-read rather than kept
-            // live; slots not evaluated hold values below b1)
-            if (tr.on && ties >= 2 && ok) kb = cache_tie_winner<G>(cj, inB, st.price, b1, tr, n);
+            // decides.  When the bid is proven (b2 > bound) every object of
+            // value b1 is cached, so the cached entries hold the winner (out
+            // of line: the entries are re-read rather than kept live)
+            if (tr.on && ties >= 2 && b2 > tj)
+                kb = cache_tie_winner<G>(__float_as_uint(CT[j]) == kInB ? CB + (size_t)j * kL : C + (size_t)j * kL,
+                                         __float_as_uint(CT[j]) == kInB, st.price, b1, tr, n);
         }
         if (act && gl == G - 1) {
-            if (ok) {
+            if (b2 > tj) {
                 bid_on(st, j, kb, b1 - b2 + eps, coll);
             } else {
                 st.miss[atomicAdd(sNm, 1)] = j;
@@ -1241,14 +1092,13 @@ __device__ __forceinline__ void helper_item(const EmdWs &ws, size_t base, int i,
                                             const TieRank &tr) {
     const int lane = threadIdx.x & 63;
     const int j = __builtin_amdgcn_readfirstlane(ld_sc1(ws.ml + base + i));
-    float b1, b2, T, T1;
+    float b1, b2, T;
     int kb;
     scan_full<true>(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, price, n, ws.cacheB + (base + j) * kL, b1, kb, b2,
-                    T, T1);
+                    T);
     kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, price, n, tr);
     if (lane == 0) {
         st_sc1(ws.CTB + base + j, T);
-        st_sc1(ws.CTB1 + base + j, T1);
         st_sc1(ws.rbid + base + i, (int)kb);
         st_sc1(ws.rinc + base + i, b1 - b2 + eps);
     }
@@ -1322,7 +1172,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     __shared__ int sNu[2], sNm, sColl[2], sChainJ;  // sColl: [0] some object saw 2 bids, [1] a window contention
     __shared__ float sPb1[kTailFuseMax], sPb2[kTailFuseMax];  // split bids: each part (wave or bidder)
     __shared__ int sPkb[kTailFuseMax];
-    __shared__ float sPT[kWaves];  // split tail bids (fast parts): each part's bound
     const int n = kN > 0 ? kN : a.n, iters = a.iters;
     const float eps = a.eps;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1331,8 +1180,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     const float *Qg = a.xyz2 + base * 3;
     int32_t *bw = ws.board + (size_t)batch * kBoardWords;
     centry *C = ws.cache + base * kL;
-    float *CT = ws.CT + base;    // region-A bounds (LDS copy in the LDS-state forms, below)
-    float *CT1 = ws.CT1 + base;  // region-A tier-1 bounds (likewise)
+    float *CT = ws.CT + base;  // region-A bounds (LDS copy in the LDS-state forms, below)
     const bool hist = a.diag == kDiagHist;
     // diag >= 2: timers of batch element diag - 2
     const bool timers = a.diag >= kDiagTimers && batch == a.diag - kDiagTimers && tid == 0;
@@ -1354,7 +1202,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         st.U1 = (int *)lp; lp += 4 * (size_t)n;
         st.miss = (int *)lp; lp += 4 * (size_t)n;
         CT = (float *)lp; lp += 4 * (size_t)n;  // the bound is read first in every cache bid: LDS, not L2
-        CT1 = (float *)lp; lp += 4 * (size_t)n;
     } else {
         st.ass = ws.g_ass + base; st.inv = ws.g_inv + base; st.price = ws.g_price + base;
         st.mx = ws.g_max + base; st.claim = ws.g_claim + base; st.bid = ws.g_bid + base;
@@ -1387,10 +1234,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         st.mx[j] = f2key(0.f);  // emd_module.py:49 zero-inits max_increments
         st.claim[j] = ~0ull;
         st.U0[j] = j;           // iteration 0: every point bids
-        if constexpr (!kG) {  // the seed's bounds
-            CT[j] = ws.CT[base + j];
-            CT1[j] = ws.CT1[base + j];
-        }
+        if constexpr (!kG) CT[j] = ws.CT[base + j];  // the seed's bounds
         if constexpr (kRes) {
             sRT[j] = ws.RT[base + j];
             sRN[j] = res_on ? ws.RN[base + j] : 0;
@@ -1459,7 +1303,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         if (lane == 0) {
             if (rb.ok) {
                 CT[j] = rb.T;
-                CT1[j] = rb.T1;
                 place_bid(st, j, rb.kb, rb.b1 - rb.b2 + eps, n, sColl);
                 st.miss[q] = -1;
                 if (hist) atomicAdd(&a.stats[2 * iters + 13], 1);  // reserve bids
@@ -1469,7 +1312,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         }
     };
     auto own_scan = [&](int j) {
-        float b1, b2, T, T1;
+        float b1, b2, T;
         int kb;
         centry *cj = C + (size_t)j * kL;
         const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
@@ -1478,28 +1321,23 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         lane_top_init(t);
         scan_fast_keys(t, x1, y1, z1, Qc, st.price, 0, n);
         PCM_EMD_PHASE(6);
-        const bool ok = scan_fast_finish<false>(t, x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T, T1);
+        const bool ok = scan_fast_finish<false>(t, x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
         PCM_EMD_PHASE(7);
         if (!ok) {
-            scan_exact<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T, T1);
+            scan_exact<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
             if (hist && lane == 0) atomicAdd(&a.stats[2 * iters + 15], 1);  // exact fallbacks
             PCM_EMD_PHASE(11);
         }
 #else
-        scan_full<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T, T1);
+        scan_full<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
 #endif
         kb = tie_fix<kG>(kb, b1, b2, x1, y1, z1, Qc, st.price, n, tr);
         if (lane == 0) {
             CT[j] = T;
-            CT1[j] = T1;
             place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
         }
     };
     int active = 0, chain_its = 0, tail_its = 0;
-    // the next iteration's bidders' first-pass cache lines, loaded in D so
-    // that B1 finds them in this CU's L1 (the values are consumed, unused, at
-    // B1: the load completes off the critical path)
-    int pf0 = 0, pf1 = 0;
     bool hi_miss = false;  // the last cache-bid iteration missed on at least half its bids
     for (int it = 0; it < iters; ++it) {
         const bool last = (it == iters - 1);
@@ -1529,77 +1367,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         // of its lane top-2 are latency-bound.)
         if (it > 0 && nu == 1 && a.tail_max > 0) {
             int j = Ucur[0];
-            if (!kG && kChain1 && eps > 0.f) {
-                // One barrier per iteration (LDS state, eps > 0, so every bid
-                // wins: no other bid in the iteration, maxima reset).  Every
-                // wave merges the parts itself and resolves identically; the
-                // owner/price writes of iteration t are made by wave 0 during
-                // t + 1, after its barrier, when no wave still reads the old
-                // owner.  Until every wave is past them, the last two updates
-                // are applied in registers (patched prices, patched owners).
-                int k1 = -1, k2 = -1, j1 = -1;  // pending updates: t - 1 (k1) and t - 2 (k2)
-                float p1 = 0.f, p2 = 0.f;
-                for (; it < iters; ++it) {
-                    ++active;
-                    ++chain_its;
-                    PCM_EMD_PHASE(8);
-                    if (hist && tid == 0) {
-                        atomicAdd(&a.stats[2 * it], 1);
-                        atomicAdd(&a.stats[2 * it + 1], 1);
-                    }
-                    float *pb1 = sPb1 + (it & 1) * kChainW, *pb2 = sPb2 + (it & 1) * kChainW;
-                    int *pkb = sPkb + (it & 1) * kChainW;
-                    const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
-                    if (wave < kChainW) {
-                        float b1, b2;
-                        int kb;
-                        part_top2_pp(x1, y1, z1, Qc, st.price, n, wave, kChainW, k1, p1, k2, p2, b1, kb, b2);
-                        if (lane == 0) { pb1[wave] = b1; pkb[wave] = kb; pb2[wave] = b2; }
-                    }
-                    __syncthreads();
-                    PCM_EMD_PHASE(9);
-                    float b1, b2;
-                    int kb;
-                    part_merge(pb1, pkb, pb2, kChainW, b1, kb, b2);
-                    // update t - 2 has been written (by wave 0 before this
-                    // barrier): write t - 1 now
-                    if (wave == 0 && lane == 0 && k1 >= 0) {
-                        st.inv[k1] = j1;
-                        st.price[k1] = p1;
-                    }
-                    int next = j;  // no bid (all-NaN values): j bids again
-                    if ((unsigned)kb < (unsigned)n) {
-                        if (it == iters - 1) {
-                            if (wave == 0 && lane == 0) st.ass[j] = kb;
-                            next = -1;
-                        } else {
-                            const float inc = b1 - b2 + eps;
-                            const int old = kb == k1 ? j1 : st.inv[kb];       // update t - 2 is visible
-                            const float pold = kb == k1 ? p1 : (kb == k2 ? p2 : st.price[kb]);
-                            if (wave == 0 && lane == 0) {  // nothing else reads these in chain mode
-                                if (old != -1) st.ass[old] = -1;
-                                st.ass[j] = kb;
-                                st.mx[kb] = f2key(-1e9f);
-                            }
-                            k2 = k1;
-                            p2 = p1;
-                            k1 = kb;
-                            j1 = j;
-                            p1 = pold + inc;
-                            next = old;
-                        }
-                    }
-                    PCM_EMD_PHASE(10);
-                    j = next;
-                    if (j < 0) break;
-                }
-                if (wave == 0 && lane == 0 && k1 >= 0) {  // the last pending update
-                    st.inv[k1] = j1;
-                    st.price[k1] = p1;
-                }
-                __syncthreads();
-                break;
-            }
             for (; it < iters; ++it) {
                 ++active;
                 ++chain_its;
@@ -1766,26 +1533,21 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 }
                 continue;
             }
-            // fast parts (approximate keys, proven) from 8 objects per lane
-            const bool fast = n / (64 * W) >= kTailFastMin;
             if (W == 1) {  // whole bids, one wave each (more than 8 bidders)
                 for (int u = wave; u < nu; u += kWaves) {
                     const int j = Ucur[u];
-                    const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
-                    float b1 = -PCM_INF, b2 = -PCM_INF, T = PCM_INF;
-                    int kb = 0x7fffffff;
-                    if (fast) part_top2_fast(x1, y1, z1, Qc, st.price, n, 0, 1, b1, kb, b2, T);
-                    if (!(b2 > T)) part_top2(x1, y1, z1, Qc, st.price, n, 0, 1, b1, kb, b2);
-                    kb = tie_fix<kG>(kb, b1, b2, x1, y1, z1, Qc, st.price, n, tr);
+                    float b1, b2;
+                    int kb;
+                    part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, 0, 1, b1, kb, b2);
+                    kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, tr);
                     if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
                 }
             } else if (q < nu) {
                 const int j = Ucur[q];
-                float b1, b2, T = -PCM_INF;
+                float b1, b2;
                 int kb;
-                if (fast) part_top2_fast(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, r, W, b1, kb, b2, T);
-                else part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, r, W, b1, kb, b2);
-                if (lane == 0) { sPb1[wave] = b1; sPkb[wave] = kb; sPb2[wave] = b2; sPT[wave] = T; }
+                part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, r, W, b1, kb, b2);
+                if (lane == 0) { sPb1[wave] = b1; sPkb[wave] = kb; sPb2[wave] = b2; }
             }
             if (hist && tid == 0) {
                 atomicAdd(&a.stats[2 * it], nu);
@@ -1797,11 +1559,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 int kb;
                 part_merge(sPb1 + wave, sPkb + wave, sPb2 + wave, W, b1, kb, b2);
                 const int j = Ucur[q];
-                if (fast) {  // every part's unlisted objects lie at or below its bound
-                    float T = -PCM_INF;
-                    for (int p = 0; p < W; ++p) T = fmaxf(T, sPT[wave + p]);
-                    if (!(b2 > T)) part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, 0, 1, b1, kb, b2);
-                }
                 kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, tr);
                 if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
             }
@@ -1809,7 +1566,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             PCM_EMD_PHASE(1);
         } else {
         // ---- B1: bids from the seed (iteration 0) or the caches; misses listed
-        if (kPrefetch) asm volatile("" ::"v"(pf0), "v"(pf1));
         if (it == 0) {
             for (int u = tid; u < nu; u += kEmdThreads) {
                 const int j = Ucur[u];
@@ -1827,11 +1583,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             const float *rT = kRes ? sRT : nullptr;
             int *rN = kRes ? sRN : nullptr;
             unsigned long long *tm = timers ? sTm : nullptr;
-            const float *CTB1 = ws.CTB1 + base;
-            int *t2 = hist ? &a.stats[2 * iters + 9] : nullptr;  // bids that read past tier 1
-            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CT1, CB, CTB, CTB1, st, &sNm, sColl, rT, rN, n, tr, t2, tm);
-            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CT1, CB, CTB, CTB1, st, &sNm, sColl, rT, rN, n, tr, t2, tm);
-            else cache_bids<4>(nu, eps, Ucur, C, CT, CT1, CB, CTB, CTB1, st, &sNm, sColl, rT, rN, n, tr, t2, tm);
+            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
+            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
+            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
         }
         __syncthreads();
         PCM_EMD_PHASE(0);
@@ -1939,15 +1693,14 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                             lane_top_merge(t, xA1[o], xQ1[o], xA2[o], xQ2[o], xA3[o]);
                         }
                         PCM_B2_PHASE(6);
-                        float b1, b2, T, T1;
+                        float b1, b2, T;
                         int kb;
                         centry *cj = C + (size_t)j * kL;
-                        if (!scan_fast_finish<false>(t, x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T, T1))
-                            scan_exact<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T, T1);
+                        if (!scan_fast_finish<false>(t, x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T))
+                            scan_exact<false>(x1, y1, z1, Qc, st.price, n, cj, b1, kb, b2, T);
                         kb = tie_fix<kG>(kb, b1, b2, x1, y1, z1, Qc, st.price, n, tr);
                         if (lane == 0) {
                             CT[j] = T;
-                            CT1[j] = T1;
                             place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
                         }
                         PCM_B2_PHASE(7);
@@ -2017,11 +1770,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 if (lane == 0 && bal) pos = atomicAdd(&sNu[cur ^ 1], __popcll(bal));
                 pos = __shfl(pos, 0, 64);
                 if (push >= 0) Unext[pos + __popcll(bal & ((1ull << lane) - 1ull))] = push;
-                if (kPrefetch && push >= 0) {
-                    const int *l = reinterpret_cast<const int *>(C + (size_t)push * kL);
-                    pf0 = l[0];
-                    if constexpr (kL1 > 16) pf1 = l[32];  // the second 128-B line
-                }
             }
         }
         __syncthreads();
@@ -2124,10 +1872,8 @@ size_t ws_layout(int b, int n, EmdWs *w, char *basep) {
     EmdWs t{};
     t.cache = (centry *)take(pts * kL * sizeof(centry));
     t.CT = (float *)take(pts * 4);
-    t.CT1 = (float *)take(pts * 4);
     t.cacheB = (centry *)take(pts * kL * sizeof(centry));
     t.CTB = (float *)take(pts * 4);
-    t.CTB1 = (float *)take(pts * 4);
     t.bid0 = (int32_t *)take(pts * 4);
     t.inc0 = (float *)take(pts * 4);
     t.board = (int32_t *)take((size_t)b * kBoardWords * 4);
@@ -2220,7 +1966,7 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     const size_t xchg = 5 * (size_t)kEmdThreads * 4;
     const bool stage_p = n <= (g_state ? 4096 : kStagePN);  // !g_state: n == kStagePN exactly
     const bool res = !g_state && stage_p;  // n == kStagePN: the reserve form (bounds + counts in LDS)
-    const size_t m_lds = (g_state ? 0 : 52 * (size_t)n) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
+    const size_t m_lds = (g_state ? 0 : 48 * (size_t)n) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
                          xchg + (res ? 8 * (size_t)n : 0);
     const size_t h_lds = H > 0 ? (stage ? 12 * (size_t)n : 0) + 4 * (size_t)n : 0;
     size_t lds = m_lds > h_lds ? m_lds : h_lds;

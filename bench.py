@@ -226,7 +226,6 @@ def emd_leg(dev, reps=10, eps=EMD_EPS, iters=EMD_ITERS, clouds=None, label="unif
     bids = int(per[:, 0].sum())
     misses = int(per[:, 1].sum())  # cache misses; the reserve bids some of them without a full scan
     reserve_bids = int(st[2 * iters + 13].item())
-    past_tier1 = int(st[2 * iters + 9].item())  # cache bids that read past the first kL1 entries
     full_scans = misses - reserve_bids
 
     def run():
@@ -238,7 +237,7 @@ def emd_leg(dev, reps=10, eps=EMD_EPS, iters=EMD_ITERS, clouds=None, label="unif
     return {"config": f"B={b} N=M={n} iters={iters} eps={eps}", "clouds": label,
             "ms_per_forward": us / 1000.0, "iters_requested": iters, "iters_run": active,
             "iters_per_s": iters / (us * 1e-6), "active_iters_per_s": active / (us * 1e-6),
-            "bids": bids, "cache_misses": misses, "reserve_bids": reserve_bids, "full_scans": full_scans, "past_tier1": past_tier1, "bid_pair_evals_per_s": pairs / (us * 1e-6),
+            "bids": bids, "cache_misses": misses, "reserve_bids": reserve_bids, "full_scans": full_scans, "bid_pair_evals_per_s": pairs / (us * 1e-6),
             "roofline": {"bound": "valu", "kernel": "emd_seed_kernel + emd_auction_kernel",
                          "achieved": lane_ops / 1e12, "peak": VALU_LANE_OPS_PEAK / 1e12,
                          "unit": "T lane-ops/s", "frac": lane_ops / VALU_LANE_OPS_PEAK,

@@ -39,7 +39,7 @@ def main():
     wall = [w / 100.0 for w in st[3 * iters + 16:3 * iters + 16 + b].tolist()]
     lib = os.path.basename(os.environ.get("PCM_HIP_LIB", "libpcm_hip.so"))
     print(f"{lib}: bids {int(per[:, 0].sum())} misses {int(per[:, 1].sum())} reserve bids {misc[13]} "
-          f"jobs {misc[10]} past-tier-1 {misc[9]}; wall us min {min(wall):.1f} med {sorted(wall)[b // 2]:.1f} max {max(wall):.1f}")
+          f"jobs {misc[10]}; wall us min {min(wall):.1f} med {sorted(wall)[b // 2]:.1f} max {max(wall):.1f}")
     if "--hist" in sys.argv:  # bids / misses per iteration, summed over the batch, in bins
         pr = per.numpy()
         last = int(np.nonzero(pr[:, 0])[0].max()) + 1 if pr[:, 0].any() else 0

@@ -1,5 +1,5 @@
 # EMD iteration: parity tests of the default build and of the feature
-# variant lib/libpcm_hip_vall.so, then the same-box A/B of every build and
+# variant lib/libpcm_hip_vtr.so, then the same-box A/B of every build and
 # per-build config-3 diagnostics (tag = $1)
 set -o pipefail
 export TMPDIR=/tmp
@@ -8,6 +8,6 @@ L=3d-pointcloudreconstruction_amd/lib
 mkdir -p gpurun_out/$T
 timeout -k 10 600 python -u -m pytest tests/test_emd_gpu.py tests/test_train_gpu.py -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/$T/pytest.log 2>&1 || { echo tests failed; grep -E "FAILED|^E " gpurun_out/$T/pytest.log | head -30; exit 1; }
 tail -1 gpurun_out/$T/pytest.log
-PCM_HIP_LIB=$PWD/$L/libpcm_hip_vall.so timeout -k 10 600 python -u -m pytest tests/test_emd_gpu.py tests/test_train_gpu.py -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/$T/pytest_vall.log 2>&1 || { echo vall tests failed; grep -E "FAILED|^E " gpurun_out/$T/pytest_vall.log | head -30; exit 1; }
-echo "vall: $(tail -1 gpurun_out/$T/pytest_vall.log)"
+PCM_HIP_LIB=$PWD/$L/libpcm_hip_vtr.so timeout -k 10 600 python -u -m pytest tests/test_emd_gpu.py tests/test_train_gpu.py -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/$T/pytest_vtr.log 2>&1 || { echo vtr tests failed; grep -E "FAILED|^E " gpurun_out/$T/pytest_vtr.log | head -30; exit 1; }
+echo "vtr: $(tail -1 gpurun_out/$T/pytest_vtr.log)"
 bash tools/r3_emdab2.sh $T

@@ -51,8 +51,8 @@ GRAPH_STEPS = 10                   # steps captured per hipGraph replay
 # up in for roofline.traffic (tools/pmc_passes.sh + tools/pmc_summarize.py)
 FWD_KERNEL = "chamfer_fwd_filt_kernel<float, 8, 4, 32, 2048, 3>"  # default fused-loss forward
 BWD_KERNEL = "chamfer_bwd_staged_kernel"
-FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true>"  # the default variant (granule hand-off)
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r02", "pmc_summary.json")
+FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false>"  # the default variant (granule hand-off)
+PMC_SUMMARY = os.path.join(REPO, "profiles", "r03", "pmc_summary.json")
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0
@@ -469,7 +469,7 @@ def main():
                      "achieved": dom_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": dom_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": pmc_bytes(dom_kernel),
                      "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE*2+WRITE_SIZE, "
-                                     "profiles/r02/pmc_summary.json)",
+                                     "profiles/r03/pmc_summary.json)",
                      "kernel_us": dom_us,
                      "note": "FLOPs = 8 per point pair (algorithmic); VALU-bound, see DESIGN.md"},
         "roofline_hbm": {"bound": "hbm", "kernel": dom_kernel,

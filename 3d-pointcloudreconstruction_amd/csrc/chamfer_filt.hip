@@ -1821,6 +1821,8 @@ const GradVariant kGradVariants[] = {
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, true>, 8, 4},  // 6: screen on the matrix cores
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true>, 8, 4},  // 7: granule hand-off
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, true>, 8, 4},  // 8: 7 + the clouds copied during the scan
+    {chamfer_loss_grad_kernel<8, 4, 8, 1024, false, true>, 8, 4},   // 9: 7 with 8-candidate chunks
+    {chamfer_loss_grad_kernel<8, 4, 32, 1024, false, true>, 8, 4},  // 10: 7 with 32-candidate chunks
 };
 constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
 // tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,

@@ -250,7 +250,7 @@ __device__ __forceinline__ float entry_d(float x1, float y1, float z1, const flo
 // chosen; d1/d2: their squared distances.
 template <bool kSc1>
 __device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float d2, centry *__restrict__ cache,
-                                              bool &s1, bool &s2) {
+                                              bool &s1, bool &s2, int n) {
     const int lane = threadIdx.x & 63;
     float Kstar = wave_max(t.a3);
     s1 = t.a1 > Kstar;
@@ -275,7 +275,7 @@ __device__ __forceinline__ float select_cache(const LaneTop &t, float d1, float 
         cnt = __popcll(m1) + __popcll(m2);
     }
     const unsigned long long below = (1ull << lane) - 1ull;
-    if (lane < kL && lane >= cnt) st_entry<kSc1>(cache + lane, cpack(-1, 0.f));  // unused slots
+    if (lane < kL && lane >= cnt) st_entry<kSc1>(cache + lane, cpack(n, 0.f));  // unused slots: the sentinel
     if (s1) st_entry<kSc1>(cache + __popcll(m1 & below), cpack(t.q1, __builtin_sqrtf(d1)));
     if (s2) st_entry<kSc1>(cache + __popcll(m1) + __popcll(m2 & below), cpack(t.q2, __builtin_sqrtf(d2)));
     return Kstar;
@@ -358,7 +358,7 @@ __device__ __forceinline__ void scan_seed(float x1, float y1, float z1, const fl
     }
     bool s1, s2;
     const float d1 = -t.a1, d2 = -t.a2;  // negation is exact
-    const float Kstar = select_cache<false>(t, d1, d2, cache, s1, s2);
+    const float Kstar = select_cache<false>(t, d1, d2, cache, s1, s2, n);
     T = Kstar == PCM_INF ? PCM_INF : value_of(-Kstar, 0.f);
     wave_top2(s1 ? value_of(d1, 0.f) : -PCM_INF, s1 ? t.q1 : 0x7fffffff,
               s2 ? value_of(d2, 0.f) : -PCM_INF, s2 ? t.q2 : 0x7fffffff, b1, kb, b2);
@@ -479,7 +479,7 @@ __device__ __forceinline__ void scan_seed_res(float x1, float y1, float z1, cons
         v[i] = c ? value_of(d[i], 0.f) : -PCM_INF;
         lmax = fmaxf(lmax, v[i]);
     }
-    if (lane < kL && lane >= cpos) cache[lane] = cpack(-1, 0.f);
+    if (lane < kL && lane >= cpos) cache[lane] = cpack(n, 0.f);
     T = value_of(K, 0.f);
     b1 = wave_max(lmax);
     int lk = 0x7fffffff, lc = 0;
@@ -592,7 +592,7 @@ __device__ __forceinline__ ResBid reserve_bid(const uint16_t *__restrict__ R, in
         if (c) cache[pos + __popcll(m & below)] = cpack(k[i], sv[i]);
         pos += __popcll(m);
     }
-    if (lane < kL && lane >= pos) cache[lane] = cpack(-1, 0.f);
+    if (lane < kL && lane >= pos) cache[lane] = cpack(kStagePN, 0.f);  // the reserve form: n == kStagePN
     r.T = fmaxf(rT, K);
     r.ok = 1;
     return r;
@@ -625,7 +625,8 @@ __device__ __noinline__ ScanBid scan_exact_bid(float x1, float y1, float z1, con
     }
     bool s1, s2;
     ScanBid r;
-    r.T = select_cache<kSc1>(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cache, s1, s2);
+    r.T = select_cache<kSc1>(t, entry_d(x1, y1, z1, Qc, n, t.q1), entry_d(x1, y1, z1, Qc, n, t.q2), cache, s1, s2,
+                             n);
     wave_top2(t.a1, t.q1, t.a2, t.q2, r.b1, r.kb, r.b2);
     return r;
 }
@@ -676,7 +677,7 @@ __device__ __forceinline__ bool scan_fast_finish(const LaneTop &t, float x1, flo
                                                  int &kb, float &b2, float &T) {
     bool s1, s2;
     const float d1 = entry_d(x1, y1, z1, Qc, n, t.q1), d2 = entry_d(x1, y1, z1, Qc, n, t.q2);
-    const float Kp = select_cache<kSc1>(t, d1, d2, cache, s1, s2);
+    const float Kp = select_cache<kSc1>(t, d1, d2, cache, s1, s2, n);
     T = Kp + 4.f * 1.1920929e-7f * (6.f + fabsf(Kp));  // +inf stays +inf
     const float v1 = s1 ? value_of(d1, price[t.q1]) : -PCM_INF;
     const float v2 = s2 ? value_of(d2, price[t.q2]) : -PCM_INF;
@@ -926,7 +927,7 @@ __device__ __noinline__ int cache_tie_winner(const centry *cj, bool sc1, const f
         const int slot = 2 * (gl + G * (e >> 1)) + (e & 1);
         const centry c = sc1 ? ld_sc1(cj + slot) : cj[slot];
         const int k = (int)(unsigned)c;
-        if (k < 0) continue;
+        if ((unsigned)k >= (unsigned)n) continue;  // unused slot (the sentinel n)
         if (value_from_s(__uint_as_float((unsigned)(c >> 32)), price[k]) == b1) lr = min(lr, tie_key(tr, k, n));
     }
     return group_min_i<G>(lr) & ((1 << kTieKBits) - 1);
@@ -1014,8 +1015,11 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
                 ce[2 * e + 1] = ld_sc1(CB + (size_t)j * kL + 2 * (gl + G * e) + 1);
             }
         }
-        // values at current prices; an unused slot (k = -1) evaluates object
-        // 0 and is then forced to (-inf, INT_MAX), branch-free
+        // values at current prices.  An unused slot names the sentinel
+        // object n with s = 0: in the LDS-state form price[n] = +inf, so its
+        // value is -inf with no masking (and it never equals a best); the
+        // global-state form (prices of the next element follow) masks it to
+        // (-inf, INT_MAX)
         float v[E];
         int kk[E];
         float lmax = -PCM_INF;
@@ -1023,10 +1027,15 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
         for (int e = 0; e < E; ++e) {
             const int k = (int)(unsigned)ce[e];
             const float s = __uint_as_float((unsigned)(ce[e] >> 32));
-            const int neg = k >> 31;
-            const float v0 = value_from_s(s, st.price[k & ~neg]);
-            v[e] = __int_as_float((__float_as_int(v0) & ~neg) | (int)(0xff800000u & (unsigned)neg));
-            kk[e] = k & 0x7fffffff;
+            if constexpr (kG) {
+                const bool bad = (unsigned)k >= (unsigned)n;
+                const float v0 = value_from_s(s, st.price[bad ? 0 : k]);
+                v[e] = bad ? -PCM_INF : v0;
+                kk[e] = bad ? 0x7fffffff : k;
+            } else {
+                v[e] = value_from_s(s, st.price[k]);
+                kk[e] = k;
+            }
             lmax = fmaxf(lmax, v[e]);
         }
         PCM_B1_STAMP(7, __float_as_uint(lmax));
@@ -1193,7 +1202,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     if constexpr (!kG) {
         st.ass = (int *)lp; lp += 4 * (size_t)n;
         st.inv = (int *)lp; lp += 4 * (size_t)n;
-        st.price = (float *)lp; lp += 4 * (size_t)n;
+        st.price = (float *)lp; lp += 4 * (size_t)n + 8;  // + the sentinel price[n] = +inf (8: claim alignment)
         st.mx = (int *)lp; lp += 4 * (size_t)n;
         st.claim = (ckey *)lp; lp += 8 * (size_t)n;
         st.bid = (int *)lp; lp += 4 * (size_t)n;
@@ -1231,6 +1240,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         st.ass[j] = -1;
         st.inv[j] = -1;
         st.price[j] = 0.f;
+        if constexpr (!kG) if (j == 0) st.price[n] = PCM_INF;  // the unused cache slots' object
         st.mx[j] = f2key(0.f);  // emd_module.py:49 zero-inits max_increments
         st.claim[j] = ~0ull;
         st.U0[j] = j;           // iteration 0: every point bids
@@ -1966,7 +1976,7 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     const size_t xchg = 5 * (size_t)kEmdThreads * 4;
     const bool stage_p = n <= (g_state ? 4096 : kStagePN);  // !g_state: n == kStagePN exactly
     const bool res = !g_state && stage_p;  // n == kStagePN: the reserve form (bounds + counts in LDS)
-    const size_t m_lds = (g_state ? 0 : 48 * (size_t)n) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
+    const size_t m_lds = (g_state ? 0 : 48 * (size_t)n + 8) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
                          xchg + (res ? 8 * (size_t)n : 0);
     const size_t h_lds = H > 0 ? (stage ? 12 * (size_t)n : 0) + 4 * (size_t)n : 0;
     size_t lds = m_lds > h_lds ? m_lds : h_lds;

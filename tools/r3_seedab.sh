@@ -8,6 +8,7 @@ mkdir -p gpurun_out/$T
 bash tools/ab_emd.sh > gpurun_out/$T/ab.txt 2>&1 || { echo ab failed; tail gpurun_out/$T/ab.txt; exit 1; }
 grep -v amdgpu.ids gpurun_out/$T/ab.txt
 for lib in $L/libpcm_hip_v*.so $L/libpcm_hip.so; do
+  [ -f "$lib" ] || continue
   v=$(basename $lib .so)
   PCM_HIP_LIB=$lib timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/$T/kt_$v -o run -- python3 tools/emd_once.py > gpurun_out/$T/kt_$v.log 2>&1 || { echo rocprof failed; tail gpurun_out/$T/kt_$v.log; exit 1; }
   f=$(find gpurun_out/$T/kt_$v -name "*kernel_stats.csv" | head -1)

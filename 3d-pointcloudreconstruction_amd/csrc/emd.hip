@@ -908,11 +908,18 @@ struct AState {
 // Cache bids: G lanes per bidder, kL/G cached (id, s) entries per lane at
 // current prices, a row_shr reduction over the G lanes (G divides the 16-lane
 // DPP row); the group's last lane places the bid or lists a full scan.
+#ifndef PCM_G16_MAX
+#define PCM_G16_MAX 64
+#endif
+#ifndef PCM_G8_MAX
+#define PCM_G8_MAX 256
+#endif
+constexpr int kG16Max = PCM_G16_MAX, kG8Max = PCM_G8_MAX;  // bidder counts up to which 16 / 8 lanes bid each
 __device__ __forceinline__ int cache_bid_lanes(int nu) {
     // measured per bidder count on MI355X (tools/tune_emd.py, profiles/r01):
     // few bidders are latency-bound (more lanes per bidder), many are
     // VALU-bound (fewer lanes, fewer reduction steps per bidder)
-    return nu <= 64 ? 16 : (nu <= 256 ? 8 : 4);
+    return nu <= kG16Max ? 16 : (nu <= kG8Max ? 8 : 4);
 }
 
 // the reference's winner among a group's cached entries of value b1 (rare:

@@ -1029,7 +1029,10 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
         // (-inf, INT_MAX)
         float v[E];
         int kk[E];
-        float lmax = -PCM_INF;
+        // the lane's two largest values (multiset: a repeated best is kept
+        // twice), two instructions per entry (values are never NaN: cached
+        // entries have finite s, prices are finite or +inf)
+        float m1 = -PCM_INF, m2 = -PCM_INF;
 #pragma unroll
         for (int e = 0; e < E; ++e) {
             const int k = (int)(unsigned)ce[e];
@@ -1043,25 +1046,23 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
                 v[e] = value_from_s(s, st.price[k]);
                 kk[e] = k;
             }
-            lmax = fmaxf(lmax, v[e]);
+            m2 = __builtin_amdgcn_fmed3f(m1, m2, v[e]);
+            m1 = fmaxf(m1, v[e]);
         }
         PCM_B1_STAMP(7, __float_as_uint(lmax));
         // group top-2: best = max, argbest = lowest id at best, better = best
-        // on a tie else the max of the rest
-        const float b1 = group_max<G>(lmax);
-        int lk = 0x7fffffff, lc = 0;
-        float lrest = -PCM_INF;
+        // when two entries hold it (two lanes' maxima, or a lane's two), else
+        // the max of the best lane's second and the other lanes' maxima
+        const float b1 = group_max<G>(m1);
+        int lk = 0x7fffffff;
 #pragma unroll
-        for (int e = 0; e < E; ++e) {
-            const bool eq = v[e] == b1;
-            lk = eq ? min(lk, kk[e]) : lk;
-            lc += eq ? 1 : 0;
-            lrest = eq ? lrest : fmaxf(lrest, v[e]);
-        }
+        for (int e = 0; e < E; ++e) lk = v[e] == b1 ? min(lk, kk[e]) : lk;
         int kb = group_min_i<G>(lk);
-        const int ties = group_add_i<G>(lc);
-        const float rest = group_max<G>(lrest);
-        const float b2 = ties >= 2 ? b1 : rest;
+        const bool top = m1 == b1;
+        const int ntop = group_add_i<G>(top ? 1 : 0);
+        const float rest = group_max<G>(top ? m2 : m1);
+        const float b2 = ntop >= 2 ? b1 : rest;
+        const int ties = b2 == b1 ? 2 : 1;  // a tie at the best
         PCM_B1_STAMP(8, __float_as_uint(b2) ^ (unsigned)kb);
         if constexpr (kG) {
             // a tie at the best (group-uniform): the reference's order

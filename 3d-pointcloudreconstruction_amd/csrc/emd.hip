@@ -1049,7 +1049,7 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
             m2 = __builtin_amdgcn_fmed3f(m1, m2, v[e]);
             m1 = fmaxf(m1, v[e]);
         }
-        PCM_B1_STAMP(7, __float_as_uint(lmax));
+        PCM_B1_STAMP(7, __float_as_uint(m1));
         // group top-2: best = max, argbest = lowest id at best, better = best
         // when two entries hold it (two lanes' maxima, or a lane's two), else
         // the max of the best lane's second and the other lanes' maxima

@@ -50,10 +50,15 @@ class chamfer_3DFunction(Function):
         xyz1 = xyz1.contiguous()
         xyz2 = xyz2.contiguous()
         device = xyz1.device
-        dist1 = torch.zeros(batchsize, n, device=device)
-        dist2 = torch.zeros(batchsize, m, device=device)
-        idx1 = torch.zeros(batchsize, n, dtype=torch.int32, device=device)
-        idx2 = torch.zeros(batchsize, m, dtype=torch.int32, device=device)
+        # the kernels write every output element, except that an empty other
+        # cloud leaves a direction's outputs untouched (chamfer3D.cu: no
+        # candidate, no store), which the reference's zero-filled buffers
+        # (dist_chamfer_3D.py:40-49) turn into zeros: fill only then
+        alloc = torch.zeros if (n == 0 or m == 0) else torch.empty
+        dist1 = alloc(batchsize, n, device=device)
+        dist2 = alloc(batchsize, m, device=device)
+        idx1 = alloc(batchsize, n, dtype=torch.int32, device=device)
+        idx2 = alloc(batchsize, m, dtype=torch.int32, device=device)
         pcm_hip.chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2)
         ctx.save_for_backward(xyz1, xyz2, idx1, idx2)
         ctx.mark_non_differentiable(idx1, idx2)

@@ -8,6 +8,7 @@ chamfer3D.cu:142-143 -- SURVEY.md appendix A.5).
 """
 from __future__ import annotations
 
+import collections
 import ctypes
 import os
 
@@ -215,33 +216,50 @@ class _StickyWatch:
     """Lagged, sync-free check of a cached fused-loss workspace's sticky error
     words (a loss poll that timed out: NaN means from then on).  After every
     call the two words are copied asynchronously to pinned host memory behind
-    an event; the next call on the workspace reads them once that event has
-    completed and, if either is set, re-zeroes the workspace and raises
-    PcmError, so a timeout is reported instead of silently persisting."""
+    an event, into a small ring of such copies; each call first reads the
+    copies whose events have completed, oldest first, and, if a word is set,
+    re-zeroes the workspace and raises PcmError, so a timeout is reported
+    instead of silently persisting.  No copy is ever dropped: a host that
+    runs ahead of the GPU fills the ring, and a full ring waits for its
+    oldest copy, which bounds the calls between a timeout and its report."""
+
+    depth = 4
 
     def __init__(self, ws, b, n, m):
         L = load_library()
         self.ws = ws
         self.offs = [int(L.pcm_tune_chamfer_err_offset(w, b, n, m)) for w in (0, 1)]
-        self.host = torch.zeros(2, dtype=torch.int32, pin_memory=True)
-        self.event = None
+        self.bufs = [torch.zeros(2, dtype=torch.int32, pin_memory=True) for _ in range(self.depth)]
+        self.ring = collections.deque()  # (buffer index, event), oldest first
+        self.next = 0
 
-    def check(self):
-        if self.event is None or not self.event.query():
-            return
-        bad = bool(self.host.any())
-        self.event = None
-        if bad:
-            self.host.zero_()
+    def _read(self, k):
+        if bool(self.bufs[k].any()):
+            for kk, ev in self.ring:  # pending copies hold the same sticky words
+                ev.synchronize()
+            self.ring.clear()
+            for buf in self.bufs:
+                buf.zero_()
             self.ws.zero_()
             raise PcmError("a fused Chamfer loss kernel timed out waiting on its other workgroups "
                            "(NaN means); its workspace has been reset -- repeat the step")
 
+    def check(self):
+        while self.ring and self.ring[0][1].query():
+            self._read(self.ring.popleft()[0])
+        if len(self.ring) >= self.depth:
+            k, ev = self.ring.popleft()
+            ev.synchronize()
+            self._read(k)
+
     def record(self):
+        k = self.next
+        self.next = (k + 1) % self.depth
         for i, o in enumerate(self.offs):
-            self.host[i:i + 1].copy_(self.ws[o:o + 4].view(torch.int32), non_blocking=True)
-        self.event = torch.cuda.Event()
-        self.event.record()
+            self.bufs[k][i:i + 1].copy_(self.ws[o:o + 4].view(torch.int32), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self.ring.append((k, ev))
 
 
 _watches = {}

@@ -22,16 +22,26 @@ step / max-over-ranks wall time).  EMD (BASELINE config 3: B=16, N=1024,
 50 iterations, eps=0.005) is reported alongside as iterations/s, and the dense
 fp16 Chamfer (BASELINE config 5: B=8, N=M=16384) as point-pairs/s.
 
-Multi-GPU: one process per GPU (torchrun), batches sharded (weak scaling: each
-rank owns its own B=32 clouds).  Every step's loss pair is all-reduced over
-RCCL; the collectives are bucketed per graph of GRAPH_STEPS steps (one
-GRAPH_STEPS x 8-byte all-reduce after each replay, stream-ordered behind it).
+Multi-GPU: one process per GPU, batches sharded (weak scaling: each rank owns
+its own B=32 clouds).  `python bench.py --gpus N` with no WORLD_SIZE in the
+environment relaunches itself as N ranks under torch.distributed.run (before
+any GPU call) and exits with their status; under torchrun WORLD_SIZE must equal
+--gpus.  At N>1 every step all-reduces ITS OWN loss vector over RCCL (the
+north_star contract): the step's kernel and, on a side stream, the 12-byte
+all-reduce of that step's losses are captured together into the hipGraph, so
+step i's collective overlaps step i+1's kernel and the graph holds one
+collective per step.  If the collective cannot be captured (gloo, or a capture
+error) each step replays a one-step graph and all-reduces eagerly.  The
+bucketed form (one all-reduce of GRAPH_STEPS steps' losses per replay) is
+reported beside it.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -75,9 +85,10 @@ BWD_BYTES = 2 * B * N * 12 + 2 * B * N * 4 + 2 * B * N * 4 + 2 * B * N * 12
 FUSED_BYTES = 2 * B * N * 12 + 4 * B * N * 4 + 2 * B * N * 12
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="ranks (one per GPU); default: WORLD_SIZE under torchrun, else 1")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--eager", action="store_true", help="no hipGraph capture")
@@ -87,10 +98,59 @@ def parse():
     p.add_argument("--no-emd", action="store_true", help="skip the EMD leg")
     p.add_argument("--no-dense", action="store_true", help="skip the dense fp16 (config 5) leg")
     p.add_argument("--no-icp", action="store_true", help="skip the ICP (evaluation alignment) leg")
+    p.add_argument("--no-ref-call", action="store_true",
+                   help="skip the leg that times loss/loss.py:34-36's literal call sequence")
     p.add_argument("--dist-backend", default="nccl",
                    help="torch.distributed backend for N>1 (nccl = RCCL; gloo only to rehearse "
                         "several ranks on one GPU)")
-    return p.parse_args()
+    p.add_argument("--force-dist", action="store_true",
+                   help="run the N>1 code path (process group, per-step collective) even with one rank: "
+                        "a single-GPU rehearsal of the RCCL capture")
+    p.add_argument("--eager-allreduce", action="store_true",
+                   help="N>1: all-reduce each step's loss eagerly instead of inside the graph")
+    return p.parse_args(argv)
+
+
+def resolve_launch(gpus, env):
+    """How this invocation runs: ("self", world) -- run the benchmark in this
+    process as one of `world` ranks -- or ("spawn", n) -- relaunch as n ranks
+    under torch.distributed.run.  --gpus N with WORLD_SIZE unset spawns N ranks
+    (N > 1); under a launcher WORLD_SIZE is authoritative and --gpus, when
+    given, must equal it."""
+    ws = env.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        n = 1 if gpus is None else int(gpus)
+        if n < 1:
+            raise ValueError(f"--gpus must be >= 1 (got {n})")
+        return ("spawn", n) if n > 1 else ("self", 1)
+    world = int(ws)
+    if gpus is not None and int(gpus) != world:
+        raise ValueError(f"--gpus {gpus} disagrees with WORLD_SIZE={world} set by the launcher")
+    return ("self", world)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_command(n, argv, port):
+    """The torch.distributed.run command line that runs this file as n ranks
+    on one node (rendezvous on 127.0.0.1; the container hostname may not
+    resolve)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def spawn_ranks(n, argv):
+    """Run n rank processes as children (this process has made no GPU call)
+    and return their launcher's exit status."""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL (see DESIGN.md section 6)
+    return subprocess.call(spawn_command(n, argv, _free_port()), env=env)
 
 
 class ChamferStep:
@@ -116,6 +176,7 @@ class ChamferStep:
         self.loss = torch.zeros(slots, 3, device=dev)
         self.ws = pcm_hip.chamfer_workspace(dev, B, N, M)
         self.world = world
+        self.collective = dist.is_available() and dist.is_initialized()
         self.fused = fused and pcm_hip.loss_grad_supported(self.xyz1, self.xyz2)
 
     def __call__(self, slot=0):
@@ -132,22 +193,22 @@ class ChamferStep:
 
     def reduce_losses(self, rows):
         """sum of per-rank means over RCCL (/world = global mean), stream-ordered"""
-        if self.world > 1:
+        if self.collective:
             dist.all_reduce(self.loss[:rows])
 
 
 def time_region(fn, calls, dev, world):
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for _ in range(calls):
         fn()
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     t = time.perf_counter() - t0
-    if world > 1:
+    if dist.is_initialized():
         tt = torch.tensor([t], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         t = float(tt.item())
@@ -181,6 +242,67 @@ def kernel_avg_us(launch, reps, dev, graph=True):
     e1.record(s)
     e1.synchronize()
     return e0.elapsed_time(e1) * 1000.0 / reps
+
+
+def reference_call_leg(dev, fused_step_us, reps=50):
+    """The call sequence the UNCHANGED caller runs, literally: train.py:163
+    hands loss/loss.py a transposed view of the generator output,
+    loss/loss.py:34-36 builds chamfer_3DDist, takes mean(dist1)+mean(dist2),
+    and train.py:176 runs .backward() through chamfer_3DFunction
+    (dist_chamfer_3D.py), at BASELINE config 2.  Timed eagerly (host launch
+    cost included) and captured whole -- forward, means, autograd backward --
+    into one hipGraph; the ratio is against the fused one-launch step."""
+    sys.path.insert(0, os.path.join(PKG, "metric", "chamfer3D"))
+    import dist_chamfer_3D
+    g = torch.Generator(device="cpu").manual_seed(11)
+    fake = torch.rand(B, 3, N, generator=g).to(dev).requires_grad_(True)  # generator output layout
+    points = torch.rand(B, M, 3, generator=g).to(dev)
+
+    def call():
+        chamLoss = dist_chamfer_3D.chamfer_3DDist()
+        dist1, dist2, idx1, idx2 = chamLoss(fake.transpose(2, 1), points)
+        loss = torch.mean(dist1) + torch.mean(dist2)
+        loss.backward()
+        return loss
+
+    def eager():
+        fake.grad = None
+        call()
+
+    s = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(s)
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            eager()
+    s.wait_stream(side)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        eager()
+    torch.cuda.synchronize(dev)
+    eager_us = (time.perf_counter() - t0) * 1e6 / reps
+
+    fake.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(GRAPH_STEPS):
+            call()  # grads accumulate into the graph's own .grad buffer; the time is what counts
+    graph.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    k = max(1, reps // GRAPH_STEPS)
+    e0.record(s)
+    for _ in range(k):
+        graph.replay()
+    e1.record(s)
+    e1.synchronize()
+    graph_us = e0.elapsed_time(e1) * 1000.0 / (k * GRAPH_STEPS)
+    pairs = 2 * B * N * M
+    return {"sequence": "chamfer_3DDist()(fake.transpose(2,1), points); mean(dist1)+mean(dist2); .backward() "
+                        "(loss/loss.py:34-36, train.py:163,176)",
+            "eager_us_per_step": eager_us, "graph_us_per_step": graph_us,
+            "graph_pairs_per_s": pairs / (graph_us * 1e-6),
+            "graph_vs_fused_step": graph_us / fused_step_us}
 
 
 def generator_predictions(dev, b=EMD_B, n=EMD_N):
@@ -232,12 +354,16 @@ def emd_leg(dev, reps=10, eps=EMD_EPS, iters=EMD_ITERS, clouds=None, label="unif
         pcm_hip.emd_forward(x1, x2, eps, iters, d, a, None, ws)
 
     us = kernel_avg_us(run, reps, dev, graph=False)  # >= 250 us launches: host cost hidden
+    # elements whose master timed out on a helper job in the last timed forward
+    # (the result stays exact, but the call fell back to master-only scans)
+    timeouts = pcm_hip.emd_timeouts(ws, b, n)
     pairs = bids * n
     lane_ops = pairs * EMD_LANE_OPS_PER_PAIR / (us * 1e-6)
     return {"config": f"B={b} N=M={n} iters={iters} eps={eps}", "clouds": label,
             "ms_per_forward": us / 1000.0, "iters_requested": iters, "iters_run": active,
             "iters_per_s": iters / (us * 1e-6), "active_iters_per_s": active / (us * 1e-6),
-            "bids": bids, "cache_misses": misses, "reserve_bids": reserve_bids, "full_scans": full_scans, "bid_pair_evals_per_s": pairs / (us * 1e-6),
+            "bids": bids, "cache_misses": misses, "reserve_bids": reserve_bids, "full_scans": full_scans,
+            "helper_timeouts": timeouts, "bid_pair_evals_per_s": pairs / (us * 1e-6),
             "roofline": {"bound": "valu", "kernel": "emd_seed_kernel + emd_auction_kernel",
                          "achieved": lane_ops / 1e12, "peak": VALU_LANE_OPS_PEAK / 1e12,
                          "unit": "T lane-ops/s", "frac": lane_ops / VALU_LANE_OPS_PEAK,
@@ -377,15 +503,49 @@ def cpu_baseline(target_s=8.0):
                             "sample": f"{reps1} reps of the same workload on 1 thread, {el1:.1f} s"}}
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+def capture_steps(step, per, dev, world, allreduce):
+    """One hipGraph of `per` consecutive steps.  With `allreduce`, every step's
+    own loss row is all-reduced right after its kernel, on a side stream that
+    forks from the step and joins at the end of the graph, so the collective
+    of step i overlaps the kernel of step i+1 (the loss is reported, nothing
+    in the next step reads it)."""
+    g = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream(dev) if allreduce else None
+    if allreduce:
+        # no collective in flight for the process group's watchdog to query
+        # while the capture runs; thread_local: its event queries are legal
+        torch.cuda.synchronize(dev)
+        dist.barrier()
+    with torch.cuda.graph(g, capture_error_mode="thread_local" if allreduce else "global"):
+        cur = torch.cuda.current_stream(dev)
+        for i in range(per):
+            step(i)
+            if allreduce:
+                side.wait_stream(cur)
+                with torch.cuda.stream(side):
+                    dist.all_reduce(step.loss[i])
+        if allreduce:
+            cur.wait_stream(side)
+    return g
+
+
+def main(argv=None):
+    args = parse(argv)
+    # decided before any GPU call: a process that has initialised the GPU
+    # must not start the ranks
+    how, world = resolve_launch(args.gpus, os.environ)
+    if how == "spawn":
+        sys.exit(spawn_ranks(world, sys.argv[1:] if argv is None else argv))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one GPU per rank; a rehearsal with more ranks than GPUs (gloo) shares them
     dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
-    if world > 1:
+    multi = world > 1 or args.force_dist
+    if multi:
+        if "MASTER_ADDR" not in os.environ:  # --force-dist without a launcher: a one-rank group
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()), RANK="0",
+                              WORLD_SIZE="1")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:
@@ -401,34 +561,68 @@ def main():
 
     run_eager(args.warmup)
     torch.cuda.synchronize(dev)
-    run_steps, mode = run_eager, "eager"
+    run_steps, mode, capture_error = run_eager, "eager, one all-reduce per step" if multi else "eager", None
+    g_one = None
     if not args.eager:
-        # The step is launch-bound (two ~10 us kernels), so `per` consecutive
-        # steps are captured into one hipGraph (kernels only) and replayed,
-        # followed by one all-reduce of those steps' losses when N>1; a
-        # one-step graph covers a remainder, so exactly K steps run.
         s = torch.cuda.Stream(dev)
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
             for i in range(3):
                 step(i % per)
         torch.cuda.current_stream(dev).wait_stream(s)
-        g_many, g_one = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_many):
-            for i in range(per):
-                step(i)
-        with torch.cuda.graph(g_one):
-            step(0)
+        g_one = capture_steps(step, 1, dev, world, False)
+        if not multi:
+            # the step is one ~15 us kernel: `per` consecutive steps per hipGraph
+            # replay keep the host launch cost out of the step
+            g_many = capture_steps(step, per, dev, world, False)
 
-        def run_steps(k):
-            for _ in range(k // per):
-                g_many.replay()
-                step.reduce_losses(per)
-            for _ in range(k % per):
-                g_one.replay()
-                step.reduce_losses(1)
+            def run_steps(k):
+                for _ in range(k // per):
+                    g_many.replay()
+                for _ in range(k % per):
+                    g_one.replay()
+            mode = f"hipgraph ({per} steps per graph)"
+        else:
+            g_ar_many = g_ar_one = None
+            if args.dist_backend == "nccl" and not args.eager_allreduce:
+                try:
+                    g_ar_many = capture_steps(step, per, dev, world, True)
+                    g_ar_one = capture_steps(step, 1, dev, world, True)
+                    # the captured collective must produce the all-reduced losses
+                    g_ar_many.replay()
+                    got = step.loss.clone()
+                    for i in range(per):
+                        step(i)
+                    dist.all_reduce(step.loss)
+                    if not torch.allclose(got, step.loss, rtol=1e-6, atol=0.0):
+                        raise RuntimeError(f"captured all-reduce gave {got[0].tolist()}, eager "
+                                           f"{step.loss[0].tolist()}")
+                except Exception as e:  # noqa: BLE001 -- fall back to the eager per-step collective
+                    capture_error = f"{type(e).__name__}: {e}"
+                    g_ar_many = g_ar_one = None
+                    torch.cuda.synchronize(dev)
+                # every rank takes the same form: captured only if it worked everywhere
+                ok = torch.tensor([0 if g_ar_many is None else 1], device=dev, dtype=torch.int32)
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+                if int(ok.item()) == 0:
+                    if capture_error is None:
+                        capture_error = "the captured collective failed on another rank"
+                    g_ar_many = g_ar_one = None
+            if g_ar_many is not None:
+                def run_steps(k):
+                    for _ in range(k // per):
+                        g_ar_many.replay()
+                    for _ in range(k % per):
+                        g_ar_one.replay()
+                mode = (f"hipgraph ({per} steps per graph, each step's loss all-reduced over RCCL inside "
+                        "the graph on a side stream)")
+            else:
+                def run_steps(k):
+                    for _ in range(k):
+                        g_one.replay()
+                        step.reduce_losses(1)
+                mode = "one-step hipgraph replay + eager all-reduce of the step's loss, every step"
         run_steps(args.warmup)
-        mode = f"hipgraph ({per} steps per graph" + (", one loss all-reduce per graph)" if world > 1 else ")")
 
     t = time_region(lambda: run_steps(args.steps), 1, dev, world)
     pairs_per_step = 2 * B * N * M
@@ -448,6 +642,7 @@ def main():
     else:
         dom_kernel, dom_bytes, dom_us = FWD_KERNEL, FWD_BYTES, fwd_us
     dom_tflops = pairs_per_step * FLOP_PER_PAIR / (dom_us * 1e-6) / 1e12
+    traffic = pmc_bytes(dom_kernel)
     out = {
         "metric": "Chamfer3D fwd+bwd point-pairs/sec @ B=32 N=M=1024; EMD iters/sec",
         "value": value,
@@ -461,22 +656,26 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic: torch.rand uniform [0,1) clouds, seeded",
-        "config": {"workload": "Chamfer3D fwd+bwd (+loss sums, +RCCL all-reduce when N>1)",
+        "config": {"workload": "Chamfer3D fwd+bwd (+loss sums, +RCCL all-reduce of every step's loss when N>1)",
                    "batch_per_gpu": B, "n_points": N, "m_points": M,
                    "global_batch": world * B, "parallelism": f"dp{world} (batch-sharded)",
-                   "launch": mode},
+                   "launch": mode, "dist_backend": args.dist_backend if multi else None},
         "roofline": {"bound": "valu", "kernel": dom_kernel,
                      "achieved": dom_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": dom_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": pmc_bytes(dom_kernel),
-                     "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE*2+WRITE_SIZE, "
-                                     "profiles/r03/pmc_summary.json)",
+                     "frac": dom_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
+                     "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE*2+WRITE_SIZE, " +
+                                     os.path.relpath(PMC_SUMMARY, REPO) + ")",
                      "kernel_us": dom_us,
                      "note": "FLOPs = 8 per point pair (algorithmic); VALU-bound, see DESIGN.md"},
-        "roofline_hbm": {"bound": "hbm", "kernel": dom_kernel,
+        "roofline_hbm": {"bound": "hbm", "kernel": dom_kernel, "rank": rank,
                          "achieved": dom_bytes / (dom_us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s",
                          "frac": dom_bytes / (dom_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
-                         "algorithmic_bytes": dom_bytes, "traffic": pmc_bytes(dom_kernel)},
+                         "algorithmic_bytes": dom_bytes, "traffic": traffic,
+                         "counter_achieved": None if traffic is None else traffic / (dom_us * 1e-6) / 1e9,
+                         "counter_frac": None if traffic is None else traffic / (dom_us * 1e-6) / 1e9 / HBM_PEAK_GBS,
+                         "note": "achieved = algorithmic bytes / kernel time; counter_achieved = rocprofv3 HBM-side "
+                                 "bytes per launch / this rank's kernel time"},
         "two_launch": {"fwd_loss_kernel": FWD_KERNEL, "fwd_loss_us": fwd_us,
                        "fwd_tflops": fwd_tflops, "fwd_traffic": pmc_bytes(FWD_KERNEL),
                        "bwd_kernel": BWD_KERNEL, "bwd_us": bwd_us,
@@ -484,19 +683,41 @@ def main():
                        "bwd_algorithmic_bytes": BWD_BYTES, "bwd_traffic": pmc_bytes(BWD_KERNEL),
                        "step_us": fwd_us + bwd_us},
     }
-    if world > 1:
-        # the per-step variant: every step's 8-byte loss all-reduced right
-        # after it (eager: a collective is not captured into the graph)
-        def per_step(k):
+    if capture_error is not None:
+        out["config"]["allreduce_capture_error"] = capture_error
+    if multi:
+        # the other forms of the loss collective, beside the headline
+        per_rank_us = torch.tensor([dom_us], device=dev, dtype=torch.float64)
+        dist.all_reduce(per_rank_us, op=dist.ReduceOp.MAX)
+        out["roofline"]["kernel_us_max_over_ranks"] = float(per_rank_us.item())
+
+        def eager_per_step(k):
             for _ in range(k):
-                step(0)
+                (g_one.replay() if g_one is not None else step(0))
                 dist.all_reduce(step.loss[0])
-        per_step(3)
-        t_ps = time_region(lambda: per_step(args.steps), 1, dev, world)
-        out["per_step_allreduce"] = {
-            "launch": "eager, one RCCL all-reduce of the step's loss per step",
+        eager_per_step(3)
+        t_ps = time_region(lambda: eager_per_step(args.steps), 1, dev, world)
+        out["eager_per_step_allreduce"] = {
+            "launch": f"one-step hipgraph replay + eager {'RCCL' if args.dist_backend == 'nccl' else args.dist_backend} "
+                      "all-reduce of the step's loss, every step",
             "ms_per_step": t_ps * 1000.0 / args.steps,
-            "value": world * args.steps * 2 * B * N * M / t_ps}
+            "value": world * args.steps * pairs_per_step / t_ps}
+        if not args.eager:
+            g_bucket = capture_steps(step, per, dev, world, False)
+
+            def bucketed(k):
+                for _ in range(k // per):
+                    g_bucket.replay()
+                    step.reduce_losses(per)
+            bucketed(per)
+            kb = max(per, args.steps // per * per)
+            t_b = time_region(lambda: bucketed(kb), 1, dev, world)
+            out["bucketed_allreduce"] = {
+                "launch": f"hipgraph of {per} steps, then ONE all-reduce of their {per} loss rows",
+                "ms_per_step": t_b * 1000.0 / kb,
+                "value": world * kb * pairs_per_step / t_b}
+    if not args.no_ref_call:
+        out["reference_call"] = reference_call_leg(dev, ms * 1000.0)
     if not args.no_emd:
         out["emd"] = emd_leg(dev)
         pred, points = generator_predictions(dev)
@@ -511,7 +732,8 @@ def main():
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if multi:
+        dist.barrier()
         dist.destroy_process_group()
 
 

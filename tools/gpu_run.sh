@@ -1,0 +1,44 @@
+# One GPU-box session: `bash tools/gpu_run.sh TAG STEP...` runs the named steps
+# in order, each under its own time limit, output under gpurun_out/TAG/, and
+# stops at the first failing step (no GPU work after a fault or a time-out).
+# Steps:
+#   bench      python bench.py (the driver's default N=1 command)
+#   gloo2      bench.py --gpus 2 --dist-backend gloo (two ranks on one GPU)
+#   forcedist  bench.py --force-dist (one-rank RCCL: the captured per-step collective)
+#   pytest     pytest -m gpu (every GPU test)
+#   pytest:F   pytest -m gpu on tests/F only
+#   smoke      __graft_entry__.smoke()
+#   rocprof    rocprofv3 --kernel-trace --stats of a short bench command
+#   abc        tools/ab_chamfer.py (same-box Chamfer variant A/B)
+#   abe        tools/ab_emd.py   (same-box EMD variant A/B)
+set -o pipefail
+TAG=$1
+shift
+O=gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=/tmp
+for S in "$@"; do
+    echo "[gpu_run] $S $(date +%T)"
+    case "$S" in
+    bench) timeout -k 10 600 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
+    gloo2) timeout -k 10 300 python -u bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-cpu \
+               --no-emd --no-dense --no-icp --no-ref-call > "$O/gloo2.json" 2> "$O/gloo2.err" ;;
+    forcedist) timeout -k 10 300 python -u bench.py --force-dist --steps 50 --warmup 5 --no-cpu --no-emd \
+               --no-dense --no-icp --no-ref-call > "$O/forcedist.json" 2> "$O/forcedist.err" ;;
+    pytest) timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+               > "$O/pytest.txt" 2>&1 ;;
+    pytest:*) timeout -k 10 600 python -u -m pytest "tests/${S#pytest:}" -m gpu -x -q --timeout 120 \
+               --timeout-method thread > "$O/pytest_${S#pytest:}.txt" 2>&1 ;;
+    smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' \
+               > "$O/smoke.txt" 2>&1 ;;
+    rocprof) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" \
+               -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 200 --no-cpu > "$GRAFT_REPO_ROOT/$O/rocprof_bench.json" \
+               2> "$GRAFT_REPO_ROOT/$O/rocprof.err") ;;
+    abc) timeout -k 10 600 python -u tools/ab_chamfer.py > "$O/ab_chamfer.txt" 2>&1 ;;
+    abe) timeout -k 10 600 python -u tools/ab_emd.py > "$O/ab_emd.txt" 2>&1 ;;
+    *) echo "unknown step $S"; exit 2 ;;
+    esac
+    rc=$?
+    echo "[gpu_run] $S rc=$rc $(date +%T)"
+    if [ $rc -ne 0 ]; then exit $rc; fi
+done

@@ -102,6 +102,16 @@ struct FiltLds {
     static constexpr int kBytes = kScan > kTail ? kScan : kTail;
 };
 
+// Raw-tile slot of point p in the filtered forward's LDS copy of a resident
+// target cloud: rotated by its chunk index inside the chunk, so the rescan's
+// lanes -- one query each, random chunks -- spread over the 16 four-bank
+// groups a ds_read_b128 lane group uses, not one.
+template <int C>
+__device__ __forceinline__ int filt_slot(int p) {
+    static_assert((C & (C - 1)) == 0, "chunk is a power of two");
+    return (p & ~(C - 1)) | ((p + p / C) & (C - 1));
+}
+
 // forward outputs: plain stores, or write-through (sc1) when another
 // workgroup of the same launch reads them (fused loss + gradient)
 template <bool kSc1, typename Tv>
@@ -188,7 +198,7 @@ template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1>
 __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const TIn *__restrict__ T, int nq, int nt, int qbase,
                               float *__restrict__ D, int32_t *__restrict__ I, unsigned char *arena,
                               unsigned long long *__restrict__ Gr = nullptr, unsigned long long tag = 0,
-                              const PreDma *pre = nullptr) {
+                              const PreDma *pre = nullptr, pcm_f4 *qown = nullptr) {
     static_assert(C % 4 == 0 && TILE % C == 0, "tile must hold whole chunks of 4-candidate groups");
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
@@ -219,11 +229,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // raw-tile slot of point p: rotated by its chunk index inside the chunk, so
-    // the rescan's lanes -- one query each, random chunks -- spread over the
-    // 16 four-bank groups a ds_read_b128 lane group uses, not one
-    static_assert((C & (C - 1)) == 0, "chunk is a power of two");
-    auto slot = [](int p) { return (p & ~(C - 1)) | ((p + p / C) & (C - 1)); };
+    auto slot = [](int p) { return filt_slot<C>(p); };  // raw-tile slot of point p
 
     // ---- queries (every wave holds the same QW queries: lane + 64 qq)
     float rx[QPT], ry[QPT], rz[QPT];
@@ -270,6 +276,15 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
     const float cn = (float)wave_sum_dpp(qcnt);
     const float c0 = wave_sum_dpp(cx) / cn, c1 = wave_sum_dpp(cy) / cn, c2 = wave_sum_dpp(cz) / cn;
     PCM_STAMP(1);
+    if (qown != nullptr && wave < QPT) {
+        // the workgroup's own query coordinates, for the caller's gradient
+        // phase (wave w writes its register copy w: query slots 64 w + lane)
+        float x = rx[0], y = ry[0], z = rz[0];
+#pragma unroll
+        for (int qq = 1; qq < QPT; ++qq)
+            if (qq == wave) { x = rx[qq]; y = ry[qq]; z = rz[qq]; }
+        qown[wave * 64 + lane] = pcm_f4{x, y, z, 0.f};
+    }
 
     // centred queries, splatted for the packed math
     pcm_f2 px[QPT], py[QPT], pz[QPT];
@@ -329,12 +344,6 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         constexpr int G = C / 4;
         pcm_f4 X4n, Y4n, Z4n, W4n;
         auto fetch = [&](int cc, int g) {
-#ifdef PCM_SCAN_NOLDS  // diagnostic timing build (wrong results): the scan without its LDS reads
-            if (cc != wave || g != 0) {
-                asm volatile("" : "+v"(X4n), "+v"(Y4n), "+v"(Z4n), "+v"(W4n));
-                return;
-            }
-#endif
             const int o = cc * C + 4 * g;
             X4n = *reinterpret_cast<const pcm_f4 *>(&sU[0][o]);
             Y4n = *reinterpret_cast<const pcm_f4 *>(&sU[1][o]);
@@ -355,12 +364,6 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                 // the next group's four reads stay ahead of this group's math
                 // (hipcc otherwise sinks them to their use and waits on each)
                 __builtin_amdgcn_sched_barrier(0);
-#ifdef PCM_SCAN_NOVALU  // diagnostic timing build (wrong results): the scan's reads, one fold each
-#pragma unroll
-                for (int qq = 0; qq < QPT; ++qq)
-                    mn[qq] = __builtin_amdgcn_fmed3f(mn[qq], X4.x + Y4.y, Z4.z + W4.w);
-                continue;
-#endif
                 if constexpr (QPT == 4) {
                     filt_group4(mn, px, py, pz, X4, Y4, Z4, W4);
                     continue;
@@ -1198,7 +1201,12 @@ constexpr int kGradCap = 1024;   // points per cloud the per-element backward ho
 // itself.  The loss poll (pcm_loss::kPollMaxSpins) waits longer: its
 // producers finish within this bound plus their local scans.
 constexpr unsigned kGradWaitSpins = 1u << 16;
-constexpr int kGradSlots = 8;    // inverse-index entries per target kept in LDS (more: ordered rescan)
+constexpr int kGradSlots = 8;    // inverse-index entries per target sorted by the fast network
+// entries per target kept in LDS: 9..16 sources take a wider in-thread sort
+// (random clouds: about 2 targets per launch have more than 8; with 8 slots
+// each cost its workgroup the ballot path, ~1 us, often on the kernel's
+// critical path); more than 16 (a collapsed cloud): the ballot path
+constexpr int kGradSlotsMax = 16;
 // arena of the per-element backward: both clouds (AoS floats), a count per
 // point, kGradSlots 16-bit source ids per point
 constexpr int kGradBytes = 2 * kGradCap * 12 + 2 * kGradCap * 4 + 2 * kGradCap * kGradSlots * 2;
@@ -1220,9 +1228,40 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 // coordinates are gathered together (clamped, unconditional LDS reads), the
 // rare rest one by one.  (Measured and rejected: both clouds' targets of a
 // round interleaved in straight-line code -- 2.6 -> 3.0 us per batch element.)
+// getA(i, x, y, z): the coordinates of source i of the other cloud
+template <typename GetA>
 __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, float sx, float sy, float sz,
-                                            float h, const float *A, const uint16_t *tab, int cnt) {
-    static_assert(kGradSlots == 8, "sorting network for 8 ids");
+                                            float h, GetA getA, const uint16_t *tab, int cnt) {
+    static_assert(kGradSlots == 8 && kGradSlotsMax == 16, "sorting networks for 8 and 16 ids");
+    if (cnt > kGradSlots) {
+        // rare: 9..16 sources.  Odd-even transposition sort of the two rows
+        // (16 rounds), then the sum in ascending source order, one by one
+        int f[16];
+        const uint4 r0 = *reinterpret_cast<const uint4 *>(tab);
+        const uint4 r1 = *reinterpret_cast<const uint4 *>(tab + 8);
+        const unsigned wv[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const int t = (int)((wv[u >> 1] >> (16 * (u & 1))) & 0xffffu);
+            f[u] = u < cnt ? t : 0x7fffffff;
+        }
+#pragma unroll
+        for (int rd = 0; rd < 16; ++rd)
+#pragma unroll
+            for (int i = rd & 1; i + 1 < 16; i += 2) {
+                const int lo = min(f[i], f[i + 1]), hi = max(f[i], f[i + 1]);
+                f[i] = lo;
+                f[i + 1] = hi;
+            }
+        for (int u = 0; u < cnt; ++u) {
+            float tx, ty, tz;
+            getA(f[u], tx, ty, tz);
+            ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(tx, sx)));
+            ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(ty, sy)));
+            az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(tz, sz)));
+        }
+        return;
+    }
     int e[8];
     // the whole 16-byte row in one ds_read_b128; slots past cnt hold stale ids
     const uint4 row = *reinterpret_cast<const uint4 *>(tab);
@@ -1247,12 +1286,7 @@ __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, flo
     };
     float gx[4], gy[4], gz[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const int src = u < cnt ? e[u] : 0;
-        gx[u] = A[3 * src];
-        gy[u] = A[3 * src + 1];
-        gz[u] = A[3 * src + 2];
-    }
+    for (int u = 0; u < 4; ++u) getA(u < cnt ? e[u] : 0, gx[u], gy[u], gz[u]);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const bool on = u < cnt;
@@ -1264,8 +1298,9 @@ __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, flo
         az = on ? nz : az;
     }
     for (int u = 4; u < cnt; ++u) {
-        const int src = e[u];
-        add(A[3 * src], A[3 * src + 1], A[3 * src + 2]);
+        float tx, ty, tz;
+        getA(e[u], tx, ty, tz);
+        add(tx, ty, tz);
     }
 }
 
@@ -1284,7 +1319,13 @@ __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, flo
 // S / A: the range's cloud and the other cloud (LDS); nq / na their sizes;
 // gs / h: 2w of the range's direction (direct term) and of the other one
 // (scatter terms); Iown / Ioth: the argmins (written by other workgroups: sc1).
-template <int NT, int QW, bool kGran = false>
+//
+// kLocalC > 0 (granule form, a resident forward): nothing is copied in.  The
+// other cloud is the forward's own target tile, still in LDS as raw (x, y, z,
+// 0) rows at filt_slot<kLocalC>(i) (TA), and the range's points are the
+// forward's queries (SO[slot]); S and A are then the GLOBAL clouds, read only
+// by the timeout path's local argmin scans.
+template <int NT, int QW, bool kGran = false, int kLocalC = 0>
 __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, const float *S, const float *A,
                                            float gs, float h, const int32_t *__restrict__ Iown,
                                            const int32_t *__restrict__ Ioth, float *__restrict__ G,
@@ -1292,8 +1333,37 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                                            const unsigned long long *__restrict__ Gown = nullptr,
                                            const unsigned long long *__restrict__ Goth = nullptr,
                                            unsigned long long tag = 0, unsigned max_spins = 0,
-                                           unsigned *slow = nullptr) {
+                                           unsigned *slow = nullptr, const pcm_f4 *TA = nullptr,
+                                           const pcm_f4 *SO = nullptr) {
     constexpr int kPerS = (kGradCap + NT - 1) / NT;  // sources per thread
+    static_assert(kLocalC > 0 || 24 * kGradCap + 4 * QW + 2 * QW * kGradSlotsMax + 4 * kGradCap <= kGradBytes,
+                  "both clouds, the counts, the buckets and the overflow list fit the arena");
+    static_assert(kLocalC == 0 || kGran, "local clouds: granule form");
+    // coordinates of point i of the other cloud, and of the range's slot t
+    auto getA = [&](int i, float &x, float &y, float &z) {
+        if constexpr (kLocalC > 0) {
+            const pcm_f4 t4 = TA[filt_slot<kLocalC>(i)];
+            x = t4.x;
+            y = t4.y;
+            z = t4.z;
+        } else {
+            x = A[3 * i];
+            y = A[3 * i + 1];
+            z = A[3 * i + 2];
+        }
+    };
+    auto getS = [&](int t, float &x, float &y, float &z) {
+        if constexpr (kLocalC > 0) {
+            const pcm_f4 s4 = SO[t];
+            x = s4.x;
+            y = s4.y;
+            z = s4.z;
+        } else {
+            x = S[3 * (q0 + t)];
+            y = S[3 * (q0 + t) + 1];
+            z = S[3 * (q0 + t) + 2];
+        }
+    };
     constexpr int NW = NT / 64;
     __shared__ int sOvf[QW];   // overflowed targets (range slot)
     __shared__ int sNOvf;
@@ -1303,7 +1373,7 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
     const int wave = tid >> 6;
     int *cnt = reinterpret_cast<int *>(scratch);                   // [QW] sources per target
     uint16_t *tab = reinterpret_cast<uint16_t *>(cnt + QW);        // [QW][slots]
-    int *lst = reinterpret_cast<int *>(tab + QW * kGradSlots);     // [na] overflow source list
+    int *lst = reinterpret_cast<int *>(tab + QW * kGradSlotsMax);  // [na] overflow source list
 
     const int jt = q0 + tid;  // this thread's target (tid < QW)
     int io = 0;
@@ -1335,18 +1405,20 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                 // never correctness.  max_spins == 0 (tests) recomputes all.
                 const bool all = max_spins == 0u;
                 if (own && (all || (unsigned)(go >> 32) != want)) {
-                    float d;
+                    float d, x, y, z;
                     int k;
-                    pcm_ref_nn_scan(S[3 * jt], S[3 * jt + 1], S[3 * jt + 2], A, na, d, k);
+                    getS(tid, x, y, z);
+                    pcm_ref_nn_scan(x, y, z, A, na, d, k);
                     go = tag | (unsigned)k;
                 }
 #pragma unroll
                 for (int r = 0; r < kPerS; ++r) {
                     const int i = min(tid + r * NT, na - 1);
                     if (all || (unsigned)(gr[r] >> 32) != want) {
-                        float d;
+                        float d, x, y, z;
                         int k;
-                        pcm_ref_nn_scan(A[3 * i], A[3 * i + 1], A[3 * i + 2], S, nq, d, k);
+                        getA(i, x, y, z);
+                        pcm_ref_nn_scan(x, y, z, S, nq, d, k);
                         gr[r] = tag | (unsigned)k;
                     }
                 }
@@ -1380,25 +1452,27 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
         const int t = isr[r] - q0;
         if (i < na && (unsigned)t < (unsigned)QW) {
             const int slot = atomicAdd(&cnt[t], 1);
-            if (slot < kGradSlots) tab[t * kGradSlots + slot] = (uint16_t)i;
+            if (slot < kGradSlotsMax) tab[t * kGradSlotsMax + slot] = (uint16_t)i;
         }
     }
     __syncthreads();
     PCM_STAMP2(4);
     if (tid < QW && jt < nq) {
         const int c = cnt[tid];
-        if (c <= kGradSlots) {
-            const float sx = S[3 * jt], sy = S[3 * jt + 1], sz = S[3 * jt + 2];
-            const float dx = __fmul_rn(gs, __fsub_rn(sx, A[3 * io]));
-            const float dy = __fmul_rn(gs, __fsub_rn(sy, A[3 * io + 1]));
-            const float dz = __fmul_rn(gs, __fsub_rn(sz, A[3 * io + 2]));
+        if (c <= kGradSlotsMax) {
+            float sx, sy, sz, ox, oy, oz;
+            getS(tid, sx, sy, sz);
+            getA(io, ox, oy, oz);
+            const float dx = __fmul_rn(gs, __fsub_rn(sx, ox));
+            const float dy = __fmul_rn(gs, __fsub_rn(sy, oy));
+            const float dz = __fmul_rn(gs, __fsub_rn(sz, oz));
             float ax = 0.f, ay = 0.f, az = 0.f;
             if (dir1) {  // cloud 1: direct term first (chamfer3D.cu:184), then the cloud-2 scatters
                 ax = __fadd_rn(ax, dx);
                 ay = __fadd_rn(ay, dy);
                 az = __fadd_rn(az, dz);
             }
-            scatter_sum(ax, ay, az, sx, sy, sz, h, A, tab + tid * kGradSlots, c);
+            scatter_sum(ax, ay, az, sx, sy, sz, h, getA, tab + tid * kGradSlotsMax, c);
             if (!dir1) {  // cloud 2: cloud-1 scatters first (kernel 1 ran before kernel 2), then direct
                 ax = __fadd_rn(ax, dx);
                 ay = __fadd_rn(ay, dy);
@@ -1438,10 +1512,12 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
         }
         __syncthreads();
         if (tid == t) {  // the target's own thread holds its argmin
-            const float sx = S[3 * j], sy = S[3 * j + 1], sz = S[3 * j + 2];
-            const float dx = __fmul_rn(gs, __fsub_rn(sx, A[3 * io]));
-            const float dy = __fmul_rn(gs, __fsub_rn(sy, A[3 * io + 1]));
-            const float dz = __fmul_rn(gs, __fsub_rn(sz, A[3 * io + 2]));
+            float sx, sy, sz, ox, oy, oz;
+            getS(t, sx, sy, sz);
+            getA(io, ox, oy, oz);
+            const float dx = __fmul_rn(gs, __fsub_rn(sx, ox));
+            const float dy = __fmul_rn(gs, __fsub_rn(sy, oy));
+            const float dz = __fmul_rn(gs, __fsub_rn(sz, oz));
             float ax = 0.f, ay = 0.f, az = 0.f;
             if (dir1) {
                 ax = __fadd_rn(ax, dx);
@@ -1449,10 +1525,11 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                 az = __fadd_rn(az, dz);
             }
             for (int q = 0; q < total; ++q) {
-                const int src = lst[q];
-                ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(A[3 * src], sx)));
-                ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(A[3 * src + 1], sy)));
-                az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(A[3 * src + 2], sz)));
+                float tx, ty, tz;
+                getA(lst[q], tx, ty, tz);
+                ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(tx, sx)));
+                ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(ty, sy)));
+                az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(tz, sz)));
             }
             if (!dir1) {
                 ax = __fadd_rn(ax, dx);
@@ -1588,7 +1665,8 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
     }
 }
 
-template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false>
+template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false,
+          bool kLocal = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -1600,8 +1678,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     constexpr int kFwd = kMfma ? MfmaLds::kBytes : FiltLds<W, QPT, TILE>::kBytes;
     // kEarly: the gradient phase's clouds get an LDS region of their own, so
     // their copy is issued before the scan instead of after the forward
-    constexpr int kArena = kEarly ? kFwd : (kFwd > kGradBytes ? kFwd : kGradBytes);
+    // kLocal: the gradient phase reads the forward's own LDS data (its
+    // target tile and its queries) instead of copying both clouds in
+    constexpr int kArena = (kEarly || kLocal) ? kFwd : (kFwd > kGradBytes ? kFwd : kGradBytes);
     static_assert(!kEarly || kGran, "early cloud copy: granule hand-off form");
+    static_assert(!kLocal || (kGran && !kEarly && !kMfma), "local gradient data: the granule form's forward");
+    constexpr int kTileBytes = 16 * TILE;  // the forward's raw (x, y, z, 0) target rows (resident clouds)
+    static_assert(!kLocal || kTileBytes + 4 * QW + 2 * QW * kGradSlotsMax + 4 * kGradCap <= kFwd,
+                  "the raw tile, the counts, the buckets and the overflow list fit the forward's arena");
     static_assert(QW <= NT, "one target per thread in the gradient phase");
     __shared__ float sRed[16];
     __shared__ int sFlag, sLate;
@@ -1636,11 +1720,12 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         const unsigned long long tag = (unsigned long long)(ws.epoch[0] + 1u) << 32;
         unsigned long long *G1 = ws.ig + (size_t)batch * n, *G2 = ws.ig + (size_t)b * n + (size_t)batch * m;
         const PreDma pre{garena, X1, 12 * n, garena + 12 * kGradCap, X2, 12 * m};
+        __shared__ pcm_f4 sQown[kLocal ? QW : 1];  // kLocal: the range's points (the forward's queries)
         const float my_d = filt_forward<float, W, QPT, C, TILE, false>(
             first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
             first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
             first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, first ? G1 : G2, tag,
-            kEarly ? &pre : nullptr);
+            kEarly ? &pre : nullptr, kLocal ? sQown : nullptr);
         PCM_STAMP2(1);
         const float s = wave_sum(my_d);
         if (lane == 0) sRed[wave] = s;
@@ -1652,21 +1737,34 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         }
         // the batch element's clouds for the gradient phase (the arena is free);
         // they land during the sweep (kEarly: issued before the scan)
-        if constexpr (!kEarly) {
+        if constexpr (!kEarly && !kLocal) {
             pcm_dma_to_lds(arena, X1, 12 * n, wave, W);
             pcm_dma_to_lds(arena + 12 * kGradCap, X2, 12 * m, wave, W);
         }
         PCM_STAMP2(2);
         float *G = first ? grad1 + (size_t)batch * n * 3 : grad2 + (size_t)batch * m * 3;
-        const float *P1 = reinterpret_cast<const float *>(garena);
-        const float *P2 = P1 + 3 * kGradCap;
         const float g1 = __fmul_rn(w1, 2.f), g2 = __fmul_rn(w2, 2.f);
-        const bool ok = first ? range_grad<NT, QW, true>(true, q0, n, m, P1, P2, g1, g2, nullptr, nullptr, G,
-                                                          garena + 24 * kGradCap, G1, G2, tag, max_spins,
-                                                          ws.epoch + kGradSlowWord)
-                              : range_grad<NT, QW, true>(false, q0, m, n, P2, P1, g2, g1, nullptr, nullptr, G,
-                                                          garena + 24 * kGradCap, G2, G1, tag, max_spins,
-                                                          ws.epoch + kGradSlowWord);
+        bool ok;
+        if constexpr (kLocal) {
+            // clouds as the timeout path's global fallback; the other cloud's
+            // rows and the range's points from the forward's LDS
+            const pcm_f4 *TA = reinterpret_cast<const pcm_f4 *>(arena);
+            ok = first ? range_grad<NT, QW, true, C>(true, q0, n, m, X1, X2, g1, g2, nullptr, nullptr, G,
+                                                     arena + kTileBytes, G1, G2, tag, max_spins,
+                                                     ws.epoch + kGradSlowWord, TA, sQown)
+                       : range_grad<NT, QW, true, C>(false, q0, m, n, X2, X1, g2, g1, nullptr, nullptr, G,
+                                                     arena + kTileBytes, G2, G1, tag, max_spins,
+                                                     ws.epoch + kGradSlowWord, TA, sQown);
+        } else {
+            const float *P1 = reinterpret_cast<const float *>(garena);
+            const float *P2 = P1 + 3 * kGradCap;
+            ok = first ? range_grad<NT, QW, true>(true, q0, n, m, P1, P2, g1, g2, nullptr, nullptr, G,
+                                                  garena + 24 * kGradCap, G1, G2, tag, max_spins,
+                                                  ws.epoch + kGradSlowWord)
+                       : range_grad<NT, QW, true>(false, q0, m, n, P2, P1, g2, g1, nullptr, nullptr, G,
+                                                  garena + 24 * kGradCap, G2, G1, tag, max_spins,
+                                                  ws.epoch + kGradSlowWord);
+        }
         if (!ok) {  // a workgroup of this element never published: sticky error, NaN gradients
             if (tid == 0) __hip_atomic_store(ws.epoch + kGradErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int nq = first ? n : m;
@@ -1823,6 +1921,9 @@ const GradVariant kGradVariants[] = {
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, true>, 8, 4},  // 8: 7 + the clouds copied during the scan
     {chamfer_loss_grad_kernel<8, 4, 8, 1024, false, true>, 8, 4},   // 9: 7 with 8-candidate chunks
     {chamfer_loss_grad_kernel<8, 4, 32, 1024, false, true>, 8, 4},  // 10: 7 with 32-candidate chunks
+    // 11: 7 whose gradient phase copies nothing in: the other cloud is the
+    // forward's resident target tile, the range's points its queries
+    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true>, 8, 4},
 };
 constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
 // tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,

@@ -81,22 +81,6 @@ constexpr int kSpinLimit = 1 << 22;  // bounded polls (sticky error word on time
 constexpr int kStagePN = 1024;          // the n of the LDS-state, staged-bidder auction form
 constexpr int kDefaultOffloadMin = 24;  // misses above which an iteration is offloaded
 constexpr int kDefaultTailMax = 16;     // bidders at or below which an iteration runs in tail mode
-// ... and up to kTailFuseMax bidders (fused tail, one wave per bidder) while
-// the last cache-bid iteration's misses were at least half its bids
-#ifndef PCM_TAIL_HI
-#define PCM_TAIL_HI 0  // off: 64 measured 2-4 % slower at the training call (r03m)
-#endif
-constexpr int kTailFuseMax = 64;
-// fused tail iterations (below): bit-exact, but measured no faster at the
-// training call (within the +-3 % call-to-call spread) and 3.5 % slower at
-// config 3, where it never runs (the master kernel's code generation moves;
-// r03o) -- a build option
-#ifndef PCM_TAILFUSE
-#define PCM_TAILFUSE 0
-#endif
-constexpr bool kTailFuse = PCM_TAILFUSE;
-constexpr int kTailHi = PCM_TAIL_HI;
-static_assert(kTailHi <= kTailFuseMax, "one lane per bidder in the fused resolve");
 #ifndef PCM_CHAIN_W
 #define PCM_CHAIN_W 16
 #endif
@@ -954,10 +938,13 @@ __device__ __noinline__ int cache_tie_winner(const centry *cj, bool sc1, const f
 // coll[1] is raised (conservatively, 2e-6) whenever an atomicMax returns a
 // same-iteration value that close to the caller's increment; equal
 // increments raise it too.
+// Bids and increments are kept by the bidder's slot s in the current bidder
+// list, not by point id, so the claim and assign passes (which walk the list)
+// read them in the same LDS round trip as the point id.
 template <bool kG>
-__device__ __forceinline__ void bid_on(const AState<kG> &st, int j, int k, float inc, int *coll) {
-    st.bid[j] = k;
-    st.inc[j] = inc;
+__device__ __forceinline__ void bid_on(const AState<kG> &st, int s, int k, float inc, int *coll) {
+    st.bid[s] = k;
+    st.inc[s] = inc;
     const int old = atomicMax(&st.mx[k], f2key(inc));
     if (old > 0) {
         coll[0] = 1;
@@ -1075,9 +1062,9 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
         }
         if (act && gl == G - 1) {
             if (b2 > tj) {
-                bid_on(st, j, kb, b1 - b2 + eps, coll);
+                bid_on(st, u, kb, b1 - b2 + eps, coll);
             } else {
-                st.miss[atomicAdd(sNm, 1)] = j;
+                st.miss[atomicAdd(sNm, 1)] = u;  // list slots: the point is Ucur[u]
                 if (resN && !(tj > resT[j])) resN[j] = 0;
             }
         }
@@ -1085,14 +1072,15 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
     }
 }
 
-// a bid produced by a full scan, placed by the scanning wave's lane 0
+// a bid produced by a full scan, placed by the scanning wave's lane 0 (s:
+// the bidder's slot in the current list)
 template <bool kG>
-__device__ __forceinline__ void place_bid(const AState<kG> &st, int j, int kb, float inc, int n, int *coll) {
+__device__ __forceinline__ void place_bid(const AState<kG> &st, int s, int kb, float inc, int n, int *coll) {
     if ((unsigned)kb < (unsigned)n) {
-        bid_on(st, j, kb, inc, coll);
+        bid_on(st, s, kb, inc, coll);
     } else {  // all-NaN values: no bid (oracle: best_i = -1)
-        st.bid[j] = -1;
-        st.inc[j] = inc;
+        st.bid[s] = -1;
+        st.inc[s] = inc;
     }
 }
 
@@ -1187,8 +1175,8 @@ __device__ void helper_loop(const KArgs &a, const EmdWs &ws, int batch, int rank
 template <bool kG, bool kStage, bool kStageP, int kN>
 __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *smem) {
     __shared__ int sNu[2], sNm, sColl[2], sChainJ;  // sColl: [0] some object saw 2 bids, [1] a window contention
-    __shared__ float sPb1[kTailFuseMax], sPb2[kTailFuseMax];  // split bids: each part (wave or bidder)
-    __shared__ int sPkb[kTailFuseMax];
+    __shared__ float sPb1[kWaves], sPb2[kWaves];  // split bids: one part per wave
+    __shared__ int sPkb[kWaves];
     const int n = kN > 0 ? kN : a.n, iters = a.iters;
     const float eps = a.eps;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1279,22 +1267,14 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         sTm[i] += tn - sTm[12];                                           \
         sTm[12] = tn;                                                     \
     }
-    // experiment build (PCM_TAIL_TIMERS): slots 4-7 time the fused tail
-    // iteration's scan, first barrier, resolve and second barrier instead
-#ifdef PCM_TAIL_TIMERS
-#define PCM_B2_PHASE(i)
-#define PCM_TAIL_PHASE(i) PCM_EMD_PHASE(i)
-#else
-#define PCM_B2_PHASE(i) PCM_EMD_PHASE(i)
-#define PCM_TAIL_PHASE(i)
-#endif
     // the master's own full scan of point j: cache region A, bid placed
     // (profiling build: wave 0's key scan, proof and exact fallback timed
     // in slots 6, 7, 11 and the exact fallbacks counted)
     // the reserve bid of miss q (kRes): two entries per lane instead of n / 64
     // objects; on success the miss entry is cleared (-1) so B2b skips it
-    auto own_reserve = [&](int q) {
-        const int j = st.miss[q];
+    auto own_reserve = [&](int q, const int *Ucur) {
+        const int u = st.miss[q];
+        const int j = Ucur[u];
         const int rn = __builtin_amdgcn_readfirstlane(sRN[j]);
         if (rn <= 0) return;
 #ifdef PCM_STAMPS
@@ -1321,7 +1301,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         if (lane == 0) {
             if (rb.ok) {
                 CT[j] = rb.T;
-                place_bid(st, j, rb.kb, rb.b1 - rb.b2 + eps, n, sColl);
+                place_bid(st, u, rb.kb, rb.b1 - rb.b2 + eps, n, sColl);
                 st.miss[q] = -1;
                 if (hist) atomicAdd(&a.stats[2 * iters + 13], 1);  // reserve bids
             } else {
@@ -1329,7 +1309,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             }
         }
     };
-    auto own_scan = [&](int j) {
+    auto own_scan = [&](int u, int j) {
         float b1, b2, T;
         int kb;
         centry *cj = C + (size_t)j * kL;
@@ -1352,11 +1332,10 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         kb = tie_fix<kG>(kb, b1, b2, x1, y1, z1, Qc, st.price, n, tr);
         if (lane == 0) {
             CT[j] = T;
-            place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
+            place_bid(st, u, kb, b1 - b2 + eps, n, sColl);
         }
     };
     int active = 0, chain_its = 0, tail_its = 0;
-    bool hi_miss = false;  // the last cache-bid iteration missed on at least half its bids
     for (int it = 0; it < iters; ++it) {
         const bool last = (it == iters - 1);
         // timers: this iteration's start (cycles) and B1 total so far
@@ -1441,116 +1420,12 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
 
         // ---- tail mode (few bidders; the count never grows): one wave per
         // bidder, full scan without a cache, no cache-bid phase
-        const bool tail_hi = !kG && a.tail_max > 0 && nu <= kTailHi && hi_miss;
-        // the LDS-state form runs every tail iteration fused (below): at most
-        // kTailFuseMax bidders, one lane each
-        const int tail_cap = (kG || !kTailFuse) ? a.tail_max : min(a.tail_max, kTailFuseMax);
-        if (it > 0 && (nu <= tail_cap || tail_hi)) {
+        if (it > 0 && nu <= a.tail_max) {
             ++tail_its;
-            hi_miss = true;  // the count never grows from here
             // W waves per bidder (16 / the next power of two >= nu), each
             // scanning every W-th 64-object chunk; the bidder's first wave merges
-#if defined(PCM_TAILW1)
-            const int W = 1;
-#elif defined(PCM_TAIL_FILL)
-            const int W = nu <= 1 ? 4 : (nu <= 2 ? 2 : 1);  // just enough waves for the 4 SIMDs
-#else
             const int W = nu <= 1 ? 16 : (nu <= 2 ? 8 : (nu <= 4 ? 4 : (nu <= 8 ? 2 : 1)));
-#endif
             const int q = wave / W, r = wave - q * W;
-            if (!kG && kTailFuse) {
-                // fused: every part to LDS, one barrier, then wave 0 -- lane
-                // u for bidder u -- merges the parts, places the bids,
-                // resolves them (GetMax + the 1e-6 window claim, as the C
-                // phase) and assigns (as D), and builds the next list: one
-                // barrier more, where the general path takes four.  Within
-                // one wave the LDS executes the instructions in order, so
-                // each step sees the previous one's atomics.  (n <= 2048:
-                // tie_fix is the identity here.)
-                if (nu > kWaves) {  // more bidders than waves: whole bids, one wave each
-                    for (int u = wave; u < nu; u += kWaves) {
-                        const int j = Ucur[u];
-                        float b1, b2;
-                        int kb;
-                        part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, 0, 1, b1, kb, b2);
-                        if (lane == 0) { sPb1[u] = b1; sPkb[u] = kb; sPb2[u] = b2; }
-                    }
-                } else if (q < nu) {
-                    const int j = Ucur[q];
-                    float b1, b2;
-                    int kb;
-                    part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, r, W, b1, kb, b2);
-                    if (lane == 0) { sPb1[wave] = b1; sPkb[wave] = kb; sPb2[wave] = b2; }
-                }
-                if (hist && tid == 0) {
-                    atomicAdd(&a.stats[2 * it], nu);
-                    atomicAdd(&a.stats[2 * it + 1], nu);
-                }
-                PCM_TAIL_PHASE(4);
-                __syncthreads();
-                PCM_TAIL_PHASE(5);
-                if (wave == 0) {
-                    const bool act = lane < nu;
-                    const int j = act ? Ucur[lane] : 0;
-                    // merge of the bidder's parts: best, lowest id at the
-                    // best, the multiset's second (parts never hold NaN)
-                    float b1 = -PCM_INF, b2 = -PCM_INF;
-                    int kb = 0x7fffffff;
-                    if (act) {
-                        for (int p = lane * W; p < lane * W + W; ++p) {
-                            const float p1 = sPb1[p], p2 = sPb2[p];
-                            const int pk = sPkb[p];
-                            if (p1 > b1) {
-                                b2 = fmaxf(b1, p2);
-                                b1 = p1;
-                                kb = pk;
-                            } else if (p1 == b1) {
-                                b2 = b1;
-                                kb = min(kb, pk);
-                            } else {
-                                b2 = fmaxf(b2, p1);
-                            }
-                        }
-                    }
-                    const bool bid = act && (unsigned)kb < (unsigned)n;  // else all-NaN values: no bid
-                    const float inc = b1 - b2 + eps;
-                    const ckey key = ((ckey)(~(unsigned)it) << 32) | (unsigned)j;
-                    int push = act && !bid ? j : -1;
-                    if (bid && last) st.ass[j] = kb;
-                    if (bid && !last) atomicMax(&st.mx[kb], f2key(inc));
-                    if (bid && !last) {
-                        const double bi = (double)inc, mi = (double)key2f(st.mx[kb]);
-                        if (bi - 1e-6 <= mi && mi <= bi + 1e-6) atomicMin(&st.claim[kb], key);
-                    }
-                    if (bid && !last) {
-                        if (st.claim[kb] == key) {
-                            const int old = st.inv[kb];
-                            if (old != -1) { st.ass[old] = -1; push = old; }
-                            st.inv[kb] = j;
-                            st.ass[j] = kb;
-                            st.price[kb] += inc;
-                            st.mx[kb] = f2key(-1e9f);
-                        } else {
-                            push = j;  // outbid
-                        }
-                    }
-                    if (!last) {
-                        const unsigned long long bal = __ballot(push >= 0);
-                        if (push >= 0) Unext[__popcll(bal & ((1ull << lane) - 1ull))] = push;
-                        if (lane == 0) sNu[cur ^ 1] = __popcll(bal);
-                    }
-                }
-                PCM_TAIL_PHASE(6);
-                __syncthreads();
-                PCM_TAIL_PHASE(7);
-                PCM_EMD_PHASE(1);
-                if (timers) {
-                    a.stats[2 * it] = (int)((__builtin_amdgcn_s_memtime() - it_t0) >> 4);
-                    a.stats[2 * it + 1] = 0;
-                    a.stats[2 * iters + 16 + it] = nu;
-                }
-                continue;
-            }
             if (W == 1) {  // whole bids, one wave each (more than 8 bidders)
                 for (int u = wave; u < nu; u += kWaves) {
                     const int j = Ucur[u];
@@ -1558,7 +1433,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     int kb;
                     part_top2(P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, 0, 1, b1, kb, b2);
                     kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, tr);
-                    if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
+                    if (lane == 0) place_bid(st, u, kb, b1 - b2 + eps, n, sColl);
                 }
             } else if (q < nu) {
                 const int j = Ucur[q];
@@ -1578,7 +1453,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 part_merge(sPb1 + wave, sPkb + wave, sPb2 + wave, W, b1, kb, b2);
                 const int j = Ucur[q];
                 kb = tie_fix<kG>(kb, b1, b2, P[3 * j], P[3 * j + 1], P[3 * j + 2], Qc, st.price, n, tr);
-                if (lane == 0) place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
+                if (lane == 0) place_bid(st, q, kb, b1 - b2 + eps, n, sColl);
             }
             __syncthreads();
             PCM_EMD_PHASE(1);
@@ -1589,9 +1464,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 const int j = Ucur[u];
                 const int k = ws.bid0[base + j];
                 if (k >= 0) {
-                    bid_on(st, j, k, ws.inc0[base + j], sColl);
+                    bid_on(st, u, k, ws.inc0[base + j], sColl);
                 } else {
-                    st.miss[atomicAdd(&sNm, 1)] = j;
+                    st.miss[atomicAdd(&sNm, 1)] = u;
                 }
             }
         } else {
@@ -1610,7 +1485,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
 
         // ---- B2: full scans of the misses, caches rebuilt
         const int nm = sNm;
-        hi_miss = 2 * nm >= nu;
         if (hist && tid == 0) {
             atomicAdd(&a.stats[2 * it], nu);
             atomicAdd(&a.stats[2 * it + 1], nm);
@@ -1619,7 +1493,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             if (H > 0 && nm > a.offload_min) {
                 // publish the job: miss list, price snapshot, size
                 ++gen;
-                for (int i = tid; i < nm; i += kEmdThreads) st_sc1(ws.ml + base + i, st.miss[i]);
+                for (int i = tid; i < nm; i += kEmdThreads) st_sc1(ws.ml + base + i, Ucur[st.miss[i]]);
                 for (int k = tid; k < n; k += kEmdThreads) st_sc1(ws.pp + base + k, st.price[k]);
                 if (tid == 0) {
                     st_sc1(bw + kBoardJn, nm);
@@ -1628,19 +1502,19 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 vm_drain();
                 __syncthreads();
                 if (tid == 0) st_sc1(bw + kBoardGen, gen);
-                PCM_B2_PHASE(4);
+                PCM_EMD_PHASE(4);
                 // the master's own groups (owner 0); an item it scans itself
                 // goes to region A and is marked (miss entry negated) so the
                 // collection skips it
                 for (int g0 = 0; g0 * kWaves < nm; g0 += a.H + 1) {
                     const int i = g0 * kWaves + wave;
                     if (i >= nm) break;
-                    const int j = st.miss[i];
-                    own_scan(j);
-                    if (lane == 0) st.miss[i] = -1 - j;
+                    const int u = st.miss[i];
+                    own_scan(u, Ucur[u]);
+                    if (lane == 0) st.miss[i] = -1 - u;
                 }
                 __syncthreads();
-                PCM_B2_PHASE(5);
+                PCM_EMD_PHASE(5);
                 // collect the helpers' items once their done words show this
                 // job.  An item whose done word does not arrive within the
                 // bound (a helper that is not resident, or left) keeps its
@@ -1648,8 +1522,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 // costs time, never correctness
                 bool late = false;
                 for (int i = tid; i < nm; i += kEmdThreads) {
-                    const int j = st.miss[i];
-                    if (j < 0) continue;
+                    const int u = st.miss[i];
+                    if (u < 0) continue;
+                    const int j = Ucur[u];
                     int spin = 0;
                     while (!late && ld_sc1(ws.idone + base + i) != gen) {
                         if (++spin > a.spin_limit) late = true;
@@ -1657,8 +1532,8 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     }
                     if (late) continue;
                     CT[j] = __uint_as_float(kInB);
-                    place_bid(st, j, ld_sc1(ws.rbid + base + i), ld_sc1(ws.rinc + base + i), n, sColl);
-                    st.miss[i] = -1 - j;
+                    place_bid(st, u, ld_sc1(ws.rbid + base + i), ld_sc1(ws.rinc + base + i), n, sColl);
+                    st.miss[i] = -1 - u;
                 }
                 if (__syncthreads_or(late ? 1 : 0)) {
                     // region A rebuilt for the unanswered items, bids placed;
@@ -1666,8 +1541,8 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     H = 0;
                     if (tid == 0) st_sc1(bw + kBoardErr, 1);
                     for (int i = wave; i < nm; i += kWaves) {
-                        const int j = __builtin_amdgcn_readfirstlane(st.miss[i]);
-                        if (j >= 0) own_scan(j);
+                        const int u = __builtin_amdgcn_readfirstlane(st.miss[i]);
+                        if (u >= 0) own_scan(u, Ucur[u]);
                     }
                 }
                 if (hist && tid == 0) {
@@ -1682,18 +1557,22 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     if constexpr (kRes) {
                         // B2a: reserve bids; B2b: full scans of the rest (the
                         // same wave's misses: no barrier between the two)
-                        for (int q = wave; q < nm; q += kWaves) own_reserve(q);
+                        for (int q = wave; q < nm; q += kWaves) own_reserve(q, Ucur);
                         for (int q = wave; q < nm; q += kWaves) {
-                            const int j = __builtin_amdgcn_readfirstlane(st.miss[q]);
-                            if (j >= 0) own_scan(j);
+                            const int u = __builtin_amdgcn_readfirstlane(st.miss[q]);
+                            if (u >= 0) own_scan(u, Ucur[u]);
                         }
                     } else {
-                        for (int q = wave; q < nm; q += kWaves) own_scan(st.miss[q]);
+                        for (int q = wave; q < nm; q += kWaves) {
+                            const int u = st.miss[q];
+                            own_scan(u, Ucur[u]);
+                        }
                     }
                 } else {
                     const int q = wave / W, r = wave - q * W;
                     const bool act = q < nm;
-                    const int j = act ? st.miss[q] : 0;
+                    const int uq = act ? st.miss[q] : 0;
+                    const int j = Ucur[uq];
                     const float x1 = P[3 * j], y1 = P[3 * j + 1], z1 = P[3 * j + 2];
                     LaneTop t;
                     lane_top_init(t);
@@ -1702,15 +1581,15 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     if (act && r != 0) {
                         xA1[tid] = t.a1; xA2[tid] = t.a2; xA3[tid] = t.a3; xQ1[tid] = t.q1; xQ2[tid] = t.q2;
                     }
-                    PCM_B2_PHASE(4);
+                    PCM_EMD_PHASE(4);
                     __syncthreads();
-                    PCM_B2_PHASE(5);
+                    PCM_EMD_PHASE(5);
                     if (act && r == 0) {
                         for (int rr = 1; rr < W; ++rr) {
                             const int o = tid + 64 * rr;
                             lane_top_merge(t, xA1[o], xQ1[o], xA2[o], xQ2[o], xA3[o]);
                         }
-                        PCM_B2_PHASE(6);
+                        PCM_EMD_PHASE(6);
                         float b1, b2, T;
                         int kb;
                         centry *cj = C + (size_t)j * kL;
@@ -1719,9 +1598,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                         kb = tie_fix<kG>(kb, b1, b2, x1, y1, z1, Qc, st.price, n, tr);
                         if (lane == 0) {
                             CT[j] = T;
-                            place_bid(st, j, kb, b1 - b2 + eps, n, sColl);
+                            place_bid(st, uq, kb, b1 - b2 + eps, n, sColl);
                         }
-                        PCM_B2_PHASE(7);
+                        PCM_EMD_PHASE(7);
                     }
                 }
             }
@@ -1741,9 +1620,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         if (!last && !by_max) {
             for (int u = tid; u < nu; u += kEmdThreads) {
                 const int j = Ucur[u];
-                const int k = st.bid[j];
+                const int k = st.bid[u];
                 if (k < 0) continue;
-                const double bi = (double)st.inc[j];
+                const double bi = (double)st.inc[u];
                 const double mi = (double)key2f(st.ld_max(k));
                 if (bi - 1e-6 <= mi && mi <= bi + 1e-6) atomicMin(&st.claim[k], itag | (unsigned)j);
             }
@@ -1759,14 +1638,15 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             const int u = u0 + tid;
             int push = -1;
             if (u < nu) {
+                // point, bid and increment in one LDS round trip (slot-indexed
+                // bids); then the owner, maximum and price of the object in one
                 const int j = Ucur[u];
-                const int k = st.bid[j];
-                // the owner, increment and maximum are read together (one
-                // LDS round trip instead of three dependent ones)
+                const int k = st.bid[u];
+                const float inc = st.inc[u];
                 const int kc = k < 0 ? 0 : k;
                 const int old = st.inv[kc];
-                const float inc = st.inc[j];
                 const int mxk = by_max ? st.ld_max(kc) : 0;
+                const float pk = st.price[kc];
                 if (k < 0) {
                     push = j;  // no bid: stays unassigned
                 } else if (last) {
@@ -1775,7 +1655,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     if (old != -1) { st.ass[old] = -1; push = old; }
                     st.inv[k] = j;
                     st.ass[j] = k;
-                    st.price[k] += inc;
+                    st.price[k] = pk + inc;
                     st.mx[k] = f2key(-1e9f);
                 } else {
                     push = j;  // outbid
@@ -1786,7 +1666,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 const unsigned long long bal = __ballot(push >= 0);
                 int pos = 0;
                 if (lane == 0 && bal) pos = atomicAdd(&sNu[cur ^ 1], __popcll(bal));
-                pos = __shfl(pos, 0, 64);
+                pos = __builtin_amdgcn_readlane(pos, 0);  // lane 0's slot, no LDS round trip
                 if (push >= 0) Unext[pos + __popcll(bal & ((1ull << lane) - 1ull))] = push;
             }
         }
@@ -1799,8 +1679,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
         }
     }
 #undef PCM_EMD_PHASE
-#undef PCM_B2_PHASE
-#undef PCM_TAIL_PHASE
     if (a.H > 0 && tid == 0) st_sc1(bw + kBoardQuit, 1);  // helpers exit
     if (a.stats && tid == 0)  // diagnostics: whole-auction wall time per batch element
         a.stats[3 * iters + 16 + batch] = (int)(__builtin_amdgcn_s_memrealtime() - t_start);

@@ -509,6 +509,35 @@ def test_loss_grad_collapsed_cloud(cuda, oracle):
     np.testing.assert_array_equal(o["g2"].view(np.int32), gr2.view(np.int32))
 
 
+def test_loss_grad_bucket_sizes(cuda, oracle):
+    # targets drawing exactly 1..20 sources of the other cloud: the 8-id
+    # network (<= 8), the 16-id in-thread sort (9..16) and the workgroup's
+    # ballot path (> 16), in both directions, every fused variant
+    import pcm_hip
+    b, n, m = 2, 1024, 1024
+    a, c = _clouds(113, b, n, m)
+    g = torch.Generator().manual_seed(114)
+    for bb in range(b):
+        pos = 0
+        for size in range(1, 21):
+            # `size` cloud-2 points within 1e-3 of cloud-1 point 16*size (and
+            # symmetrically for cloud 1 around cloud-2 point 16*size + 8)
+            for src, dst, t in ((c, a, 16 * size), (a, c, 16 * size + 8)):
+                for r in range(size):
+                    src[bb, 400 + pos + r] = dst[bb, t] + 1e-3 * (torch.rand(3, generator=g) - 0.5)
+            pos += size
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    counts = np.bincount(ref[3][0], minlength=n)  # sources per cloud-1 target, element 0
+    assert counts.max() >= 17 and (counts == 12).any() and (counts == 9).any()
+    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), np.float32(1.0 / (b * n)), np.float32),
+                                       np.full((b, m), np.float32(1.0 / (b * m)), np.float32), ref[2], ref[3])
+    for v in range(pcm_hip.tune_num_chamfer_loss_grad_variants()):
+        o, _, _ = _loss_grad(cuda, a, c, variant=v)
+        _assert_fwd_equal((o["d1"], o["d2"], o["i1"], o["i2"]), ref)
+        np.testing.assert_array_equal(o["g1"].view(np.int32), gr1.view(np.int32))
+        np.testing.assert_array_equal(o["g2"].view(np.int32), gr2.view(np.int32))
+
+
 def test_loss_grad_nonfinite(cuda, oracle):
     import pcm_hip
     a, c = _clouds(112, 2, 600, 500)

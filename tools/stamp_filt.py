@@ -125,6 +125,11 @@ def run_fused(v, b, n, m, dev):
               f"min {min(ghz):.2f}, max {max(ghz):.2f}")
         for r in lo:
             r[0] = r[1]
+    else:
+        # the fused kernel's forward writes no stamp 0 of its own: its
+        # centre phase starts at the workgroup's entry (upper-half stamp 0)
+        for r, u in zip(lo, rows):
+            r[0] = u[0]
     for nm, k0, k1 in [("centre", 0, 1), ("stage", 1, 2), ("scan", 2, 3), ("proof", 3, 4), ("rescan", 4, 5),
                        ("ties", 5, 6)]:
         dur = [(r[k1] - r[k0]) * TICK_US for r in lo]

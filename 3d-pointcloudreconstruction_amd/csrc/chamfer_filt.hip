@@ -29,16 +29,25 @@
 // scan (NaN placement depends on the reference's tile boundaries).
 //
 // Fused loss + gradient (pcm_chamfer_loss_grad): the training step of
-// loss/loss.py:31-37 and its backward (chamfer3D.cu:155-195) in ONE launch.
-// Every workgroup runs its forward share, stores dist/idx write-through (sc1)
-// and its partial distance sum, drains, and adds to its batch element's
-// arrival counter; the LAST arriver of a batch element (told by the value its
-// add returned -- MI355X_MICROARCH.md visibility table, "the workgroup whose
-// add came last") computes that element's gradients with both clouds,
-// argmins and the two inverse-index counting sorts in LDS, in the reference's
-// kernel order (identical bits to pcm_chamfer_backward with constant
-// graddists), publishes the element's loss sums, and the last element's
-// finisher sums those in a fixed order.  No workgroup ever waits on another.
+// loss/loss.py:31-37 and its backward (chamfer3D.cu:155-195) in ONE launch
+// (default: the granule hand-off, kGran).  A workgroup owns 256 queries of one
+// (batch element, direction).  It runs its forward share and publishes every
+// argmin as an 8-byte {call tag, idx} granule (one sc1 store: the data is its
+// own flag, MI355X_MICROARCH.md handoff-1to1) and its partial distance sum as
+// a {tag, sum} granule.  It then computes the gradients of its OWN query
+// range: it sweeps the granules it needs (its range's argmins and the other
+// direction's), waiting -- bounded -- only on its own batch element's
+// workgroups, buckets the sources by target in LDS and sums them in ascending
+// source order, in the reference's kernel order (identical bits to
+// pcm_chamfer_backward fed graddist = w).  The grid's last workgroup sweeps
+// the partial granules and sums them in a fixed order (deterministic means).
+// Granules of earlier calls carry older tags, so the workspace is never
+// re-zeroed; a timed-out wait recomputes the missing argmins locally (time,
+// never correctness).  Variants 11/12 (round 4) read the gradient phase's
+// clouds from the forward's own LDS (its resident target tile and its
+// queries) instead of copying both clouds in; 12 also stages the target tile
+// in two halves so the scan starts before the prologue's loads have all
+// landed.
 #include "pcm_common.h"
 #include "pcm_internal.h"
 #include "chamfer_loss.h"
@@ -194,7 +203,12 @@ __device__ __forceinline__ void filt_group4(float (&mn)[4], const pcm_f2 (&px)[4
 // cloud Q (nq points) against the nt points of T.  Writes D[q], I[q]; returns
 // the distance of query slot threadIdx.x (0 past nq and for threads >= 64 QPT),
 // for the loss partial.  `arena` holds FiltLds<W, QPT, TILE>::kBytes.
-template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1>
+// kSplit: each tile is staged and scanned in parts of NT points (one per
+// staged point of a thread), each behind its own barrier, so the scan of the
+// first part overlaps the rest of the prologue's load burst.  Chunks are
+// visited in the same order (c = wave, wave + W, ...), so results are
+// identical.
+template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1, bool kSplit = false>
 __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const TIn *__restrict__ T, int nq, int nt, int qbase,
                               float *__restrict__ D, int32_t *__restrict__ I, unsigned char *arena,
                               unsigned long long *__restrict__ Gr = nullptr, unsigned long long tag = 0,
@@ -309,82 +323,90 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             load_tile(t0);
             __syncthreads();  // previous tile fully consumed
         }
+        constexpr int kParts = kSplit ? kPer : 1;
+        constexpr int kRpp = kPer / kParts;  // staged points per thread per part
+        static_assert(!kSplit || ((NT % C) == 0 && ((NT / C) % W) == 0), "parts of whole chunks, every wave's share");
 #pragma unroll
-        for (int r = 0; r < kPer; ++r) {
-            const int p = tid + r * NT;
-            if (p < padded) {
-                float ux = 0.f, uy = 0.f, uz = 0.f, w = PCM_INF;  // pad: a = +inf
-                if (p < cnt) {
-                    nonfinite |= !(pcm_finite(tv[r][0]) && pcm_finite(tv[r][1]) && pcm_finite(tv[r][2]));
-                    const float x = tv[r][0] - c0, y = tv[r][1] - c1, z = tv[r][2] - c2;
-                    w = __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
-                    rt2 = __builtin_fmaxf(rt2, w);
-                    ux = -2.f * x;
-                    uy = -2.f * y;
-                    uz = -2.f * z;
+        for (int h = 0; h < kParts; ++h) {
+#pragma unroll
+            for (int r = h * kRpp; r < (h + 1) * kRpp; ++r) {
+                const int p = tid + r * NT;
+                if (p < padded) {
+                    float ux = 0.f, uy = 0.f, uz = 0.f, w = PCM_INF;  // pad: a = +inf
+                    if (p < cnt) {
+                        nonfinite |= !(pcm_finite(tv[r][0]) && pcm_finite(tv[r][1]) && pcm_finite(tv[r][2]));
+                        const float x = tv[r][0] - c0, y = tv[r][1] - c1, z = tv[r][2] - c2;
+                        w = __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
+                        rt2 = __builtin_fmaxf(rt2, w);
+                        ux = -2.f * x;
+                        uy = -2.f * y;
+                        uz = -2.f * z;
+                    }
+                    sU[0][p] = ux;
+                    sU[1][p] = uy;
+                    sU[2][p] = uz;
+                    sU[3][p] = w;
                 }
-                sU[0][p] = ux;
-                sU[1][p] = uy;
-                sU[2][p] = uz;
-                sU[3][p] = w;
             }
-        }
-        __syncthreads();
-        if (t0 == 0) PCM_STAMP(2);
-        if (t0 == 0 && pre) {
-            pcm_dma_to_lds(pre->dst1, pre->src1, pre->bytes1, wave, W);
-            pcm_dma_to_lds(pre->dst2, pre->src2, pre->bytes2, wave, W);
-        }
+            __syncthreads();
+            if (t0 == 0 && h == 0) PCM_STAMP(2);
+            if (t0 == 0 && h == 0 && pre) {
+                pcm_dma_to_lds(pre->dst1, pre->src1, pre->bytes1, wave, W);
+                pcm_dma_to_lds(pre->dst2, pre->src2, pre->bytes2, wave, W);
+            }
 
-        const int nch = padded / C;
-        const int gc0 = t0 / C;
-        // software-pipelined: the next 4-candidate group's four ds_read_b128
-        // are issued before the current group is evaluated (the last group of
-        // a chunk prefetches the wave's next chunk, or re-reads this one)
-        constexpr int G = C / 4;
-        pcm_f4 X4n, Y4n, Z4n, W4n;
-        auto fetch = [&](int cc, int g) {
-            const int o = cc * C + 4 * g;
-            X4n = *reinterpret_cast<const pcm_f4 *>(&sU[0][o]);
-            Y4n = *reinterpret_cast<const pcm_f4 *>(&sU[1][o]);
-            Z4n = *reinterpret_cast<const pcm_f4 *>(&sU[2][o]);
-            W4n = *reinterpret_cast<const pcm_f4 *>(&sU[3][o]);
-        };
-        if (wave < nch) fetch(wave, 0);
-        for (int c = wave; c < nch; c += W) {
-            float mn[QPT];
+            // this part's chunks [c_lo, c_hi) (all of the tile's without kSplit)
+            const int c_lo = kSplit ? h * kRpp * NT / C : 0;
+            const int c_hi = kSplit ? min(padded, (h + 1) * kRpp * NT) / C : padded / C;
+            const int gc0 = t0 / C;
+            // software-pipelined: the next 4-candidate group's four ds_read_b128
+            // are issued before the current group is evaluated (the last group of
+            // a chunk prefetches the wave's next chunk, or re-reads this one)
+            constexpr int G = C / 4;
+            pcm_f4 X4n, Y4n, Z4n, W4n;
+            auto fetch = [&](int cc, int g) {
+                const int o = cc * C + 4 * g;
+                X4n = *reinterpret_cast<const pcm_f4 *>(&sU[0][o]);
+                Y4n = *reinterpret_cast<const pcm_f4 *>(&sU[1][o]);
+                Z4n = *reinterpret_cast<const pcm_f4 *>(&sU[2][o]);
+                W4n = *reinterpret_cast<const pcm_f4 *>(&sU[3][o]);
+            };
+            if (c_lo + wave < c_hi) fetch(c_lo + wave, 0);
+            for (int c = c_lo + wave; c < c_hi; c += W) {
+                float mn[QPT];
 #pragma unroll
-            for (int qq = 0; qq < QPT; ++qq) mn[qq] = PCM_INF;
-            const int cn = (c + W < nch) ? c + W : c;
+                for (int qq = 0; qq < QPT; ++qq) mn[qq] = PCM_INF;
+                const int cn = (c + W < c_hi) ? c + W : c;
 #pragma unroll
-            for (int g = 0; g < G; ++g) {
-                const pcm_f4 X4 = X4n, Y4 = Y4n, Z4 = Z4n, W4 = W4n;
-                if (g + 1 < G) fetch(c, g + 1);
-                else fetch(cn, 0);
-                // the next group's four reads stay ahead of this group's math
-                // (hipcc otherwise sinks them to their use and waits on each)
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (QPT == 4) {
-                    filt_group4(mn, px, py, pz, X4, Y4, Z4, W4);
-                    continue;
+                for (int g = 0; g < G; ++g) {
+                    const pcm_f4 X4 = X4n, Y4 = Y4n, Z4 = Z4n, W4 = W4n;
+                    if (g + 1 < G) fetch(c, g + 1);
+                    else fetch(cn, 0);
+                    // the next group's four reads stay ahead of this group's math
+                    // (hipcc otherwise sinks them to their use and waits on each)
+                    __builtin_amdgcn_sched_barrier(0);
+                    if constexpr (QPT == 4) {
+                        filt_group4(mn, px, py, pz, X4, Y4, Z4, W4);
+                        continue;
+                    }
+#pragma unroll
+                    for (int qq = 0; qq < QPT; ++qq) {
+                        const pcm_f2 a01 = __builtin_elementwise_fma(
+                            px[qq], X4.xy,
+                            __builtin_elementwise_fma(py[qq], Y4.xy, __builtin_elementwise_fma(pz[qq], Z4.xy, W4.xy)));
+                        const pcm_f2 a23 = __builtin_elementwise_fma(
+                            px[qq], X4.zw,
+                            __builtin_elementwise_fma(py[qq], Y4.zw, __builtin_elementwise_fma(pz[qq], Z4.zw, W4.zw)));
+                        mn[qq] = __builtin_fminf(__builtin_fminf(mn[qq], a01.x), a01.y);
+                        mn[qq] = __builtin_fminf(__builtin_fminf(mn[qq], a23.x), a23.y);
+                    }
                 }
 #pragma unroll
                 for (int qq = 0; qq < QPT; ++qq) {
-                    const pcm_f2 a01 = __builtin_elementwise_fma(
-                        px[qq], X4.xy,
-                        __builtin_elementwise_fma(py[qq], Y4.xy, __builtin_elementwise_fma(pz[qq], Z4.xy, W4.xy)));
-                    const pcm_f2 a23 = __builtin_elementwise_fma(
-                        px[qq], X4.zw,
-                        __builtin_elementwise_fma(py[qq], Y4.zw, __builtin_elementwise_fma(pz[qq], Z4.zw, W4.zw)));
-                    mn[qq] = __builtin_fminf(__builtin_fminf(mn[qq], a01.x), a01.y);
-                    mn[qq] = __builtin_fminf(__builtin_fminf(mn[qq], a23.x), a23.y);
+                    // best <= sec always: sec' = median(mn, best, sec)
+                    sec[qq] = __builtin_amdgcn_fmed3f(mn[qq], best[qq], sec[qq]);
+                    if (mn[qq] < best[qq]) { best[qq] = mn[qq]; bchunk[qq] = gc0 + c; }
                 }
-            }
-#pragma unroll
-            for (int qq = 0; qq < QPT; ++qq) {
-                // best <= sec always: sec' = median(mn, best, sec)
-                sec[qq] = __builtin_amdgcn_fmed3f(mn[qq], best[qq], sec[qq]);
-                if (mn[qq] < best[qq]) { best[qq] = mn[qq]; bchunk[qq] = gc0 + c; }
             }
         }
     }
@@ -1666,7 +1688,7 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
 }
 
 template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false,
-          bool kLocal = false>
+          bool kLocal = false, bool kSplit = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -1721,7 +1743,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         unsigned long long *G1 = ws.ig + (size_t)batch * n, *G2 = ws.ig + (size_t)b * n + (size_t)batch * m;
         const PreDma pre{garena, X1, 12 * n, garena + 12 * kGradCap, X2, 12 * m};
         __shared__ pcm_f4 sQown[kLocal ? QW : 1];  // kLocal: the range's points (the forward's queries)
-        const float my_d = filt_forward<float, W, QPT, C, TILE, false>(
+        const float my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
             first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
             first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
             first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, first ? G1 : G2, tag,
@@ -1924,6 +1946,8 @@ const GradVariant kGradVariants[] = {
     // 11: 7 whose gradient phase copies nothing in: the other cloud is the
     // forward's resident target tile, the range's points its queries
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true>, 8, 4},
+    // 12: 11 with the target tile staged and scanned in two halves
+    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, true>, 8, 4},
 };
 constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
 // tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,

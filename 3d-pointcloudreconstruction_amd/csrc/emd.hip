@@ -27,18 +27,22 @@
 //     the same proof applies.  Points whose cache cannot prove the top two get
 //     a full scan: selection on an fp32 approximation with a proven error
 //     bound, exact values of the chosen entries, cache rebuilt (exact scan as
-//     fallback).  A few misses are split over 2 or 4 waves each.
+//     fallback).  At n = 1024 a miss first tries the seed's reserve (every
+//     object within a radius ~8x the cache's) before a full scan.  Few
+//     bidders (<= 16) run as tail mode (each bid an exact scan split over
+//     16 / bidders waves), one bidder as chain mode (bid, resolve, assign of
+//     the evicted owner, two barriers per step).
 //
 //     HELPER workgroups (the rest of the grid, up to 31 per batch element, on
 //     the master's XCD where the dispatcher allows) take the full scans of
 //     heavy iterations: the master publishes the miss list and a price
-//     snapshot, helpers and the master itself claim items with a CAS on a
-//     per-item ticket that the master armed for this job (so a late helper can
-//     never take an item of a newer job), write the rebuilt cache and the bid
-//     write-through (sc1) and raise a per-item done word; the master polls
-//     those words, then places the bids.  The master never waits for an item
-//     nobody claimed -- it claims what is left itself -- so the result and the
-//     termination never depend on how many helpers are resident.
+//     snapshot; items are split statically (groups of 16 consecutive items
+//     round-robin over the master and the helpers, one item per wave), so no
+//     claim atomic sits on anyone's critical path.  A helper writes the
+//     rebuilt cache and the bid write-through (sc1) and raises a per-item done
+//     word; the master polls those words (bounded), then places the bids.  An
+//     item whose done word does not arrive in time is scanned by the master
+//     itself, so the result never depends on how many helpers are resident.
 //     (MI355X_MICROARCH.md, inter-workgroup visibility, row 1: sc1 stores,
 //     s_waitcnt vmcnt(0), sc1 flag; sc1 polls and sc1 loads.)
 //
@@ -93,6 +97,10 @@ constexpr int kDefaultWsplit = 1;       // most waves one miss's scan is split o
 // workspace keeps only the 16-bit object ids (n = 1024): the reserve bid
 // recomputes d from the LDS-staged clouds, the same pinned arithmetic.
 constexpr int kR = 256;
+// LDS-state n = 1024 form: slots of the bidder-list whose cache entries the
+// assign phase copies into LDS (LDS-DMA) for the next iteration's cache bids
+// (the rest of the master's 160 KB: 112 x 512 B)
+constexpr int kPfSlots = 112;
 constexpr float kResGrow = 6.f, kResShrink = 0.85f;
 constexpr int kResTries = 16;           // 6 * 0.85^11 < 1: the radius reaches dK (<= 128 objects inside)
 
@@ -970,11 +978,14 @@ __device__ __forceinline__ void bid_on(const AState<kG> &st, int s, int k, float
 #else
 #define PCM_B1_STAMP(slot, dep)
 #endif
+// PF (LDS-state n = 1024 form, else null): slot u < kPfSlots of the list has
+// its cache entries in PF[u * kL ..] (copied by the previous assign phase)
+// unless the point's cache is in region B
 template <int G, bool kG>
 __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, const centry *C, const float *CT,
                                            const centry *CB, const float *CTB, const AState<kG> &st, int *sNm,
                                            int *coll, const float *resT, int *resN, int n, TieRank tr,
-                                           unsigned long long *tm = nullptr) {
+                                           unsigned long long *tm = nullptr, const centry *PF = nullptr) {
     (void)tm;
     static_assert(G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
     constexpr int E = kL / G;
@@ -994,11 +1005,20 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
         // lane gl evaluates the slot pairs 2 (gl + G e') + {0, 1}: one 16-byte
         // load per pair (any partition of the kL slots over the group works)
         typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        if (PF != nullptr && u < kPfSlots && __float_as_uint(tj) != kInB) {
 #pragma unroll
-        for (int e = 0; e < E / 2; ++e) {
-            const u64x2 w = *reinterpret_cast<const u64x2 *>(C + (size_t)j * kL + 2 * (gl + G * e));
-            ce[2 * e] = w.x;
-            ce[2 * e + 1] = w.y;
+            for (int e = 0; e < E / 2; ++e) {
+                const u64x2 w = *reinterpret_cast<const u64x2 *>(PF + (size_t)u * kL + 2 * (gl + G * e));
+                ce[2 * e] = w.x;
+                ce[2 * e + 1] = w.y;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < E / 2; ++e) {
+                const u64x2 w = *reinterpret_cast<const u64x2 *>(C + (size_t)j * kL + 2 * (gl + G * e));
+                ce[2 * e] = w.x;
+                ce[2 * e + 1] = w.y;
+            }
         }
         PCM_B1_STAMP(6, (unsigned)ce[0] ^ (unsigned)ce[E - 1] ^ __float_as_uint(tj));
         if (__float_as_uint(tj) == kInB) {
@@ -1226,6 +1246,8 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     float *sRT = (float *)(xQ2 + kEmdThreads);  // [n] (kRes)
     int *sRN = (int *)(sRT + n);                // [n] (kRes)
     const bool res_on = eps >= 0.f;             // prices never fall: the reserve bounds hold
+    // kRes: the next iteration's first kPfSlots bidders' cache entries (16-B aligned)
+    centry *sPF = reinterpret_cast<centry *>(((uintptr_t)(sRN + n) + 15) & ~(uintptr_t)15);
 
     if constexpr (kStage) pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kWaves);
     if constexpr (kStageP) pcm_dma_to_lds(sP, Pg, 12 * n, wave, kWaves);
@@ -1476,9 +1498,10 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             const float *rT = kRes ? sRT : nullptr;
             int *rN = kRes ? sRN : nullptr;
             unsigned long long *tm = timers ? sTm : nullptr;
-            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
-            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
-            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
+            const centry *PF = kRes ? sPF : nullptr;
+            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm, PF);
+            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm, PF);
+            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm, PF);
         }
         __syncthreads();
         PCM_EMD_PHASE(0);
@@ -1667,7 +1690,26 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 int pos = 0;
                 if (lane == 0 && bal) pos = atomicAdd(&sNu[cur ^ 1], __popcll(bal));
                 pos = __builtin_amdgcn_readlane(pos, 0);  // lane 0's slot, no LDS round trip
-                if (push >= 0) Unext[pos + __popcll(bal & ((1ull << lane) - 1ull))] = push;
+                const int rank = __popcll(bal & ((1ull << lane) - 1ull));
+                if (push >= 0) Unext[pos + rank] = push;
+                if constexpr (kRes) {
+                    // copy the next bidders' cache entries into LDS slots
+                    // (pos + rank < kPfSlots; a region-B cache is left to the
+                    // bid's own sc1 loads): one LDS-DMA of 32 x 16 B per
+                    // bidder.  The copies land before the iteration's last
+                    // barrier (vm_drain below), under the rest of this phase.
+                    // Caches are final here: B2 rewrites them before claim.
+                    const bool pf = push >= 0 && pos + rank < kPfSlots && __float_as_uint(CT[push]) != kInB;
+                    for (unsigned long long m = __ballot(pf); m; m &= m - 1ull) {
+                        const int L = __builtin_ctzll(m);
+                        const int jL = __builtin_amdgcn_readlane(push, L);
+                        const int sL = pos + __builtin_amdgcn_readlane(rank, L);
+                        if (lane < 32)
+                            __builtin_amdgcn_global_load_lds((const void *)(C + (size_t)jL * kL + 2 * lane),
+                                                             (pcm_lds_void *)(sPF + (size_t)sL * kL), 16, 0, 0);
+                    }
+                    vm_drain();
+                }
             }
         }
         __syncthreads();
@@ -1863,7 +1905,7 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     const bool stage_p = n <= (g_state ? 4096 : kStagePN);  // !g_state: n == kStagePN exactly
     const bool res = !g_state && stage_p;  // n == kStagePN: the reserve form (bounds + counts in LDS)
     const size_t m_lds = (g_state ? 0 : 48 * (size_t)n + 8) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
-                         xchg + (res ? 8 * (size_t)n : 0);
+                         xchg + (res ? 8 * (size_t)n + 16 + (size_t)kPfSlots * kL * sizeof(centry) : 0);
     const size_t h_lds = H > 0 ? (stage ? 12 * (size_t)n : 0) + 4 * (size_t)n : 0;
     size_t lds = m_lds > h_lds ? m_lds : h_lds;
     // one workgroup per CU when helpers run: a master never shares its SIMDs

@@ -43,6 +43,10 @@ int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n,
                              size_t workspace_bytes, int helpers, int offload_min, int diag, int wsplit,
                              int tail_max, int spin_limit, int32_t *stats, void *stream);
 // batch elements of the last EMD forward whose master timed out on a helper job (>= 0)
+// the grid forward (csrc/chamfer_grid.hip) at any size: mode bit 0 = binary16 clouds, bit 1 = exact scan
+int pcm_tune_chamfer_forward_grid(int mode, const void *xyz1, const void *xyz2, int b, int n, int m, float *dist1,
+                                  float *dist2, int32_t *idx1, int32_t *idx2, void *workspace,
+                                  size_t workspace_bytes, void *stream);
 int pcm_tune_emd_timeouts(const void *workspace, size_t workspace_bytes, int b, int n, void *stream);
 #ifdef __cplusplus
 }

@@ -27,6 +27,7 @@ EXPORTED = (
     "pcm_chamfer_workspace_bytes", "pcm_chamfer_forward_loss", "pcm_chamfer_workspace_status",
     "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward", "pcm_emd_workspace_status",
     "pcm_chamfer_forward_f16", "pcm_chamfer_backward_f16",
+    "pcm_chamfer_forward_ws_bytes", "pcm_chamfer_forward_ws", "pcm_chamfer_forward_ws_f16",
     "pcm_chamfer_loss_grad",
     "pcm_icp_workspace_bytes", "pcm_icp", "pcm_icp_workspace_status", "pcm_nearest_neighbor",
     "pcm_best_fit_transform",
@@ -90,6 +91,15 @@ def load_library():
     L.pcm_chamfer_forward_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
     L.pcm_chamfer_backward_f16.restype = ci
     L.pcm_chamfer_backward_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
+    if hasattr(L, "pcm_chamfer_forward_ws"):  # absent from A/B builds of older sources
+        L.pcm_chamfer_forward_ws_bytes.restype = cs
+        L.pcm_chamfer_forward_ws_bytes.argtypes = [ci, ci, ci]
+        L.pcm_chamfer_forward_ws.restype = ci
+        L.pcm_chamfer_forward_ws.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp]
+        L.pcm_chamfer_forward_ws_f16.restype = ci
+        L.pcm_chamfer_forward_ws_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp]
+        L.pcm_tune_chamfer_forward_grid.restype = ci
+        L.pcm_tune_chamfer_forward_grid.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp]
     L.pcm_tune_num_chamfer_f16_variants.restype = ci
     L.pcm_tune_num_chamfer_f16_variants.argtypes = []
     L.pcm_tune_chamfer_forward_f16.restype = ci
@@ -164,17 +174,59 @@ def _cloud_kind(xyz1, xyz2) -> str:
     return "f16" if xyz1.dtype == torch.float16 else "f32"
 
 
+# clouds at least this large (both) take the grid forward (csrc/chamfer_grid.hip
+# kGridMinPoints), which needs pcm_chamfer_forward_ws_bytes of workspace
+GRID_MIN_POINTS = 4096
+
+
+def forward_workspace(dev: torch.device, b: int, n: int, m: int) -> torch.Tensor:
+    """Scratch for the grid forward (no state between calls, no zero-fill),
+    cached per (device, current stream, size) like chamfer_workspace."""
+    need = int(load_library().pcm_chamfer_forward_ws_bytes(b, n, m))
+    key = ("forward", dev, _stream_id(dev), need)
+    ws = _ws_cache.get(key)
+    if ws is None:
+        ws = torch.empty(need, dtype=torch.uint8, device=dev)
+        _ws_cache[key] = ws
+    return ws
+
+
 def chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:
     """pcm_chamfer_forward (float32 clouds) or pcm_chamfer_forward_f16 (float16
-    clouds) on contiguous [B,N,3]/[B,M,3] device tensors; dist is float32."""
+    clouds) on contiguous [B,N,3]/[B,M,3] device tensors; dist is float32.
+    Clouds of >= GRID_MIN_POINTS points go through pcm_chamfer_forward_ws[_f16]
+    (the grid forward; same outputs bit for bit)."""
     dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2)
     b, n, _ = xyz1.shape
     m = xyz2.shape[1]
-    fn = "pcm_chamfer_forward_f16" if _cloud_kind(xyz1, xyz2) == "f16" else "pcm_chamfer_forward"
+    f16 = _cloud_kind(xyz1, xyz2) == "f16"
+    L = load_library()
     with torch.cuda.device(dev):
-        _check(getattr(load_library(), fn)(
+        if n >= GRID_MIN_POINTS and m >= GRID_MIN_POINTS and b > 0:
+            fn = "pcm_chamfer_forward_ws_f16" if f16 else "pcm_chamfer_forward_ws"
+            ws = forward_workspace(dev, b, n, m)
+            _check(getattr(L, fn)(
+                _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
+                _ptr(ws), ws.numel(), _stream(dev)), fn)
+            return
+        fn = "pcm_chamfer_forward_f16" if f16 else "pcm_chamfer_forward"
+        _check(getattr(L, fn)(
             _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
             _stream(dev)), fn)
+
+
+def tune_chamfer_forward_grid(xyz1, xyz2, dist1, dist2, idx1, idx2, exact_scan=False) -> None:
+    """Internal: the grid forward at any size (float32 or float16 clouds);
+    exact_scan evaluates every candidate's key instead of the screened scan."""
+    dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    f16 = _cloud_kind(xyz1, xyz2) == "f16"
+    with torch.cuda.device(dev):
+        ws = forward_workspace(dev, b, n, m)
+        _check(load_library().pcm_tune_chamfer_forward_grid(
+            int(f16) | (2 if exact_scan else 0), _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
+            _ptr(ws), ws.numel(), _stream(dev)), "pcm_tune_chamfer_forward_grid")
 
 
 def tune_chamfer_forward_f16(variant, xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:

@@ -152,8 +152,26 @@ int pcm_chamfer_backward_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, 
                              const int32_t *idx1, const int32_t *idx2,
                              uint16_t *gradxyz1, uint16_t *gradxyz2, void *stream);
 
+/*
+ * Forward with a caller-owned workspace (extension): the same outputs as
+ * pcm_chamfer_forward / pcm_chamfer_forward_f16, bit for bit.  When both
+ * clouds hold >= 4096 points it sorts them into a uniform grid in the
+ * workspace and scans only the cells around each block of queries (with a
+ * proof that no farther point can win, else a full scan), which is what
+ * large clouds (BASELINE config 5, N=M=16384) need; smaller clouds take the
+ * dense kernels and ignore the workspace.  The workspace needs no
+ * initialisation and holds no state between calls.
+ */
+size_t pcm_chamfer_forward_ws_bytes(int b, int n, int m);
+int pcm_chamfer_forward_ws(const float *xyz1, const float *xyz2, int b, int n, int m,
+                           float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                           void *workspace, size_t workspace_bytes, void *stream);
+int pcm_chamfer_forward_ws_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
+                               float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                               void *workspace, size_t workspace_bytes, void *stream);
+
 /* ---------------------------------------------------------------------- */
-/* EMD (auction approximation)                                             */
+/* EMD (auction approximation)                                           */
 /* ---------------------------------------------------------------------- */
 
 /* Device workspace (bytes) pcm_emd_forward needs for a [b, n] problem. */

@@ -132,8 +132,12 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         h = st.cpu()[:2 * args.emd_iters].view(-1, 2)
+        # elements whose master timed out on a helper job and scanned the items
+        # itself (exact, but a silent fall back to master-only scans)
+        timeouts = pcm_hip.emd_timeouts(pcm_hip.emd_workspace(dev, b, n), b, n)
         emd_work.append({"iterations_with_bidders": int((h[:, 0] > 0).sum()), "bids": int(h[:, 0].sum()),
-                         "full_scans": int(h[:, 1].sum()), "emd_fwd_ms": e0.elapsed_time(e1)})
+                         "full_scans": int(h[:, 1].sum()), "emd_fwd_ms": e0.elapsed_time(e1),
+                         "helper_timeouts": timeouts})
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -634,17 +634,19 @@ __device__ inline int block_exclusive_scan(int v, int *wave_tot) {
     return before + x - v;
 }
 
-template <typename TIn>
-__global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
+// NT targets per workgroup (= threads): every workgroup reads the whole
+// other direction's argmins, so large clouds take NT = 1024 (4x less of that)
+template <typename TIn, int NT = kBwdT, int CAP = kBwdCap>
+__global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
     const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2, int b, int n, int m,
     const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
     const int32_t *__restrict__ idx2, TIn *__restrict__ grad1, TIn *__restrict__ grad2,
     int nblk1, int nblk2) {
-    __shared__ int sCnt[kBwdT];
-    __shared__ int sOff[kBwdT + 1];
-    __shared__ int sTmp[kBwdCap];
-    __shared__ int sSrt[kBwdCap];
-    __shared__ int sWave[kBwdT / 64];
+    __shared__ int sCnt[NT];
+    __shared__ int sOff[NT + 1];
+    __shared__ int sTmp[CAP];
+    __shared__ int sSrt[CAP];
+    __shared__ int sWave[NT / 64];
 
     const int tid = threadIdx.x;
     int bid = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
@@ -684,8 +686,8 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
         no = n;
         direct_first = false;
     }
-    const int t0 = blk * kBwdT;
-    const int T = min(kBwdT, ns - t0);
+    const int t0 = blk * NT;
+    const int T = min(NT, ns - t0);
 
     // direct term first: its loads overlap the histogram pass
     const int i = t0 + tid;
@@ -705,24 +707,24 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
     // 1. histogram of the other direction's argmins that land in [t0, t0+T)
     sCnt[tid] = 0;
     __syncthreads();
-    for (int j = tid; j < no; j += kBwdT) {
+    for (int j = tid; j < no; j += NT) {
         const unsigned k = (unsigned)(ido[j] - t0);
         if (k < (unsigned)T) atomicAdd(&sCnt[k], 1);
     }
     __syncthreads();
     // 2. bucket offsets
     const int c = sCnt[tid];
-    const int off = block_exclusive_scan<kBwdT>(c, sWave);
+    const int off = block_exclusive_scan<NT>(c, sWave);
     sOff[tid] = off;
-    if (tid == kBwdT - 1) sOff[kBwdT] = off + c;
+    if (tid == NT - 1) sOff[NT] = off + c;
     sCnt[tid] = 0;
     __syncthreads();
-    const int total = sOff[kBwdT];
-    const bool fits = total <= kBwdCap;  // uniform
+    const int total = sOff[NT];
+    const bool fits = total <= CAP;  // uniform
 
     if (fits && total > 0) {
         // 3. fill buckets (arbitrary order inside a bucket) ...
-        for (int j = tid; j < no; j += kBwdT) {
+        for (int j = tid; j < no; j += NT) {
             const unsigned k = (unsigned)(ido[j] - t0);
             if (k < (unsigned)T) {
                 const int s = atomicAdd(&sCnt[k], 1);
@@ -731,7 +733,7 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_kernel(
         }
         __syncthreads();
         // 4. ... then rank each entry by source index inside its bucket
-        for (int p = tid; p < total; p += kBwdT) {
+        for (int p = tid; p < total; p += NT) {
             const int j = sTmp[p];
             const int k = ido[j] - t0;
             const int lo = sOff[k], hi = sOff[k + 1];
@@ -1232,6 +1234,10 @@ extern "C" int pcm_tune_chamfer_forward_loss(int variant, int loss_mode, const f
 extern "C" int pcm_tune_num_chamfer_variants(void) { return num_fwd_variants(); }
 
 namespace {
+constexpr int kBwdWideT = 1024;    // targets per workgroup for large clouds
+constexpr int kBwdWideCap = 8192;  // their sortable scatter entries (64 KiB of LDS)
+inline bool wide_bwd(int n, int m) { return n >= 4096 && m >= 4096; }
+
 int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
                const float *graddist1, const float *graddist2, const int32_t *idx1,
                const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream) {
@@ -1261,6 +1267,13 @@ int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
         hipLaunchKernelGGL(chamfer_bwd_lds_kernel, dim3((unsigned)b), dim3(kBwdLdsT), lds,
                            (hipStream_t)stream, xyz1, xyz2, n, m, graddist1, graddist2, idx1, idx2,
                            gradxyz1, gradxyz2);
+        return pcm_launch_status();
+    }
+    if (variant == 3 || (variant == 0 && wide_bwd(n, m))) {
+        const int w1 = (n + kBwdWideT - 1) / kBwdWideT, w2 = (m + kBwdWideT - 1) / kBwdWideT;
+        hipLaunchKernelGGL((chamfer_bwd_kernel<float, kBwdWideT, kBwdWideCap>), dim3((unsigned)(b * (w1 + w2))),
+                           dim3(kBwdWideT), 0, (hipStream_t)stream, xyz1, xyz2, b, n, m, graddist1, graddist2,
+                           idx1, idx2, gradxyz1, gradxyz2, w1, w2);
         return pcm_launch_status();
     }
     hipLaunchKernelGGL(chamfer_bwd_kernel<float>, dim3((unsigned)blocks), dim3(kBwdT), 0,
@@ -1350,15 +1363,22 @@ extern "C" int pcm_tune_chamfer_forward_f16(int variant, const uint16_t *xyz1, c
 
 extern "C" int pcm_tune_num_chamfer_f16_variants(void) { return num_fwd16_variants(); }
 
-extern "C" int pcm_chamfer_backward_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
-                                        const float *graddist1, const float *graddist2,
-                                        const int32_t *idx1, const int32_t *idx2, uint16_t *gradxyz1,
-                                        uint16_t *gradxyz2, void *stream) {
+namespace {
+int launch_bwd16(int variant, const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m, const float *graddist1,
+                 const float *graddist2, const int32_t *idx1, const int32_t *idx2, uint16_t *gradxyz1,
+                 uint16_t *gradxyz2, void *stream) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     if (n == 0 || m == 0) return PCM_ERR_INVALID_ARG;
     if (!xyz1 || !xyz2 || !graddist1 || !graddist2 || !idx1 || !idx2 || !gradxyz1 || !gradxyz2)
         return PCM_ERR_INVALID_ARG;
+    if (variant == 3 || (variant == 0 && wide_bwd(n, m))) {
+        const int w1 = (n + kBwdWideT - 1) / kBwdWideT, w2 = (m + kBwdWideT - 1) / kBwdWideT;
+        hipLaunchKernelGGL((chamfer_bwd_kernel<pcm_h, kBwdWideT, kBwdWideCap>), dim3((unsigned)(b * (w1 + w2))),
+                           dim3(kBwdWideT), 0, (hipStream_t)stream, (const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n,
+                           m, graddist1, graddist2, idx1, idx2, (pcm_h *)gradxyz1, (pcm_h *)gradxyz2, w1, w2);
+        return pcm_launch_status();
+    }
     const int nblk1 = (n + kBwdT - 1) / kBwdT;
     const int nblk2 = (m + kBwdT - 1) / kBwdT;
     const long long blocks = (long long)b * (nblk1 + nblk2);
@@ -1367,4 +1387,21 @@ extern "C" int pcm_chamfer_backward_f16(const uint16_t *xyz1, const uint16_t *xy
                        (const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n, m, graddist1, graddist2, idx1, idx2,
                        (pcm_h *)gradxyz1, (pcm_h *)gradxyz2, nblk1, nblk2);
     return pcm_launch_status();
+}
+}  // namespace
+
+extern "C" int pcm_chamfer_backward_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
+                                        const float *graddist1, const float *graddist2,
+                                        const int32_t *idx1, const int32_t *idx2, uint16_t *gradxyz1,
+                                        uint16_t *gradxyz2, void *stream) {
+    return launch_bwd16(0, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2, stream);
+}
+
+// variant 0 = default, 1 = 256-target workgroups, 3 = 1024-target workgroups
+extern "C" int pcm_tune_chamfer_backward_f16(int variant, const uint16_t *xyz1, const uint16_t *xyz2, int b, int n,
+                                             int m, const float *graddist1, const float *graddist2,
+                                             const int32_t *idx1, const int32_t *idx2, uint16_t *gradxyz1,
+                                             uint16_t *gradxyz2, void *stream) {
+    return launch_bwd16(variant, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2,
+                        stream);
 }

@@ -47,6 +47,10 @@ int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n,
 int pcm_tune_chamfer_forward_grid(int mode, const void *xyz1, const void *xyz2, int b, int n, int m, float *dist1,
                                   float *dist2, int32_t *idx1, int32_t *idx2, void *workspace,
                                   size_t workspace_bytes, void *stream);
+// fp16 backward variant: 0 default, 1 256-target workgroups, 3 1024-target workgroups
+int pcm_tune_chamfer_backward_f16(int variant, const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
+                                  const float *graddist1, const float *graddist2, const int32_t *idx1,
+                                  const int32_t *idx2, uint16_t *gradxyz1, uint16_t *gradxyz2, void *stream);
 int pcm_tune_emd_timeouts(const void *workspace, size_t workspace_bytes, int b, int n, void *stream);
 #ifdef __cplusplus
 }

@@ -100,6 +100,8 @@ def load_library():
         L.pcm_chamfer_forward_ws_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp]
         L.pcm_tune_chamfer_forward_grid.restype = ci
         L.pcm_tune_chamfer_forward_grid.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp]
+        L.pcm_tune_chamfer_backward_f16.restype = ci
+        L.pcm_tune_chamfer_backward_f16.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
     L.pcm_tune_num_chamfer_f16_variants.restype = ci
     L.pcm_tune_num_chamfer_f16_variants.argtypes = []
     L.pcm_tune_chamfer_forward_f16.restype = ci
@@ -432,9 +434,23 @@ def tune_chamfer_forward(variant, xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:
             _ptr(idx2), _stream(dev)), "pcm_tune_chamfer_forward")
 
 
+def tune_chamfer_backward_f16(variant, xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1,
+                              gradxyz2) -> None:
+    """Internal: fp16 backward `variant` (0 = automatic, 1 = 256-target workgroups, 3 = 1024-target)."""
+    dev = _require_device(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_tune_chamfer_backward_f16(
+            int(variant), _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(graddist1), _ptr(graddist2),
+            _ptr(idx1), _ptr(idx2), _ptr(gradxyz1), _ptr(gradxyz2), _stream(dev)),
+            "pcm_tune_chamfer_backward_f16")
+
+
 def tune_chamfer_backward(variant, xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1,
                           gradxyz2) -> None:
-    """Internal: backward path `variant` (0 = automatic: staged, 1 = global-memory kernel, 2 = per-batch LDS kernel)."""
+    """Internal: backward path `variant` (0 = automatic: staged, 1 = global-memory kernel, 2 = per-batch LDS
+    kernel, 3 = global-memory kernel with 1024-target workgroups)."""
     dev = _require_device(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
     b, n, _ = xyz1.shape
     m = xyz2.shape[1]

@@ -239,7 +239,8 @@ def test_fused_loss_forward(cuda, oracle):
         np.testing.assert_allclose(means[0].numpy(), r, rtol=2e-6)
 
 
-@pytest.mark.parametrize("b,n,m", [(32, 1024, 1024), (2, 2048, 2048), (3, 700, 1900), (2, 5000, 300)])
+@pytest.mark.parametrize("b,n,m", [(32, 1024, 1024), (2, 2048, 2048), (3, 700, 1900), (2, 5000, 300),
+                                   (2, 5000, 4100)])
 def test_backward_paths_identical(cuda, oracle, b, n, m):
     import pcm_hip
     a, c = _clouds(61, b, n, m)
@@ -253,7 +254,7 @@ def test_backward_paths_identical(cuda, oracle, b, n, m):
     g1 = torch.rand(b, n, generator=gen).to(cuda)
     g2 = torch.rand(b, m, generator=gen).to(cuda)
     outs = []
-    for v in (0, 1, 2):
+    for v in (0, 1, 2, 3):  # 3: 1024-target workgroups (the default from 4096 points)
         gx1 = torch.full((b, n, 3), float("nan"), device=cuda)
         gx2 = torch.full((b, m, 3), float("nan"), device=cuda)
         pcm_hip.tune_chamfer_backward(v, x1, x2, g1, g2, i1, i2, gx1, gx2)
@@ -351,6 +352,34 @@ def test_backward_f16_is_rounded_fp32_gradient(cuda, oracle, b, n, m, seed):
     r1, r2 = oracle.chamfer_backward(ah.float().numpy(), ch.float().numpy(), g1.numpy(), g2.numpy(), i1, i2)
     np.testing.assert_array_equal(gx1.view(np.int16), r1.astype(np.float16).view(np.int16))
     np.testing.assert_array_equal(gx2.view(np.int16), r2.astype(np.float16).view(np.int16))
+
+
+@pytest.mark.parametrize("b,n,m,collapse", [(2, 4100, 5000, False), (2, 4096, 4096, True), (3, 700, 900, False)])
+def test_backward_f16_variants_identical(cuda, oracle, b, n, m, collapse):
+    # 256- and 1024-target workgroups; a collapsed prediction overflows the
+    # LDS sort (every source on one target) and takes the ordered scan
+    import pcm_hip
+    a, c = _clouds(95, b, n, m)
+    if collapse:
+        a[0] = 0.5
+    ah, ch = a.half(), c.half()
+    x1, x2 = ah.to(cuda), ch.to(cuda)
+    d1, d2 = torch.empty(b, n, device=cuda), torch.empty(b, m, device=cuda)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+    pcm_hip.chamfer_forward(x1, x2, d1, d2, i1, i2)
+    gen = torch.Generator().manual_seed(96)
+    g1 = torch.rand(b, n, generator=gen)
+    g2 = torch.rand(b, m, generator=gen)
+    r1, r2 = oracle.chamfer_backward(ah.float().numpy(), ch.float().numpy(), g1.numpy(), g2.numpy(),
+                                     i1.cpu().numpy(), i2.cpu().numpy())
+    for v in (0, 1, 3):
+        gx1 = torch.full((b, n, 3), float("nan"), device=cuda).half()
+        gx2 = torch.full((b, m, 3), float("nan"), device=cuda).half()
+        pcm_hip.tune_chamfer_backward_f16(v, x1, x2, g1.to(cuda), g2.to(cuda), i1, i2, gx1, gx2)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(gx1.cpu().numpy().view(np.int16), r1.astype(np.float16).view(np.int16))
+        np.testing.assert_array_equal(gx2.cpu().numpy().view(np.int16), r2.astype(np.float16).view(np.int16))
 
 
 def test_all_f16_variants_bit_identical(cuda, oracle):

@@ -80,5 +80,32 @@ def main():
               f"identical={same}", flush=True)
 
 
+def backward_f16(dev):
+    """Config-5 fp16 backward: 256- against 1024-target workgroups."""
+    b, n = 8, 16384
+    g = torch.Generator().manual_seed(5)
+    x1 = torch.rand(b, n, 3, generator=g).half().to(dev)
+    x2 = torch.rand(b, n, 3, generator=g).half().to(dev)
+    d1, d2 = torch.empty(b, n, device=dev), torch.empty(b, n, device=dev)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=dev)
+    i2 = torch.empty(b, n, dtype=torch.int32, device=dev)
+    pcm_hip.chamfer_forward(x1, x2, d1, d2, i1, i2)
+    g1 = torch.full((b, n), 1.0 / (b * n), device=dev)
+    g2 = torch.full((b, n), 1.0 / (b * n), device=dev)
+    res, outs = {}, {}
+    for v in (1, 3):
+        gx1, gx2 = torch.empty_like(x1), torch.empty_like(x2)
+
+        def call():
+            pcm_hip.tune_chamfer_backward_f16(v, x1, x2, g1, g2, i1, i2, gx1, gx2)
+        res[v] = timed(call)
+        torch.cuda.synchronize()
+        outs[v] = (gx1.clone(), gx2.clone())
+    same = all(torch.equal(a.view(torch.int16), c.view(torch.int16)) for a, c in zip(outs[1], outs[3]))
+    print(f"config-5 fp16 backward: 256-target workgroups {res[1]:.1f} us, 1024-target {res[3]:.1f} us, "
+          f"identical={same}", flush=True)
+
+
 if __name__ == "__main__":
+    backward_f16(torch.device("cuda:0"))
     main()

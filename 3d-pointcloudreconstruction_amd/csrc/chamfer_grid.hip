@@ -43,6 +43,7 @@ constexpr int kMaxGBits = 5;
 constexpr int kMaxCells = 1 << (3 * kMaxGBits);  // 32768
 constexpr int kFineMin = 12000;  // clouds from this size get G = 32
 constexpr int kBuildT = 1024;
+constexpr int kK = 8;            // points per build thread and chunk (8192 per chunk)
 constexpr int kNnT = 256;        // 4 waves, each an independent block of 64 queries
 constexpr int kWaveCap = 512;    // candidates staged per wave and round (8 KiB of LDS)
 constexpr int kGeo = 8;          // floats per cloud: lo.xyz, h, 1/h, non-finite flag, G, margin
@@ -102,6 +103,8 @@ __device__ __forceinline__ int block_excl_scan(int v, int *sw, int &total) {
 // LDS hand-off inside one wave: the wave's LDS operations complete in order,
 // so waiting for them (and fencing the compiler) is all a wave needs
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// the wave's LDS-DMA copies have landed
+__device__ __forceinline__ void wave_vm_sync() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // (distance bits, index) key of candidate t for query (qx, qy, qz)
 __device__ __forceinline__ unsigned long long nn_key(pcm_f4 t, float qx, float qy, float qz) {
@@ -126,15 +129,34 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     int *st = start + (size_t)c * (kMaxCells + 1);
     const int gb = np >= kFineMin ? 5 : 4, G = 1 << gb, ncells = 1 << (3 * gb);
 
+    // the thread's points, kK per chunk, loads issued together: one latency
+    // per chunk and pass, not per point (passes after the first hit L2)
+    float px[kK], py[kK], pz[kK];
+    auto load = [&](int c0) {
+#pragma unroll
+        for (int k = 0; k < kK; ++k) {
+            const int i = min(c0 + k * kBuildT + tid, np - 1);  // clamped: unconditional loads
+            px[k] = pcm_ld(src + 3 * i);
+            py[k] = pcm_ld(src + 3 * i + 1);
+            pz[k] = pcm_ld(src + 3 * i + 2);
+        }
+    };
+
     float mn[3] = {PCM_INF, PCM_INF, PCM_INF}, mx[3] = {-PCM_INF, -PCM_INF, -PCM_INF};
     float bad = 0.f;
-    for (int i = tid; i < np; i += kBuildT) {
+    for (int c0 = 0; c0 < np; c0 += kK * kBuildT) {
+        load(c0);
 #pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            const float v = pcm_ld(src + 3 * (size_t)i + a);
-            bad = pcm_finite(v) ? bad : 1.f;
-            mn[a] = fminf(mn[a], v);
-            mx[a] = fmaxf(mx[a], v);
+        for (int k = 0; k < kK; ++k) {
+            if (c0 + k * kBuildT + tid < np) {
+                bad = (pcm_finite(px[k]) && pcm_finite(py[k]) && pcm_finite(pz[k])) ? bad : 1.f;
+                mn[0] = fminf(mn[0], px[k]);
+                mx[0] = fmaxf(mx[0], px[k]);
+                mn[1] = fminf(mn[1], py[k]);
+                mx[1] = fmaxf(mx[1], py[k]);
+                mn[2] = fminf(mn[2], pz[k]);
+                mx[2] = fmaxf(mx[2], pz[k]);
+            }
         }
     }
 #pragma unroll
@@ -170,13 +192,17 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
         h = 1.f;
         inv = 1.f;
     }
-
-    // row-major histogram (cell = (iz * G + iy) * G + ix)
-    for (int i = tid; i < np; i += kBuildT) {
-        const TIn *p = src + 3 * (size_t)i;
-        const int cell = (cell_axis(pcm_ld(p + 2), lo[2], inv, G) * G + cell_axis(pcm_ld(p + 1), lo[1], inv, G)) * G +
-                         cell_axis(pcm_ld(p), lo[0], inv, G);
-        atomicAdd(&hist[cell], 1);
+    // row-major cell = (iz * G + iy) * G + ix (recomputed per pass: registers
+    // are the budget here)
+    auto cell = [&](int k) {
+        return (cell_axis(pz[k], lo[2], inv, G) * G + cell_axis(py[k], lo[1], inv, G)) * G +
+               cell_axis(px[k], lo[0], inv, G);
+    };
+    for (int c0 = 0; c0 < np; c0 += kK * kBuildT) {
+        load(c0);
+#pragma unroll
+        for (int k = 0; k < kK; ++k)
+            if (c0 + k * kBuildT + tid < np) atomicAdd(&hist[cell(k)], 1);
     }
     __syncthreads();
     const int per = ncells / kBuildT;  // 4 or 32 consecutive cells per thread
@@ -191,13 +217,20 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     }
     if (tid == 0) st[ncells] = np;
     __syncthreads();
-    for (int i = tid; i < np; i += kBuildT) {
-        const TIn *p = src + 3 * (size_t)i;
-        const float x = pcm_ld(p), y = pcm_ld(p + 1), z = pcm_ld(p + 2);
-        const int cell = (cell_axis(z, lo[2], inv, G) * G + cell_axis(y, lo[1], inv, G)) * G + cell_axis(x, lo[0], inv, G);
-        const int slot = atomicAdd(&hist[cell], 1);
-        tpts[off + slot] = pcm_f4{x, y, z, __int_as_float(i)};
-    }
+    auto scatter = [&](pcm_f4 *dst) {
+        for (int c0 = 0; c0 < np; c0 += kK * kBuildT) {
+            load(c0);
+#pragma unroll
+            for (int k = 0; k < kK; ++k) {
+                const int i = c0 + k * kBuildT + tid;
+                if (i < np) {
+                    const int slot = atomicAdd(&hist[cell(k)], 1);
+                    dst[off + slot] = pcm_f4{px[k], py[k], pz[k], __int_as_float(i)};
+                }
+            }
+        }
+    };
+    scatter(tpts);
     __syncthreads();
     // the same cells in Morton order: hist[cell] now holds the end of the
     // cell's row-major range, so count = hist[cell] - hist[cell - 1]
@@ -228,13 +261,7 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
         }
     }
     __syncthreads();
-    for (int i = tid; i < np; i += kBuildT) {
-        const TIn *p = src + 3 * (size_t)i;
-        const float x = pcm_ld(p), y = pcm_ld(p + 1), z = pcm_ld(p + 2);
-        const int cell = (cell_axis(z, lo[2], inv, G) * G + cell_axis(y, lo[1], inv, G)) * G + cell_axis(x, lo[0], inv, G);
-        const int slot = atomicAdd(&hist[cell], 1);
-        qpts[off + slot] = pcm_f4{x, y, z, __int_as_float(i)};
-    }
+    scatter(qpts);
     if (tid == 0) {
         // margin (cells): the nearest neighbour of a uniform cloud of np points
         // lies beyond r with probability exp(-np 4/3 pi r^3); r = 1.43 np^-1/3
@@ -390,25 +417,31 @@ __global__ __launch_bounds__(kNnT) void grid_nn_kernel(const pcm_f4 *__restrict_
             wave_lds_sync();
             for (int w0 = 0; w0 < tot;) {
                 const int take = min(tot - w0, kWaveCap - filled);
-                for (int p = lane; p < take; p += 64) {
-                    const int v = w0 + p;
-                    int a = 0;  // last row whose prefix is <= v (it holds v)
+                // candidate copies global -> LDS by LDS-DMA (lane l of a batch
+                // lands at slot base + l): every batch's loads in flight at once
+                for (int p0 = 0; p0 < take; p0 += 64) {
+                    const int v = w0 + p0 + lane;
+                    if (v < w0 + take) {
+                        int a = 0;  // last row whose prefix is <= v (it holds v)
 #pragma unroll
-                    for (int step = 32; step > 0; step >>= 1)
-                        a = spre[a + step] <= v ? a + step : a;
-                    cand[filled + p] = T[sst[a] + (v - spre[a])];
+                        for (int step = 32; step > 0; step >>= 1)
+                            a = spre[a + step] <= v ? a + step : a;
+                        __builtin_amdgcn_global_load_lds((const void *)(T + sst[a] + (v - spre[a])),
+                                                         (pcm_lds_void *)(cand + filled + p0), 16, 0, 0);
+                    }
                 }
                 filled += take;
                 w0 += take;
                 if (filled == kWaveCap) {
-                    wave_lds_sync();
+                    wave_vm_sync();
                     scan_cands<kScreen>(cand, kWaveCap, q.x, q.y, q.z, best);
                     wave_lds_sync();
                     filled = 0;
                 }
             }
-            wave_lds_sync();
+            wave_lds_sync();  // spre / sst are rewritten by the next 64 rows
         }
+        wave_vm_sync();
         scan_cands<kScreen>(cand, filled, q.x, q.y, q.z, best);
         wave_lds_sync();
 

@@ -97,10 +97,6 @@ constexpr int kDefaultWsplit = 1;       // most waves one miss's scan is split o
 // workspace keeps only the 16-bit object ids (n = 1024): the reserve bid
 // recomputes d from the LDS-staged clouds, the same pinned arithmetic.
 constexpr int kR = 256;
-// LDS-state n = 1024 form: slots of the bidder-list whose cache entries the
-// assign phase copies into LDS (LDS-DMA) for the next iteration's cache bids
-// (the rest of the master's 160 KB: 112 x 512 B)
-constexpr int kPfSlots = 112;
 constexpr float kResGrow = 6.f, kResShrink = 0.85f;
 constexpr int kResTries = 16;           // 6 * 0.85^11 < 1: the radius reaches dK (<= 128 objects inside)
 
@@ -978,14 +974,11 @@ __device__ __forceinline__ void bid_on(const AState<kG> &st, int s, int k, float
 #else
 #define PCM_B1_STAMP(slot, dep)
 #endif
-// PF (LDS-state n = 1024 form, else null): slot u < kPfSlots of the list has
-// its cache entries in PF[u * kL ..] (copied by the previous assign phase)
-// unless the point's cache is in region B
 template <int G, bool kG>
 __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, const centry *C, const float *CT,
                                            const centry *CB, const float *CTB, const AState<kG> &st, int *sNm,
                                            int *coll, const float *resT, int *resN, int n, TieRank tr,
-                                           unsigned long long *tm = nullptr, const centry *PF = nullptr) {
+                                           unsigned long long *tm = nullptr) {
     (void)tm;
     static_assert(G == 4 || G == 8 || G == 16, "G lanes inside one DPP row");
     constexpr int E = kL / G;
@@ -1005,20 +998,11 @@ __device__ __forceinline__ void cache_bids(int nu, float eps, const int *Ucur, c
         // lane gl evaluates the slot pairs 2 (gl + G e') + {0, 1}: one 16-byte
         // load per pair (any partition of the kL slots over the group works)
         typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-        if (PF != nullptr && u < kPfSlots && __float_as_uint(tj) != kInB) {
 #pragma unroll
-            for (int e = 0; e < E / 2; ++e) {
-                const u64x2 w = *reinterpret_cast<const u64x2 *>(PF + (size_t)u * kL + 2 * (gl + G * e));
-                ce[2 * e] = w.x;
-                ce[2 * e + 1] = w.y;
-            }
-        } else {
-#pragma unroll
-            for (int e = 0; e < E / 2; ++e) {
-                const u64x2 w = *reinterpret_cast<const u64x2 *>(C + (size_t)j * kL + 2 * (gl + G * e));
-                ce[2 * e] = w.x;
-                ce[2 * e + 1] = w.y;
-            }
+        for (int e = 0; e < E / 2; ++e) {
+            const u64x2 w = *reinterpret_cast<const u64x2 *>(C + (size_t)j * kL + 2 * (gl + G * e));
+            ce[2 * e] = w.x;
+            ce[2 * e + 1] = w.y;
         }
         PCM_B1_STAMP(6, (unsigned)ce[0] ^ (unsigned)ce[E - 1] ^ __float_as_uint(tj));
         if (__float_as_uint(tj) == kInB) {
@@ -1246,8 +1230,6 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
     float *sRT = (float *)(xQ2 + kEmdThreads);  // [n] (kRes)
     int *sRN = (int *)(sRT + n);                // [n] (kRes)
     const bool res_on = eps >= 0.f;             // prices never fall: the reserve bounds hold
-    // kRes: the next iteration's first kPfSlots bidders' cache entries (16-B aligned)
-    centry *sPF = reinterpret_cast<centry *>(((uintptr_t)(sRN + n) + 15) & ~(uintptr_t)15);
 
     if constexpr (kStage) pcm_dma_to_lds(sQ, Qg, 12 * n, wave, kWaves);
     if constexpr (kStageP) pcm_dma_to_lds(sP, Pg, 12 * n, wave, kWaves);
@@ -1498,10 +1480,9 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
             const float *rT = kRes ? sRT : nullptr;
             int *rN = kRes ? sRN : nullptr;
             unsigned long long *tm = timers ? sTm : nullptr;
-            const centry *PF = kRes ? sPF : nullptr;
-            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm, PF);
-            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm, PF);
-            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm, PF);
+            if (G == 16) cache_bids<16>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
+            else if (G == 8) cache_bids<8>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
+            else cache_bids<4>(nu, eps, Ucur, C, CT, CB, CTB, st, &sNm, sColl, rT, rN, n, tr, tm);
         }
         __syncthreads();
         PCM_EMD_PHASE(0);
@@ -1690,26 +1671,7 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                 int pos = 0;
                 if (lane == 0 && bal) pos = atomicAdd(&sNu[cur ^ 1], __popcll(bal));
                 pos = __builtin_amdgcn_readlane(pos, 0);  // lane 0's slot, no LDS round trip
-                const int rank = __popcll(bal & ((1ull << lane) - 1ull));
-                if (push >= 0) Unext[pos + rank] = push;
-                if constexpr (kRes) {
-                    // copy the next bidders' cache entries into LDS slots
-                    // (pos + rank < kPfSlots; a region-B cache is left to the
-                    // bid's own sc1 loads): one LDS-DMA of 32 x 16 B per
-                    // bidder.  The copies land before the iteration's last
-                    // barrier (vm_drain below), under the rest of this phase.
-                    // Caches are final here: B2 rewrites them before claim.
-                    const bool pf = push >= 0 && pos + rank < kPfSlots && __float_as_uint(CT[push]) != kInB;
-                    for (unsigned long long m = __ballot(pf); m; m &= m - 1ull) {
-                        const int L = __builtin_ctzll(m);
-                        const int jL = __builtin_amdgcn_readlane(push, L);
-                        const int sL = pos + __builtin_amdgcn_readlane(rank, L);
-                        if (lane < 32)
-                            __builtin_amdgcn_global_load_lds((const void *)(C + (size_t)jL * kL + 2 * lane),
-                                                             (pcm_lds_void *)(sPF + (size_t)sL * kL), 16, 0, 0);
-                    }
-                    vm_drain();
-                }
+                if (push >= 0) Unext[pos + __popcll(bal & ((1ull << lane) - 1ull))] = push;
             }
         }
         __syncthreads();
@@ -1905,7 +1867,7 @@ int launch_emd(const float *xyz1, const float *xyz2, int b, int n, float eps, in
     const bool stage_p = n <= (g_state ? 4096 : kStagePN);  // !g_state: n == kStagePN exactly
     const bool res = !g_state && stage_p;  // n == kStagePN: the reserve form (bounds + counts in LDS)
     const size_t m_lds = (g_state ? 0 : 48 * (size_t)n + 8) + (stage ? 12 * (size_t)n : 0) + (stage_p ? 12 * (size_t)n : 0) +
-                         xchg + (res ? 8 * (size_t)n + 16 + (size_t)kPfSlots * kL * sizeof(centry) : 0);
+                         xchg + (res ? 8 * (size_t)n : 0);
     const size_t h_lds = H > 0 ? (stage ? 12 * (size_t)n : 0) + 4 * (size_t)n : 0;
     size_t lds = m_lds > h_lds ? m_lds : h_lds;
     // one workgroup per CU when helpers run: a master never shares its SIMDs

@@ -2,7 +2,9 @@
 """Fixed kernel sequence for rocprofv3 counter passes (BASELINE configs 2 and 3):
 20x Chamfer fused-loss forward, 20x Chamfer backward, 20x one-launch loss +
 gradient (B=32, N=M=1024), 3x EMD forward (B=16, N=1024, 50 iters, eps 0.005),
-2x the filtered forward at B=8, N=M=16384.  Inputs resident before the loop."""
+then BASELINE config 5 (B=8, N=M=16384): 2x the fp32 forward and 2x the fp16
+forward (both the grid path from 4096 points), 1x the dense fp16 forward,
+2x the fp16 backward.  Inputs resident before the loop."""
 import os
 import sys
 
@@ -49,6 +51,16 @@ def main():
     j2 = torch.empty(b5, n5, dtype=torch.int32, device=dev)
     for _ in range(2):
         pcm_hip.chamfer_forward(y1, y2, f1, f2, j1, j2)
+    h1, h2 = y1.half(), y2.half()
+    for _ in range(2):
+        pcm_hip.chamfer_forward(h1, h2, f1, f2, j1, j2)
+    L, P = pcm_hip.load_library(), pcm_hip._ptr
+    pcm_hip._check(L.pcm_chamfer_forward_f16(P(h1), P(h2), b5, n5, n5, P(f1), P(f2), P(j1), P(j2),
+                                             pcm_hip._stream(dev)), "pcm_chamfer_forward_f16")
+    k1 = torch.full((b5, n5), 1.0 / (b5 * n5), device=dev)
+    hx1, hx2 = torch.empty_like(h1), torch.empty_like(h2)
+    for _ in range(2):
+        pcm_hip.chamfer_backward(h1, h2, k1, k1, j1, j2, hx1, hx2)
     torch.cuda.synchronize()
     print("done")
 

@@ -11,8 +11,8 @@
 //                      and two counting sorts of the points into (x, y, z,
 //                      index) float4 arrays: by row-major cell -- the target
 //                      copy, where one row of cells is one contiguous range --
-//                      and by Morton cell -- the query copy, where 64
-//                      consecutive points are spatially compact.
+//                      and by serpentine brick order -- the query copy, where
+//                      64 consecutive points are spatially compact.
 //   grid_nn_kernel     one wave per 64 consecutive query-order points of one
 //                      direction.  The wave's bounding box in the target grid,
 //                      widened by `margin` cells, is gathered row range by row
@@ -49,9 +49,20 @@ constexpr int kWaveCap = 512;    // candidates staged per wave and round (8 KiB 
 constexpr int kGeo = 8;          // floats per cloud: lo.xyz, h, 1/h, non-finite flag, G, margin
 constexpr int kGridMinPoints = 4096;  // smaller clouds take the dense kernels
 
-// Morton index -> one axis coordinate: bits 0, 3, 6, 9, 12
-__device__ __forceinline__ unsigned compact5(unsigned v) {
-    return (v & 1u) | ((v >> 2) & 2u) | ((v >> 4) & 4u) | ((v >> 6) & 8u) | ((v >> 8) & 16u);
+// Query order: bricks of 4x4x4 cells visited in a serpentine (boustrophedon)
+// order -- consecutive bricks always share a face, so any run of consecutive
+// points spans a few neighbouring bricks (a Z-order curve jumps across the
+// grid at its octant seams) -- and the cells of a brick in row-major order.
+// key -> row-major cell index.
+__device__ __forceinline__ int query_key_cell(int key, int G) {
+    const int nb = G >> 2;
+    const int bi = key >> 6, l = key & 63;
+    const int r = bi / nb, bxp = bi - r * nb;
+    const int bz = r / nb, byp = r - bz * nb;
+    const int bx = (r & 1) ? nb - 1 - bxp : bxp;
+    const int by = (bz & 1) ? nb - 1 - byp : byp;
+    const int x = 4 * bx + (l & 3), y = 4 * by + ((l >> 2) & 3), z = 4 * bz + (l >> 4);
+    return (z * G + y) * G + x;
 }
 // cell coordinate along one axis: floor((v - lo) / h) clamped to the grid
 // (NaN -> 0; only reached for clouds flagged non-finite, whose results come
@@ -232,12 +243,11 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     };
     scatter(tpts);
     __syncthreads();
-    // the same cells in Morton order: hist[cell] now holds the end of the
+    // the same cells in query order: hist[cell] now holds the end of the
     // cell's row-major range, so count = hist[cell] - hist[cell - 1]
     s = 0;
     for (int k = 0; k < per; ++k) {
-        const unsigned mi = (unsigned)(per * tid + k);
-        const int cell = ((int)compact5(mi >> 2) * G + (int)compact5(mi >> 1)) * G + (int)compact5(mi);
+        const int cell = query_key_cell(per * tid + k, G);
         s += hist[cell] - (cell > 0 ? hist[cell - 1] : 0);
     }
     run = block_excl_scan(s, sw, total);  // its barriers order the reads above before the writes below
@@ -245,8 +255,7 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
         if (k < per) {
-            const unsigned mi = (unsigned)(per * tid + k);
-            const int cell = ((int)compact5(mi >> 2) * G + (int)compact5(mi >> 1)) * G + (int)compact5(mi);
+            const int cell = query_key_cell(per * tid + k, G);
             const int cnt = hist[cell] - (cell > 0 ? hist[cell - 1] : 0);
             cur[k] = run;
             run += cnt;
@@ -256,8 +265,7 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
         if (k < per) {
-            const unsigned mi = (unsigned)(per * tid + k);
-            hist[((int)compact5(mi >> 2) * G + (int)compact5(mi >> 1)) * G + (int)compact5(mi)] = cur[k];
+            hist[query_key_cell(per * tid + k, G)] = cur[k];
         }
     }
     __syncthreads();
@@ -338,7 +346,8 @@ __global__ __launch_bounds__(kNnT) void grid_nn_kernel(const pcm_f4 *__restrict_
                                                        const float *__restrict__ geo, const TIn *__restrict__ xyz1,
                                                        const TIn *__restrict__ xyz2, int b, int n, int m, int nb1,
                                                        int nb2, float *__restrict__ dist1, float *__restrict__ dist2,
-                                                       int32_t *__restrict__ idx1, int32_t *__restrict__ idx2) {
+                                                       int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
+                                                       int *__restrict__ stats) {
     constexpr int kW = kNnT / 64;
     __shared__ pcm_f4 cand_all[kW][kWaveCap];
     __shared__ int spre_all[kW][65];
@@ -386,6 +395,7 @@ __global__ __launch_bounds__(kNnT) void grid_nn_kernel(const pcm_f4 *__restrict_
     const float qc[3] = {q.x, q.y, q.z};
     unsigned long long best = ~0ull;
     bool pending = valid;
+    int nround = 0, cand0 = 0, candall = 0;  // diagnostics (stats != nullptr)
     for (int round = 0; __ballot(pending) != 0; ++round) {
         const bool full = round >= 2;  // the last round gathers the whole grid
         const int mg = round == 0 ? margin : 3 * margin;
@@ -411,6 +421,8 @@ __global__ __launch_bounds__(kNnT) void grid_nn_kernel(const pcm_f4 *__restrict_
             }
             const int inc = wave_incl_scan(cnt);
             const int tot = __shfl(inc, 63, 64);
+            candall += tot;
+            cand0 += round == 0 ? tot : 0;
             spre[lane] = inc - cnt;
             sst[lane] = cs;
             if (lane == 63) spre[64] = inc;
@@ -460,6 +472,13 @@ __global__ __launch_bounds__(kNnT) void grid_nn_kernel(const pcm_f4 *__restrict_
         const float bd = __uint_as_float((unsigned)(best >> 32));
         const bool ok = gap > 0.f && bd < gap * gap * (1.f - 0x1p-18f);
         pending = pending && !ok && !full;
+        nround = round + 1;
+    }
+    if (stats != nullptr && lane == 0) {
+        stats[4 * blk_all + 0] = nround;
+        stats[4 * blk_all + 1] = cand0;
+        stats[4 * blk_all + 2] = candall;
+        stats[4 * blk_all + 3] = e * 2 + (dir2 ? 1 : 0);
     }
     if (valid) {
         const int oid = __float_as_int(q.w);
@@ -488,7 +507,8 @@ inline bool bad_dims(int b, int n, int m) { return b < 0 || n < 0 || m < 0; }
 
 template <typename TIn>
 int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *dist1, float *dist2, int32_t *idx1,
-                int32_t *idx2, void *workspace, size_t workspace_bytes, void *stream, bool screen = true) {
+                int32_t *idx2, void *workspace, size_t workspace_bytes, void *stream, bool screen = true,
+                int *stats = nullptr, bool build = true, bool nn = true) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2)))
@@ -507,11 +527,13 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
     int *start = (int *)(base + L.start);
     float *geo = (float *)(base + L.geo);
     hipStream_t st = (hipStream_t)stream;
-    hipLaunchKernelGGL(grid_build_kernel<TIn>, dim3(2 * b), dim3(kBuildT), 0, st, xyz1, xyz2, b, n, m, tpts, qpts,
-                       start, geo);
-    auto nn = screen ? grid_nn_kernel<TIn, true> : grid_nn_kernel<TIn, false>;
-    hipLaunchKernelGGL(nn, dim3((unsigned)blocks), dim3(kNnT), 0, st, tpts, qpts, start, geo, xyz1, xyz2, b, n, m,
-                       nb1, nb2, dist1, dist2, idx1, idx2);
+    if (build)
+        hipLaunchKernelGGL(grid_build_kernel<TIn>, dim3(2 * b), dim3(kBuildT), 0, st, xyz1, xyz2, b, n, m, tpts,
+                           qpts, start, geo);
+    auto nnk = screen ? grid_nn_kernel<TIn, true> : grid_nn_kernel<TIn, false>;
+    if (nn)
+        hipLaunchKernelGGL(nnk, dim3((unsigned)blocks), dim3(kNnT), 0, st, tpts, qpts, start, geo, xyz1, xyz2, b, n,
+                           m, nb1, nb2, dist1, dist2, idx1, idx2, stats);
     return pcm_launch_status();
 }
 
@@ -540,14 +562,18 @@ extern "C" int pcm_chamfer_forward_ws_f16(const uint16_t *xyz1, const uint16_t *
 }
 
 // the grid path at any size (tests and A/B): mode bit 0 = binary16 clouds,
-// bit 1 = exact scan of every candidate instead of the screened scan
+// bit 1 = exact scan of every candidate instead of the screened scan, bit 2 =
+// the build kernel only, bit 3 = the search kernel only (on the workspace of a
+// previous call with the same clouds); stats (nullable): per wave of the
+// search, {rounds, candidates of round 0, candidates of all rounds,
+// 2 * element + direction}
 extern "C" int pcm_tune_chamfer_forward_grid(int mode, const void *xyz1, const void *xyz2, int b, int n, int m,
                                              float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
-                                             void *workspace, size_t workspace_bytes, void *stream) {
-    const bool screen = !(mode & 2);
+                                             void *workspace, size_t workspace_bytes, void *stream, int *stats) {
+    const bool screen = !(mode & 2), build = !(mode & 8), nn = !(mode & 4);
     if (mode & 1)
         return launch_grid((const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace,
-                           workspace_bytes, stream, screen);
+                           workspace_bytes, stream, screen, stats, build, nn);
     return launch_grid((const float *)xyz1, (const float *)xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace,
-                       workspace_bytes, stream, screen);
+                       workspace_bytes, stream, screen, stats, build, nn);
 }

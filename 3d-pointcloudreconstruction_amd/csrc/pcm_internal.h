@@ -43,10 +43,11 @@ int pcm_tune_emd_forward_cfg(const float *xyz1, const float *xyz2, int b, int n,
                              size_t workspace_bytes, int helpers, int offload_min, int diag, int wsplit,
                              int tail_max, int spin_limit, int32_t *stats, void *stream);
 // batch elements of the last EMD forward whose master timed out on a helper job (>= 0)
-// the grid forward (csrc/chamfer_grid.hip) at any size: mode bit 0 = binary16 clouds, bit 1 = exact scan
+// the grid forward (csrc/chamfer_grid.hip) at any size: mode bit 0 = binary16 clouds, bit 1 = exact scan,
+// bit 2 = build kernel only, bit 3 = search kernel only; stats (nullable): 4 ints per search wave
 int pcm_tune_chamfer_forward_grid(int mode, const void *xyz1, const void *xyz2, int b, int n, int m, float *dist1,
                                   float *dist2, int32_t *idx1, int32_t *idx2, void *workspace,
-                                  size_t workspace_bytes, void *stream);
+                                  size_t workspace_bytes, void *stream, int *stats);
 // fp16 backward variant: 0 default, 1 256-target workgroups, 3 1024-target workgroups
 int pcm_tune_chamfer_backward_f16(int variant, const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
                                   const float *graddist1, const float *graddist2, const int32_t *idx1,

@@ -99,7 +99,7 @@ def load_library():
         L.pcm_chamfer_forward_ws_f16.restype = ci
         L.pcm_chamfer_forward_ws_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp]
         L.pcm_tune_chamfer_forward_grid.restype = ci
-        L.pcm_tune_chamfer_forward_grid.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp]
+        L.pcm_tune_chamfer_forward_grid.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp, vp]
         L.pcm_tune_chamfer_backward_f16.restype = ci
         L.pcm_tune_chamfer_backward_f16.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
     L.pcm_tune_num_chamfer_f16_variants.restype = ci
@@ -217,18 +217,23 @@ def chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:
             _stream(dev)), fn)
 
 
-def tune_chamfer_forward_grid(xyz1, xyz2, dist1, dist2, idx1, idx2, exact_scan=False) -> None:
+def tune_chamfer_forward_grid(xyz1, xyz2, dist1, dist2, idx1, idx2, exact_scan=False, only=None,
+                              stats=None, workspace=None) -> None:
     """Internal: the grid forward at any size (float32 or float16 clouds);
-    exact_scan evaluates every candidate's key instead of the screened scan."""
+    exact_scan evaluates every candidate's key instead of the screened scan;
+    only = "build" / "search" runs one of its two kernels (search reuses the
+    workspace of a previous call with the same clouds); stats: int32 device
+    tensor of 4 ints per search wave (csrc/chamfer_grid.hip)."""
     dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2)
     b, n, _ = xyz1.shape
     m = xyz2.shape[1]
     f16 = _cloud_kind(xyz1, xyz2) == "f16"
+    mode = int(f16) | (2 if exact_scan else 0) | {None: 0, "build": 4, "search": 8}[only]
     with torch.cuda.device(dev):
-        ws = forward_workspace(dev, b, n, m)
+        ws = workspace if workspace is not None else forward_workspace(dev, b, n, m)
         _check(load_library().pcm_tune_chamfer_forward_grid(
-            int(f16) | (2 if exact_scan else 0), _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
-            _ptr(ws), ws.numel(), _stream(dev)), "pcm_tune_chamfer_forward_grid")
+            mode, _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
+            _ptr(ws), ws.numel(), _stream(dev), _ptr(stats)), "pcm_tune_chamfer_forward_grid")
 
 
 def tune_chamfer_forward_f16(variant, xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""Grid forward diagnostics at BASELINE config 5 (B=8, N=M=16384 fp16) and a
+few other sizes: the build and search kernels timed apart (graph of 20 calls,
+HIP events), and per search wave the rounds it ran and the candidates it
+gathered (csrc/chamfer_grid.hip stats)."""
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+import pcm_hip  # noqa: E402
+from ab_grid import timed  # noqa: E402
+
+
+def main():
+    dev = torch.device("cuda:0")
+    for (b, n, m, dt) in [(8, 16384, 16384, torch.float16), (2, 4096, 4096, torch.float32),
+                          (4, 65536, 65536, torch.float32)]:
+        g = torch.Generator().manual_seed(5)
+        x1 = torch.rand(b, n, 3, generator=g).to(dt).to(dev)
+        x2 = torch.rand(b, m, 3, generator=g).to(dt).to(dev)
+        d1, d2 = torch.empty(b, n, device=dev), torch.empty(b, m, device=dev)
+        i1 = torch.empty(b, n, dtype=torch.int32, device=dev)
+        i2 = torch.empty(b, m, dtype=torch.int32, device=dev)
+        ws = pcm_hip.forward_workspace(dev, b, n, m)
+        waves = b * ((n + 63) // 64 + (m + 63) // 64)
+        st = torch.zeros(waves, 4, dtype=torch.int32, device=dev)
+        pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, stats=st, workspace=ws)
+        torch.cuda.synchronize()
+        t_all = timed(lambda: pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, workspace=ws))
+        t_b = timed(lambda: pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, only="build", workspace=ws))
+        t_s = timed(lambda: pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, only="search", workspace=ws))
+        s = st.cpu()
+        r, c0, ca = s[:, 0].float(), s[:, 1].float(), s[:, 2].float()
+        q = torch.tensor([0.5, 0.9, 0.99, 1.0])
+        print(f"B={b} N={n} M={m} {str(dt)[6:]}: both {t_all:.1f} us, build {t_b:.1f} us, search {t_s:.1f} us; "
+              f"{waves} waves", flush=True)
+        print(f"  rounds: 1: {(r == 1).sum().item()}, 2: {(r == 2).sum().item()}, 3: {(r == 3).sum().item()}", flush=True)
+        print(f"  candidates round 0 p50/p90/p99/max {[round(v) for v in torch.quantile(c0, q).tolist()]}, "
+              f"all rounds {[round(v) for v in torch.quantile(ca, q).tolist()]}, mean {ca.mean().item():.0f}",
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -71,24 +71,34 @@ __device__ __forceinline__ int cell_axis(float v, float lo, float inv_h, int G) 
     return (int)fminf(fmaxf((v - lo) * inv_h, 0.f), (float)(G - 1));
 }
 
-__device__ __forceinline__ float wave_minf(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
-    return v;
+// wave-wide reductions and scans on DPP row shifts / broadcasts (VALU operand
+// modifiers: no LDS round trip per step); results are taken from lane 63
+template <int CTRL, int ROWMASK, bool BC>
+__device__ __forceinline__ int dpp(int old, int v) {
+    return __builtin_amdgcn_update_dpp(old, v, CTRL, ROWMASK, 0xf, BC);
 }
-__device__ __forceinline__ float wave_maxf(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+template <bool kMax>
+__device__ __forceinline__ float wave_extf(float v) {
+    auto f = [](float a, float b) { return kMax ? fmaxf(a, b) : fminf(a, b); };
+    int x = __float_as_int(v);
+    x = __float_as_int(f(__int_as_float(x), __int_as_float(dpp<0x111, 0xf, false>(x, x))));  // row_shr:1
+    x = __float_as_int(f(__int_as_float(x), __int_as_float(dpp<0x112, 0xf, false>(x, x))));  // row_shr:2
+    x = __float_as_int(f(__int_as_float(x), __int_as_float(dpp<0x114, 0xf, false>(x, x))));  // row_shr:4
+    x = __float_as_int(f(__int_as_float(x), __int_as_float(dpp<0x118, 0xf, false>(x, x))));  // row_shr:8
+    x = __float_as_int(f(__int_as_float(x), __int_as_float(dpp<0x142, 0xa, false>(x, x))));  // row_bcast:15
+    x = __float_as_int(f(__int_as_float(x), __int_as_float(dpp<0x143, 0xc, false>(x, x))));  // row_bcast:31
+    return __int_as_float(__builtin_amdgcn_readlane(x, 63));
 }
-// inclusive prefix sum over the wave
+__device__ __forceinline__ float wave_minf(float v) { return wave_extf<false>(v); }
+__device__ __forceinline__ float wave_maxf(float v) { return wave_extf<true>(v); }
+// inclusive prefix sum over the wave (shifted-in lanes read 0)
 __device__ __forceinline__ int wave_incl_scan(int x) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        x += lane >= o ? y : 0;
-    }
+    x += dpp<0x111, 0xf, true>(0, x);  // row_shr:1
+    x += dpp<0x112, 0xf, true>(0, x);  // row_shr:2
+    x += dpp<0x114, 0xf, true>(0, x);  // row_shr:4
+    x += dpp<0x118, 0xf, true>(0, x);  // row_shr:8
+    x += dpp<0x142, 0xa, false>(0, x); // row_bcast:15 into rows 1 and 3
+    x += dpp<0x143, 0xc, false>(0, x); // row_bcast:31 into rows 2 and 3
     return x;
 }
 
@@ -216,15 +226,17 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
             if (c0 + k * kBuildT + tid < np) atomicAdd(&hist[cell(k)], 1);
     }
     __syncthreads();
-    const int per = ncells / kBuildT;  // 4 or 32 consecutive cells per thread
-    int total, s = 0;
-    for (int k = 0; k < per; ++k) s += hist[per * tid + k];
-    int run = block_excl_scan(s, sw, total);
-    for (int k = 0; k < per; ++k) {
-        const int cnt = hist[per * tid + k];
-        st[per * tid + k] = run;
-        hist[per * tid + k] = run;  // becomes the scatter cursor
-        run += cnt;
+    // prefix sums over the cells in segments of kBuildT consecutive cells
+    // (thread t takes cell j + t: conflict-free LDS, one block scan each)
+    const int nseg = ncells / kBuildT;  // 4 or 32
+    int total, run = 0;
+    for (int j = 0; j < ncells; j += kBuildT) {
+        const int c = j + tid;
+        const int cnt = hist[c];
+        const int ex = block_excl_scan(cnt, sw, total);
+        st[c] = run + ex;
+        hist[c] = run + ex;  // becomes the scatter cursor (own entry only)
+        run += total;
     }
     if (tid == 0) st[ncells] = np;
     __syncthreads();
@@ -244,30 +256,22 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     scatter(tpts);
     __syncthreads();
     // the same cells in query order: hist[cell] now holds the end of the
-    // cell's row-major range, so count = hist[cell] - hist[cell - 1]
-    s = 0;
-    for (int k = 0; k < per; ++k) {
-        const int cell = query_key_cell(per * tid + k, G);
-        s += hist[cell] - (cell > 0 ? hist[cell - 1] : 0);
-    }
-    run = block_excl_scan(s, sw, total);  // its barriers order the reads above before the writes below
+    // cell's row-major range, so count = hist[cell] - hist[cell - 1]; every
+    // count is read before any cursor is written (cursors in registers)
     int cur[32];
+    run = 0;
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
-        if (k < per) {
-            const int cell = query_key_cell(per * tid + k, G);
+        if (k < nseg) {
+            const int cell = query_key_cell(k * kBuildT + tid, G);
             const int cnt = hist[cell] - (cell > 0 ? hist[cell - 1] : 0);
-            cur[k] = run;
-            run += cnt;
+            cur[k] = run + block_excl_scan(cnt, sw, total);
+            run += total;
         }
     }
-    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        if (k < per) {
-            hist[query_key_cell(per * tid + k, G)] = cur[k];
-        }
-    }
+    for (int k = 0; k < 32; ++k)
+        if (k < nseg) hist[query_key_cell(k * kBuildT + tid, G)] = cur[k];
     __syncthreads();
     scatter(qpts);
     if (tid == 0) {
@@ -341,7 +345,7 @@ __device__ __forceinline__ void scan_cands(const pcm_f4 *cand, int cnt, float qx
 }
 
 template <typename TIn, bool kScreen>
-__global__ __launch_bounds__(kNnT) void grid_nn_kernel(const pcm_f4 *__restrict__ tpts,
+__global__ __launch_bounds__(kNnT) __attribute__((amdgpu_waves_per_eu(4))) void grid_nn_kernel(const pcm_f4 *__restrict__ tpts,
                                                        const pcm_f4 *__restrict__ qpts, const int *__restrict__ start,
                                                        const float *__restrict__ geo, const TIn *__restrict__ xyz1,
                                                        const TIn *__restrict__ xyz2, int b, int n, int m, int nb1,
@@ -431,16 +435,26 @@ __global__ __launch_bounds__(kNnT) void grid_nn_kernel(const pcm_f4 *__restrict_
                 const int take = min(tot - w0, kWaveCap - filled);
                 // candidate copies global -> LDS by LDS-DMA (lane l of a batch
                 // lands at slot base + l): every batch's loads in flight at once
-                for (int p0 = 0; p0 < take; p0 += 64) {
-                    const int v = w0 + p0 + lane;
-                    if (v < w0 + take) {
-                        int a = 0;  // last row whose prefix is <= v (it holds v)
+                // the row of slot v: the last row whose prefix is <= v (it
+                // holds v); the batches' searches interleaved (independent
+                // LDS chains)
+                constexpr int kB = kWaveCap / 64;
+                int v[kB], a[kB];
 #pragma unroll
-                        for (int step = 32; step > 0; step >>= 1)
-                            a = spre[a + step] <= v ? a + step : a;
-                        __builtin_amdgcn_global_load_lds((const void *)(T + sst[a] + (v - spre[a])),
-                                                         (pcm_lds_void *)(cand + filled + p0), 16, 0, 0);
-                    }
+                for (int bt = 0; bt < kB; ++bt) {
+                    v[bt] = w0 + bt * 64 + lane;
+                    a[bt] = 0;
+                }
+#pragma unroll
+                for (int step = 32; step > 0; step >>= 1) {
+#pragma unroll
+                    for (int bt = 0; bt < kB; ++bt) a[bt] = spre[a[bt] + step] <= v[bt] ? a[bt] + step : a[bt];
+                }
+#pragma unroll
+                for (int bt = 0; bt < kB; ++bt) {
+                    if (bt * 64 < take && bt * 64 + lane < take)
+                        __builtin_amdgcn_global_load_lds((const void *)(T + sst[a[bt]] + (v[bt] - spre[a[bt]])),
+                                                         (pcm_lds_void *)(cand + filled + bt * 64), 16, 0, 0);
                 }
                 filled += take;
                 w0 += take;

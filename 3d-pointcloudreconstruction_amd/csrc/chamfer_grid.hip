@@ -137,7 +137,8 @@ template <typename TIn>
 __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restrict__ xyz1,
                                                              const TIn *__restrict__ xyz2, int b, int n, int m,
                                                              pcm_f4 *__restrict__ tpts, pcm_f4 *__restrict__ qpts,
-                                                             int *__restrict__ start, float *__restrict__ geo) {
+                                                             int *__restrict__ start, float *__restrict__ geo,
+                                                             unsigned *__restrict__ stamps) {
     constexpr int kW = kBuildT / 64;
     __shared__ int hist[kMaxCells];
     __shared__ float red[7][kW];
@@ -149,6 +150,11 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     const size_t off = two ? (size_t)b * n + (size_t)e * m : (size_t)e * n;
     int *st = start + (size_t)c * (kMaxCells + 1);
     const int gb = np >= kFineMin ? 5 : 4, G = 1 << gb, ncells = 1 << (3 * gb);
+    // diagnostics (stamps != nullptr): s_memrealtime (100 MHz) at phase ends
+    auto stamp = [&](int i) {
+        if (stamps != nullptr && tid == 0) stamps[8 * c + i] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
 
     // the thread's points, kK per chunk, loads issued together: one latency
     // per chunk and pass, not per point (passes after the first hit L2)
@@ -196,6 +202,7 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     }
     for (int i = tid; i < ncells; i += kBuildT) hist[i] = 0;
     __syncthreads();
+    stamp(1);
     float lo[3], ext = 0.f;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -226,6 +233,7 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
             if (c0 + k * kBuildT + tid < np) atomicAdd(&hist[cell(k)], 1);
     }
     __syncthreads();
+    stamp(2);
     // prefix sums over the cells in segments of kBuildT consecutive cells
     // (thread t takes cell j + t: conflict-free LDS, one block scan each)
     const int nseg = ncells / kBuildT;  // 4 or 32
@@ -240,6 +248,7 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     }
     if (tid == 0) st[ncells] = np;
     __syncthreads();
+    stamp(3);
     auto scatter = [&](pcm_f4 *dst) {
         for (int c0 = 0; c0 < np; c0 += kK * kBuildT) {
             load(c0);
@@ -255,6 +264,7 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     };
     scatter(tpts);
     __syncthreads();
+    stamp(4);
     // the same cells in query order: hist[cell] now holds the end of the
     // cell's row-major range, so count = hist[cell] - hist[cell - 1]; every
     // count is read before any cursor is written (cursors in registers)
@@ -273,7 +283,10 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     for (int k = 0; k < 32; ++k)
         if (k < nseg) hist[query_key_cell(k * kBuildT + tid, G)] = cur[k];
     __syncthreads();
+    stamp(5);
     scatter(qpts);
+    __syncthreads();
+    stamp(6);
     if (tid == 0) {
         // margin (cells): the nearest neighbour of a uniform cloud of np points
         // lies beyond r with probability exp(-np 4/3 pi r^3); r = 1.43 np^-1/3
@@ -351,7 +364,7 @@ __global__ __launch_bounds__(kNnT) __attribute__((amdgpu_waves_per_eu(4))) void 
                                                        const TIn *__restrict__ xyz2, int b, int n, int m, int nb1,
                                                        int nb2, float *__restrict__ dist1, float *__restrict__ dist2,
                                                        int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
-                                                       int *__restrict__ stats) {
+                                                       int *__restrict__ stats, unsigned *__restrict__ stamps) {
     constexpr int kW = kNnT / 64;
     __shared__ pcm_f4 cand_all[kW][kWaveCap];
     __shared__ int spre_all[kW][65];
@@ -361,6 +374,10 @@ __global__ __launch_bounds__(kNnT) __attribute__((amdgpu_waves_per_eu(4))) void 
     const int per = nb1 + nb2;
     const long long blk_all = (long long)pcm_xcd_remap(blockIdx.x, gridDim.x) * kW + w;
     if (blk_all >= (long long)b * per) return;  // whole wave; no workgroup barriers below
+    auto stamp = [&](int i) {
+        if (stamps != nullptr && lane == 0) stamps[8 * blk_all + i] = (unsigned)__builtin_amdgcn_s_memrealtime();
+    };
+    stamp(0);
     const int e = (int)(blk_all / per), r = (int)(blk_all % per);
     const bool dir2 = r >= nb1;
     const int blk = dir2 ? r - nb1 : r;
@@ -394,6 +411,7 @@ __global__ __launch_bounds__(kNnT) __attribute__((amdgpu_waves_per_eu(4))) void 
 
     pcm_f4 *cand = cand_all[w];
     int *spre = spre_all[w], *sst = sst_all[w];
+    stamp(1);
     const float lo[3] = {gt[0], gt[1], gt[2]}, h = gt[3], inv = gt[4];
     const int G = (int)gt[6], margin = (int)gt[7];
     const float qc[3] = {q.x, q.y, q.z};
@@ -423,6 +441,7 @@ __global__ __launch_bounds__(kNnT) __attribute__((amdgpu_waves_per_eu(4))) void 
                 cs = Ts[base + cl[0]];
                 cnt = Ts[base + ch[0] + 1] - cs;
             }
+            if (round == 0 && r0 == 0) stamp(2);
             const int inc = wave_incl_scan(cnt);
             const int tot = __shfl(inc, 63, 64);
             candall += tot;
@@ -468,8 +487,10 @@ __global__ __launch_bounds__(kNnT) __attribute__((amdgpu_waves_per_eu(4))) void 
             wave_lds_sync();  // spre / sst are rewritten by the next 64 rows
         }
         wave_vm_sync();
+        if (round == 0) stamp(3);
         scan_cands<kScreen>(cand, filled, q.x, q.y, q.z, best);
         wave_lds_sync();
+        if (round == 0) stamp(4);
 
         // proof: every target outside the gathered cells is at least `gap`
         // away along some axis.  Cell boundaries carry the rounding of
@@ -499,6 +520,7 @@ __global__ __launch_bounds__(kNnT) __attribute__((amdgpu_waves_per_eu(4))) void 
         dout[oid] = __uint_as_float((unsigned)(best >> 32));
         iout[oid] = (int32_t)(unsigned)best;
     }
+    stamp(5);
 }
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
@@ -541,13 +563,16 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
     int *start = (int *)(base + L.start);
     float *geo = (float *)(base + L.geo);
     hipStream_t st = (hipStream_t)stream;
+    // diagnostics layout: [waves][4] stats, [2b][8] build stamps, [waves][8] search stamps
+    unsigned *bst = stats ? (unsigned *)(stats + 4 * waves) : nullptr;
+    unsigned *sst = stats ? bst + 16 * (size_t)b : nullptr;
     if (build)
         hipLaunchKernelGGL(grid_build_kernel<TIn>, dim3(2 * b), dim3(kBuildT), 0, st, xyz1, xyz2, b, n, m, tpts,
-                           qpts, start, geo);
+                           qpts, start, geo, bst);
     auto nnk = screen ? grid_nn_kernel<TIn, true> : grid_nn_kernel<TIn, false>;
     if (nn)
         hipLaunchKernelGGL(nnk, dim3((unsigned)blocks), dim3(kNnT), 0, st, tpts, qpts, start, geo, xyz1, xyz2, b, n,
-                           m, nb1, nb2, dist1, dist2, idx1, idx2, stats);
+                           m, nb1, nb2, dist1, dist2, idx1, idx2, stats, sst);
     return pcm_launch_status();
 }
 
@@ -580,7 +605,8 @@ extern "C" int pcm_chamfer_forward_ws_f16(const uint16_t *xyz1, const uint16_t *
 // the build kernel only, bit 3 = the search kernel only (on the workspace of a
 // previous call with the same clouds); stats (nullable): per wave of the
 // search, {rounds, candidates of round 0, candidates of all rounds,
-// 2 * element + direction}
+// 2 * element + direction}, then s_memrealtime stamps: 8 per cloud of the
+// build, 8 per search wave
 extern "C" int pcm_tune_chamfer_forward_grid(int mode, const void *xyz1, const void *xyz2, int b, int n, int m,
                                              float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                              void *workspace, size_t workspace_bytes, void *stream, int *stats) {

@@ -44,7 +44,7 @@ constexpr int kMaxCells = 1 << (3 * kMaxGBits);  // 32768
 constexpr int kFineMin = 12000;  // clouds from this size get G = 32
 constexpr int kBuildT = 1024;
 constexpr int kK = 8;            // points per build thread and chunk (8192 per chunk)
-constexpr int kNnT = 256;        // 4 waves, each an independent block of 64 queries
+constexpr int kNnT = 1024;       // 16 waves (one workgroup per CU), each an independent block of 64 queries
 constexpr int kWaveCap = 512;    // candidates staged per wave and round (8 KiB of LDS)
 constexpr int kGeo = 8;          // floats per cloud: lo.xyz, h, 1/h, non-finite flag, G, margin
 constexpr int kGridMinPoints = 4096;  // smaller clouds take the dense kernels
@@ -102,25 +102,6 @@ __device__ __forceinline__ int wave_incl_scan(int x) {
     return x;
 }
 
-// exclusive prefix sum over the kBuildT threads of a workgroup; two barriers
-__device__ __forceinline__ int block_excl_scan(int v, int *sw, int &total) {
-    constexpr int kW = kBuildT / 64;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int x = wave_incl_scan(v);
-    if (lane == 63) sw[w] = x;
-    __syncthreads();
-    int pre = 0, tot = 0;
-#pragma unroll
-    for (int i = 0; i < kW; ++i) {
-        const int s = sw[i];
-        pre += i < w ? s : 0;
-        tot += s;
-    }
-    __syncthreads();
-    total = tot;
-    return pre + x - v;
-}
-
 // LDS hand-off inside one wave: the wave's LDS operations complete in order,
 // so waiting for them (and fencing the compiler) is all a wave needs
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -169,20 +150,29 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
         }
     };
 
+    // bounding box from the flat coordinate array (coalesced: lane l reads
+    // element f = f0 + 1024 j + l, whose axis is (j + l) % 3 as 1024 = 1 mod 3)
     float mn[3] = {PCM_INF, PCM_INF, PCM_INF}, mx[3] = {-PCM_INF, -PCM_INF, -PCM_INF};
     float bad = 0.f;
-    for (int c0 = 0; c0 < np; c0 += kK * kBuildT) {
-        load(c0);
+    {
+        constexpr int kJ = 24;  // loads in flight per thread (a multiple of 3)
+        const int nf = 3 * np;
+        for (int f0 = 0; f0 < nf; f0 += kJ * kBuildT) {
+            float v[kJ];
 #pragma unroll
-        for (int k = 0; k < kK; ++k) {
-            if (c0 + k * kBuildT + tid < np) {
-                bad = (pcm_finite(px[k]) && pcm_finite(py[k]) && pcm_finite(pz[k])) ? bad : 1.f;
-                mn[0] = fminf(mn[0], px[k]);
-                mx[0] = fmaxf(mx[0], px[k]);
-                mn[1] = fminf(mn[1], py[k]);
-                mx[1] = fmaxf(mx[1], py[k]);
-                mn[2] = fminf(mn[2], pz[k]);
-                mx[2] = fmaxf(mx[2], pz[k]);
+            for (int j = 0; j < kJ; ++j) v[j] = pcm_ld(src + min(f0 + j * kBuildT + tid, nf - 1));
+#pragma unroll
+            for (int j = 0; j < kJ; ++j) {
+                if (f0 + j * kBuildT + tid < nf) {
+                    const int a = (j + tid) % 3;
+                    bad = pcm_finite(v[j]) ? bad : 1.f;
+                    mn[0] = a == 0 ? fminf(mn[0], v[j]) : mn[0];
+                    mx[0] = a == 0 ? fmaxf(mx[0], v[j]) : mx[0];
+                    mn[1] = a == 1 ? fminf(mn[1], v[j]) : mn[1];
+                    mx[1] = a == 1 ? fmaxf(mx[1], v[j]) : mx[1];
+                    mn[2] = a == 2 ? fminf(mn[2], v[j]) : mn[2];
+                    mx[2] = a == 2 ? fmaxf(mx[2], v[j]) : mx[2];
+                }
             }
         }
     }
@@ -234,17 +224,27 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     }
     __syncthreads();
     stamp(2);
-    // prefix sums over the cells in segments of kBuildT consecutive cells
-    // (thread t takes cell j + t: conflict-free LDS, one block scan each)
-    const int nseg = ncells / kBuildT;  // 4 or 32
-    int total, run = 0;
-    for (int j = 0; j < ncells; j += kBuildT) {
-        const int c = j + tid;
+    // prefix sums over the cells: wave w owns rows [w R, w R + R) of 64
+    // consecutive cells (conflict-free LDS), DPP scans with a running carry,
+    // then one barrier for the waves' offsets
+    const int R = ncells / kBuildT;  // rows per wave: 4 or 32
+    int carry = 0;
+    for (int r = 0; r < R; ++r) {
+        const int c = (w * R + r) * 64 + lane;
         const int cnt = hist[c];
-        const int ex = block_excl_scan(cnt, sw, total);
-        st[c] = run + ex;
-        hist[c] = run + ex;  // becomes the scatter cursor (own entry only)
-        run += total;
+        const int inc = wave_incl_scan(cnt);
+        hist[c] = carry + inc - cnt;
+        carry += __builtin_amdgcn_readlane(inc, 63);
+    }
+    if (lane == 0) sw[w] = carry;
+    __syncthreads();
+    int woff = 0;
+    for (int i = 0; i < w; ++i) woff += sw[i];
+    for (int r = 0; r < R; ++r) {
+        const int c = (w * R + r) * 64 + lane;
+        const int v = hist[c] + woff;
+        hist[c] = v;  // becomes the scatter cursor
+        st[c] = v;
     }
     if (tid == 0) st[ncells] = np;
     __syncthreads();
@@ -269,19 +269,24 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
     // cell's row-major range, so count = hist[cell] - hist[cell - 1]; every
     // count is read before any cursor is written (cursors in registers)
     int cur[32];
-    run = 0;
+    carry = 0;
 #pragma unroll
-    for (int k = 0; k < 32; ++k) {
-        if (k < nseg) {
-            const int cell = query_key_cell(k * kBuildT + tid, G);
+    for (int r = 0; r < 32; ++r) {
+        if (r < R) {
+            const int cell = query_key_cell((w * R + r) * 64 + lane, G);
             const int cnt = hist[cell] - (cell > 0 ? hist[cell - 1] : 0);
-            cur[k] = run + block_excl_scan(cnt, sw, total);
-            run += total;
+            const int inc = wave_incl_scan(cnt);
+            cur[r] = carry + inc - cnt;
+            carry += __builtin_amdgcn_readlane(inc, 63);
         }
     }
+    if (lane == 0) sw[w] = carry;  // sw was last read before the scatter's barrier
+    __syncthreads();
+    woff = 0;
+    for (int i = 0; i < w; ++i) woff += sw[i];
 #pragma unroll
-    for (int k = 0; k < 32; ++k)
-        if (k < nseg) hist[query_key_cell(k * kBuildT + tid, G)] = cur[k];
+    for (int r = 0; r < 32; ++r)
+        if (r < R) hist[query_key_cell((w * R + r) * 64 + lane, G)] = cur[r] + woff;
     __syncthreads();
     stamp(5);
     scatter(qpts);
@@ -357,15 +362,15 @@ __device__ __forceinline__ void scan_cands(const pcm_f4 *cand, int cnt, float qx
     scan_exact(cand, c8, cnt, qx, qy, qz, best);
 }
 
-template <typename TIn, bool kScreen>
-__global__ __launch_bounds__(kNnT) __attribute__((amdgpu_waves_per_eu(4))) void grid_nn_kernel(const pcm_f4 *__restrict__ tpts,
+template <typename TIn, bool kScreen, int NT>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void grid_nn_kernel(const pcm_f4 *__restrict__ tpts,
                                                        const pcm_f4 *__restrict__ qpts, const int *__restrict__ start,
                                                        const float *__restrict__ geo, const TIn *__restrict__ xyz1,
                                                        const TIn *__restrict__ xyz2, int b, int n, int m, int nb1,
                                                        int nb2, float *__restrict__ dist1, float *__restrict__ dist2,
                                                        int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
                                                        int *__restrict__ stats, unsigned *__restrict__ stamps) {
-    constexpr int kW = kNnT / 64;
+    constexpr int kW = NT / 64;
     __shared__ pcm_f4 cand_all[kW][kWaveCap];
     __shared__ int spre_all[kW][65];
     __shared__ int sst_all[kW][64];
@@ -544,7 +549,7 @@ inline bool bad_dims(int b, int n, int m) { return b < 0 || n < 0 || m < 0; }
 template <typename TIn>
 int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *dist1, float *dist2, int32_t *idx1,
                 int32_t *idx2, void *workspace, size_t workspace_bytes, void *stream, bool screen = true,
-                int *stats = nullptr, bool build = true, bool nn = true) {
+                int *stats = nullptr, bool build = true, bool nn = true, bool small_wg = false) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2)))
@@ -555,7 +560,11 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
     const int nb2 = n > 0 ? (m + 63) / 64 : 0;
     const long long waves = (long long)b * (nb1 + nb2);
     if (waves == 0) return PCM_OK;
-    const long long blocks = (waves + kNnT / 64 - 1) / (kNnT / 64);
+    // threads per search workgroup: 16 waves (fewer workgroups to dispatch)
+    // when that still fills every CU, else 4
+    if (waves < (long long)(kNnT / 64) * pcm_device_cus()) small_wg = true;
+    const int nt_wg = small_wg ? 256 : kNnT;
+    const long long blocks = (waves + nt_wg / 64 - 1) / (nt_wg / 64);
     if (blocks > 0x7fffffffLL || 2LL * b > 0x7fffffffLL) return PCM_ERR_UNSUPPORTED;
     char *base = (char *)workspace;
     pcm_f4 *tpts = (pcm_f4 *)(base + L.tpts);
@@ -569,9 +578,10 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
     if (build)
         hipLaunchKernelGGL(grid_build_kernel<TIn>, dim3(2 * b), dim3(kBuildT), 0, st, xyz1, xyz2, b, n, m, tpts,
                            qpts, start, geo, bst);
-    auto nnk = screen ? grid_nn_kernel<TIn, true> : grid_nn_kernel<TIn, false>;
+    auto nnk = small_wg ? (screen ? grid_nn_kernel<TIn, true, 256> : grid_nn_kernel<TIn, false, 256>)
+                        : (screen ? grid_nn_kernel<TIn, true, kNnT> : grid_nn_kernel<TIn, false, kNnT>);
     if (nn)
-        hipLaunchKernelGGL(nnk, dim3((unsigned)blocks), dim3(kNnT), 0, st, tpts, qpts, start, geo, xyz1, xyz2, b, n,
+        hipLaunchKernelGGL(nnk, dim3((unsigned)blocks), dim3(nt_wg), 0, st, tpts, qpts, start, geo, xyz1, xyz2, b, n,
                            m, nb1, nb2, dist1, dist2, idx1, idx2, stats, sst);
     return pcm_launch_status();
 }
@@ -603,17 +613,17 @@ extern "C" int pcm_chamfer_forward_ws_f16(const uint16_t *xyz1, const uint16_t *
 // the grid path at any size (tests and A/B): mode bit 0 = binary16 clouds,
 // bit 1 = exact scan of every candidate instead of the screened scan, bit 2 =
 // the build kernel only, bit 3 = the search kernel only (on the workspace of a
-// previous call with the same clouds); stats (nullable): per wave of the
+// previous call with the same clouds), bit 4 = 256-thread search workgroups; stats (nullable): per wave of the
 // search, {rounds, candidates of round 0, candidates of all rounds,
 // 2 * element + direction}, then s_memrealtime stamps: 8 per cloud of the
 // build, 8 per search wave
 extern "C" int pcm_tune_chamfer_forward_grid(int mode, const void *xyz1, const void *xyz2, int b, int n, int m,
                                              float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                              void *workspace, size_t workspace_bytes, void *stream, int *stats) {
-    const bool screen = !(mode & 2), build = !(mode & 8), nn = !(mode & 4);
+    const bool screen = !(mode & 2), build = !(mode & 8), nn = !(mode & 4), small_wg = (mode & 16) != 0;
     if (mode & 1)
         return launch_grid((const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace,
-                           workspace_bytes, stream, screen, stats, build, nn);
+                           workspace_bytes, stream, screen, stats, build, nn, small_wg);
     return launch_grid((const float *)xyz1, (const float *)xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace,
-                       workspace_bytes, stream, screen, stats, build, nn);
+                       workspace_bytes, stream, screen, stats, build, nn, small_wg);
 }

@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/r04i
+O=gpurun_out/r04j
 mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_chamfer_grid_gpu.py -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_grid.txt 2>&1 && \
 timeout -k 10 300 python -u tools/grid_diag.py > $O/grid_diag.txt 2>&1 && \

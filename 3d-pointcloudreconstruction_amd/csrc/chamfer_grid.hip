@@ -6,13 +6,15 @@
 // candidates a query evaluates shrinks from the whole cloud to the points of
 // the grid cells around its block, plus a proof that nothing outside can win:
 //
-//   grid_build_kernel  one workgroup per cloud (2B clouds): bounding box, a
-//                      G^3 grid of cubic cells (G = 16, or 32 from 12k points),
-//                      and two counting sorts of the points into (x, y, z,
-//                      index) float4 arrays: by row-major cell -- the target
-//                      copy, where one row of cells is one contiguous range --
-//                      and by serpentine brick order -- the query copy, where
-//                      64 consecutive points are spatially compact.
+//   build (4 kernels, workgroups over (cloud, 4096-point slice) so every CU
+//   takes part): grid_bbox_kernel -- partial bounding boxes; grid_count_kernel
+//   -- a G^3 grid of cubic cells (G = 16, or 32 from 12k points) and the cell
+//   counts (global atomics); grid_scan_kernel -- one workgroup per cloud:
+//   row-major cell starts and cursors, query-order cursors; and
+//   grid_scatter_kernel -- two sorted (x, y, z, index) float4 copies: by
+//   row-major cell -- the target copy, where one row of cells is one
+//   contiguous range -- and by serpentine brick order -- the query copy,
+//   where 64 consecutive points are spatially compact.
 //   grid_nn_kernel     one wave per 64 consecutive query-order points of one
 //                      direction.  The wave's bounding box in the target grid,
 //                      widened by `margin` cells, is gathered row range by row
@@ -43,7 +45,6 @@ constexpr int kMaxGBits = 5;
 constexpr int kMaxCells = 1 << (3 * kMaxGBits);  // 32768
 constexpr int kFineMin = 12000;  // clouds from this size get G = 32
 constexpr int kBuildT = 1024;
-constexpr int kK = 8;            // points per build thread and chunk (8192 per chunk)
 constexpr int kNnT = 1024;       // 16 waves (one workgroup per CU), each an independent block of 64 queries
 constexpr int kWaveCap = 512;    // candidates staged per wave and round (8 KiB of LDS)
 constexpr int kGeo = 8;          // floats per cloud: lo.xyz, h, 1/h, non-finite flag, G, margin
@@ -114,68 +115,113 @@ __device__ __forceinline__ unsigned long long nn_key(pcm_f4 t, float qx, float q
     return ((unsigned long long)__float_as_uint(d) << 32) | __float_as_uint(t.w);
 }
 
+// ---- build: four kernels over (cloud, slice of 4096 points) workgroups, so
+// every CU takes part (one workgroup per cloud left 16 CUs busy at config 5)
+constexpr int kSliceT = 256;                 // threads per slice workgroup
+constexpr int kSliceK = 16;                  // points per thread
+constexpr int kSlicePts = kSliceT * kSliceK; // 4096
+
+__host__ __device__ inline int grid_slices(int np) { return (np + kSlicePts - 1) / kSlicePts; }
+__device__ __forceinline__ int grid_dim(int np) { return np >= kFineMin ? 32 : 16; }
+
 template <typename TIn>
-__global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restrict__ xyz1,
-                                                             const TIn *__restrict__ xyz2, int b, int n, int m,
-                                                             pcm_f4 *__restrict__ tpts, pcm_f4 *__restrict__ qpts,
-                                                             int *__restrict__ start, float *__restrict__ geo,
-                                                             unsigned *__restrict__ stamps) {
-    constexpr int kW = kBuildT / 64;
-    __shared__ int hist[kMaxCells];
-    __shared__ float red[7][kW];
-    __shared__ int sw[kW];
-    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+struct CloudRef {
+    const TIn *src;  // [np][3]
+    size_t off;      // first point in the sorted arrays
+    int np;
+};
+template <typename TIn>
+__device__ __forceinline__ CloudRef<TIn> cloud_ref(int c, int b, int n, int m, const TIn *xyz1, const TIn *xyz2) {
     const bool two = c >= b;
-    const int e = two ? c - b : c, np = two ? m : n;
-    const TIn *src = two ? xyz2 + 3 * (size_t)e * m : xyz1 + 3 * (size_t)e * n;
-    const size_t off = two ? (size_t)b * n + (size_t)e * m : (size_t)e * n;
-    int *st = start + (size_t)c * (kMaxCells + 1);
-    const int gb = np >= kFineMin ? 5 : 4, G = 1 << gb, ncells = 1 << (3 * gb);
-    // diagnostics (stamps != nullptr): s_memrealtime (100 MHz) at phase ends
-    auto stamp = [&](int i) {
-        if (stamps != nullptr && tid == 0) stamps[8 * c + i] = (unsigned)__builtin_amdgcn_s_memrealtime();
-    };
-    stamp(0);
+    const int e = two ? c - b : c;
+    CloudRef<TIn> r;
+    r.np = two ? m : n;
+    r.src = two ? xyz2 + 3 * (size_t)e * m : xyz1 + 3 * (size_t)e * n;
+    r.off = two ? (size_t)b * n + (size_t)e * m : (size_t)e * n;
+    return r;
+}
 
-    // the thread's points, kK per chunk, loads issued together: one latency
-    // per chunk and pass, not per point (passes after the first hit L2)
-    float px[kK], py[kK], pz[kK];
-    auto load = [&](int c0) {
-#pragma unroll
-        for (int k = 0; k < kK; ++k) {
-            const int i = min(c0 + k * kBuildT + tid, np - 1);  // clamped: unconditional loads
-            px[k] = pcm_ld(src + 3 * i);
-            py[k] = pcm_ld(src + 3 * i + 1);
-            pz[k] = pcm_ld(src + 3 * i + 2);
-        }
-    };
-
-    // bounding box from the flat coordinate array (coalesced: lane l reads
-    // element f = f0 + 1024 j + l, whose axis is (j + l) % 3 as 1024 = 1 mod 3)
+// the cloud's grid from its slices' partial boxes (every thread, same bits)
+struct CloudGeom {
+    float lo[3], h, inv, bad;
+    int G;
+};
+__device__ __forceinline__ CloudGeom cloud_geom(const float *__restrict__ part, int S, int np) {
+    CloudGeom g;
     float mn[3] = {PCM_INF, PCM_INF, PCM_INF}, mx[3] = {-PCM_INF, -PCM_INF, -PCM_INF};
-    float bad = 0.f;
-    {
-        constexpr int kJ = 24;  // loads in flight per thread (a multiple of 3)
-        const int nf = 3 * np;
-        for (int f0 = 0; f0 < nf; f0 += kJ * kBuildT) {
-            float v[kJ];
+    g.bad = 0.f;
+    for (int s = 0; s < S; ++s) {
 #pragma unroll
-            for (int j = 0; j < kJ; ++j) v[j] = pcm_ld(src + min(f0 + j * kBuildT + tid, nf - 1));
+        for (int a = 0; a < 3; ++a) {
+            mn[a] = fminf(mn[a], part[8 * s + a]);
+            mx[a] = fmaxf(mx[a], part[8 * s + 3 + a]);
+        }
+        g.bad = fmaxf(g.bad, part[8 * s + 6]);
+    }
+    g.G = grid_dim(np);
+    float ext = 0.f;
 #pragma unroll
-            for (int j = 0; j < kJ; ++j) {
-                if (f0 + j * kBuildT + tid < nf) {
-                    const int a = (j + tid) % 3;
-                    bad = pcm_finite(v[j]) ? bad : 1.f;
-                    mn[0] = a == 0 ? fminf(mn[0], v[j]) : mn[0];
-                    mx[0] = a == 0 ? fmaxf(mx[0], v[j]) : mx[0];
-                    mn[1] = a == 1 ? fminf(mn[1], v[j]) : mn[1];
-                    mx[1] = a == 1 ? fmaxf(mx[1], v[j]) : mx[1];
-                    mn[2] = a == 2 ? fminf(mn[2], v[j]) : mn[2];
-                    mx[2] = a == 2 ? fmaxf(mx[2], v[j]) : mx[2];
-                }
-            }
+    for (int a = 0; a < 3; ++a) {
+        g.lo[a] = mn[a];
+        ext = fmaxf(ext, mx[a] - mn[a]);
+    }
+    g.h = ext / (float)g.G;
+    g.inv = 1.f / g.h;
+    if (!(g.h > 0.f) || !(g.inv < 1e30f)) {  // one point, coincident points or a tiny extent: unit cells
+        g.h = 1.f;
+        g.inv = 1.f;
+    }
+    return g;
+}
+// row-major cell = (iz * G + iy) * G + ix
+__device__ __forceinline__ int geom_cell(const CloudGeom &g, float x, float y, float z) {
+    return (cell_axis(z, g.lo[2], g.inv, g.G) * g.G + cell_axis(y, g.lo[1], g.inv, g.G)) * g.G +
+           cell_axis(x, g.lo[0], g.inv, g.G);
+}
+
+// the slice's points, all loads issued together (clamped: unconditional)
+template <typename TIn>
+__device__ __forceinline__ void load_slice(const CloudRef<TIn> &cr, int p0, float (&px)[kSliceK],
+                                           float (&py)[kSliceK], float (&pz)[kSliceK]) {
+#pragma unroll
+    for (int k = 0; k < kSliceK; ++k) {
+        const int i = min(p0 + k * kSliceT + (int)threadIdx.x, cr.np - 1);
+        px[k] = pcm_ld(cr.src + 3 * i);
+        py[k] = pcm_ld(cr.src + 3 * i + 1);
+        pz[k] = pcm_ld(cr.src + 3 * i + 2);
+    }
+}
+
+// 1. partial bounding box per slice; zeroes the slice's share of the counts
+template <typename TIn>
+__global__ __launch_bounds__(kSliceT) void grid_bbox_kernel(const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2,
+                                                            int b, int n, int m, int smax, float *__restrict__ part,
+                                                            int *__restrict__ counts) {
+    const int c = blockIdx.x / smax, s = blockIdx.x % smax;
+    const CloudRef<TIn> cr = cloud_ref(c, b, n, m, xyz1, xyz2);
+    const int S = grid_slices(cr.np);
+    if (s >= S) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int G = grid_dim(cr.np), ncells = G * G * G, per = (ncells + S - 1) / S;
+    int *cnt = counts + (size_t)c * kMaxCells;
+    for (int i = s * per + tid; i < min(ncells, (s + 1) * per); i += kSliceT) cnt[i] = 0;
+    float px[kSliceK], py[kSliceK], pz[kSliceK];
+    const int p0 = s * kSlicePts;
+    load_slice(cr, p0, px, py, pz);
+    float mn[3] = {PCM_INF, PCM_INF, PCM_INF}, mx[3] = {-PCM_INF, -PCM_INF, -PCM_INF}, bad = 0.f;
+#pragma unroll
+    for (int k = 0; k < kSliceK; ++k) {
+        if (p0 + k * kSliceT + tid < cr.np) {
+            bad = (pcm_finite(px[k]) && pcm_finite(py[k]) && pcm_finite(pz[k])) ? bad : 1.f;
+            mn[0] = fminf(mn[0], px[k]);
+            mx[0] = fmaxf(mx[0], px[k]);
+            mn[1] = fminf(mn[1], py[k]);
+            mx[1] = fmaxf(mx[1], py[k]);
+            mn[2] = fminf(mn[2], pz[k]);
+            mx[2] = fmaxf(mx[2], pz[k]);
         }
     }
+    __shared__ float red[7][kSliceT / 64];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         mn[a] = wave_minf(mn[a]);
@@ -190,122 +236,147 @@ __global__ __launch_bounds__(kBuildT) void grid_build_kernel(const TIn *__restri
         }
         red[6][w] = bad;
     }
-    for (int i = tid; i < ncells; i += kBuildT) hist[i] = 0;
     __syncthreads();
-    stamp(1);
-    float lo[3], ext = 0.f;
+    if (tid < 7) {
+        float v = red[tid][0];
+        for (int i = 1; i < kSliceT / 64; ++i) v = tid < 3 ? fminf(v, red[tid][i]) : fmaxf(v, red[tid][i]);
+        part[((size_t)c * smax + s) * 8 + tid] = v;
+    }
+}
+
+// 2. cell counts (global atomics)
+template <typename TIn>
+__global__ __launch_bounds__(kSliceT) void grid_count_kernel(const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2,
+                                                             int b, int n, int m, int smax,
+                                                             const float *__restrict__ part, int *__restrict__ counts) {
+    const int c = blockIdx.x / smax, s = blockIdx.x % smax;
+    const CloudRef<TIn> cr = cloud_ref(c, b, n, m, xyz1, xyz2);
+    const int S = grid_slices(cr.np);
+    if (s >= S) return;
+    const CloudGeom g = cloud_geom(part + (size_t)c * smax * 8, S, cr.np);
+    float px[kSliceK], py[kSliceK], pz[kSliceK];
+    const int p0 = s * kSlicePts;
+    load_slice(cr, p0, px, py, pz);
+    int *cnt = counts + (size_t)c * kMaxCells;
 #pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        float l = PCM_INF, hgh = -PCM_INF;
-        for (int i = 0; i < kW; ++i) {
-            l = fminf(l, red[a][i]);
-            hgh = fmaxf(hgh, red[3 + a][i]);
+    for (int k = 0; k < kSliceK; ++k)
+        if (p0 + k * kSliceT + (int)threadIdx.x < cr.np) atomicAdd(&cnt[geom_cell(g, px[k], py[k], pz[k])], 1);
+}
+
+// 3. per cloud: row-major starts (kept for the search) and scatter cursors,
+// query-order cursors, the geometry record.  Wave w owns rows [w R, w R + R)
+// of 64 consecutive cells (keys), DPP scans with a running carry, one barrier
+// for the waves' offsets.
+__global__ __launch_bounds__(kBuildT) void grid_scan_kernel(int b, int n, int m, int smax,
+                                                            const float *__restrict__ part,
+                                                            const int *__restrict__ counts, int *__restrict__ start,
+                                                            int *__restrict__ tcur, int *__restrict__ qcur,
+                                                            float *__restrict__ geo) {
+    constexpr int kW = kBuildT / 64;
+    __shared__ int sw[2][kW];
+    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int np = c >= b ? m : n;
+    const int S = grid_slices(np);
+    const int *cnt = counts + (size_t)c * kMaxCells;
+    int *st = start + (size_t)c * (kMaxCells + 1);
+    int *tc = tcur + (size_t)c * kMaxCells;
+    int *qc = qcur + (size_t)c * kMaxCells;
+    if (np == 0) {
+        if (tid == 0) {
+            st[0] = 0;
+            geo[(size_t)c * kGeo + 5] = 0.f;
         }
-        lo[a] = l;
-        ext = fmaxf(ext, hgh - l);
+        return;
     }
-    for (int i = 0; i < kW; ++i) bad = fmaxf(bad, red[6][i]);
-    float h = ext / (float)G, inv = 1.f / h;
-    if (!(h > 0.f) || !(inv < 1e30f)) {  // one point, coincident points or a tiny extent: unit cells
-        h = 1.f;
-        inv = 1.f;
-    }
-    // row-major cell = (iz * G + iy) * G + ix (recomputed per pass: registers
-    // are the budget here)
-    auto cell = [&](int k) {
-        return (cell_axis(pz[k], lo[2], inv, G) * G + cell_axis(py[k], lo[1], inv, G)) * G +
-               cell_axis(px[k], lo[0], inv, G);
-    };
-    for (int c0 = 0; c0 < np; c0 += kK * kBuildT) {
-        load(c0);
-#pragma unroll
-        for (int k = 0; k < kK; ++k)
-            if (c0 + k * kBuildT + tid < np) atomicAdd(&hist[cell(k)], 1);
-    }
-    __syncthreads();
-    stamp(2);
-    // prefix sums over the cells: wave w owns rows [w R, w R + R) of 64
-    // consecutive cells (conflict-free LDS), DPP scans with a running carry,
-    // then one barrier for the waves' offsets
-    const int R = ncells / kBuildT;  // rows per wave: 4 or 32
-    int carry = 0;
-    for (int r = 0; r < R; ++r) {
-        const int c = (w * R + r) * 64 + lane;
-        const int cnt = hist[c];
-        const int inc = wave_incl_scan(cnt);
-        hist[c] = carry + inc - cnt;
-        carry += __builtin_amdgcn_readlane(inc, 63);
-    }
-    if (lane == 0) sw[w] = carry;
-    __syncthreads();
-    int woff = 0;
-    for (int i = 0; i < w; ++i) woff += sw[i];
-    for (int r = 0; r < R; ++r) {
-        const int c = (w * R + r) * 64 + lane;
-        const int v = hist[c] + woff;
-        hist[c] = v;  // becomes the scatter cursor
-        st[c] = v;
-    }
-    if (tid == 0) st[ncells] = np;
-    __syncthreads();
-    stamp(3);
-    auto scatter = [&](pcm_f4 *dst) {
-        for (int c0 = 0; c0 < np; c0 += kK * kBuildT) {
-            load(c0);
-#pragma unroll
-            for (int k = 0; k < kK; ++k) {
-                const int i = c0 + k * kBuildT + tid;
-                if (i < np) {
-                    const int slot = atomicAdd(&hist[cell(k)], 1);
-                    dst[off + slot] = pcm_f4{px[k], py[k], pz[k], __int_as_float(i)};
-                }
-            }
-        }
-    };
-    scatter(tpts);
-    __syncthreads();
-    stamp(4);
-    // the same cells in query order: hist[cell] now holds the end of the
-    // cell's row-major range, so count = hist[cell] - hist[cell - 1]; every
-    // count is read before any cursor is written (cursors in registers)
-    int cur[32];
-    carry = 0;
+    const CloudGeom g = cloud_geom(part + (size_t)c * smax * 8, S, np);
+    const int G = g.G, ncells = G * G * G, R = ncells / kBuildT;  // rows per wave: 4 or 32
+    int rv[32], qv[32];
+    int carry = 0, qcarry = 0;
 #pragma unroll
     for (int r = 0; r < 32; ++r) {
         if (r < R) {
-            const int cell = query_key_cell((w * R + r) * 64 + lane, G);
-            const int cnt = hist[cell] - (cell > 0 ? hist[cell - 1] : 0);
-            const int inc = wave_incl_scan(cnt);
-            cur[r] = carry + inc - cnt;
-            carry += __builtin_amdgcn_readlane(inc, 63);
+            const int key = (w * R + r) * 64 + lane;
+            const int k1 = cnt[key];
+            const int i1 = wave_incl_scan(k1);
+            rv[r] = carry + i1 - k1;
+            carry += __builtin_amdgcn_readlane(i1, 63);
+            const int k2 = cnt[query_key_cell(key, G)];
+            const int i2 = wave_incl_scan(k2);
+            qv[r] = qcarry + i2 - k2;
+            qcarry += __builtin_amdgcn_readlane(i2, 63);
         }
     }
-    if (lane == 0) sw[w] = carry;  // sw was last read before the scatter's barrier
+    if (lane == 0) {
+        sw[0][w] = carry;
+        sw[1][w] = qcarry;
+    }
     __syncthreads();
-    woff = 0;
-    for (int i = 0; i < w; ++i) woff += sw[i];
+    int off = 0, qoff = 0;
+    for (int i = 0; i < w; ++i) {
+        off += sw[0][i];
+        qoff += sw[1][i];
+    }
 #pragma unroll
-    for (int r = 0; r < 32; ++r)
-        if (r < R) hist[query_key_cell((w * R + r) * 64 + lane, G)] = cur[r] + woff;
-    __syncthreads();
-    stamp(5);
-    scatter(qpts);
-    __syncthreads();
-    stamp(6);
+    for (int r = 0; r < 32; ++r) {
+        if (r < R) {
+            const int key = (w * R + r) * 64 + lane;
+            st[key] = rv[r] + off;
+            tc[key] = rv[r] + off;
+            qc[query_key_cell(key, G)] = qv[r] + qoff;
+        }
+    }
     if (tid == 0) {
+        st[ncells] = np;
         // margin (cells): the nearest neighbour of a uniform cloud of np points
         // lies beyond r with probability exp(-np 4/3 pi r^3); r = 1.43 np^-1/3
         // of the extent makes that ~e^-12
-        const float mg = ceilf(1.43f * (float)G * cbrtf(1.f / (float)(np > 0 ? np : 1)));
-        float *g = geo + (size_t)c * kGeo;
-        g[0] = lo[0];
-        g[1] = lo[1];
-        g[2] = lo[2];
-        g[3] = h;
-        g[4] = inv;
-        g[5] = bad;
-        g[6] = (float)G;
-        g[7] = fminf(fmaxf(mg, 1.f), 4.f);
+        const float mg = ceilf(1.43f * (float)G * cbrtf(1.f / (float)np));
+        float *gg = geo + (size_t)c * kGeo;
+        gg[0] = g.lo[0];
+        gg[1] = g.lo[1];
+        gg[2] = g.lo[2];
+        gg[3] = g.h;
+        gg[4] = g.inv;
+        gg[5] = g.bad;
+        gg[6] = (float)G;
+        gg[7] = fminf(fmaxf(mg, 1.f), 4.f);
+    }
+}
+
+// 4. both sorted copies (global atomics on the cursors)
+template <typename TIn>
+__global__ __launch_bounds__(kSliceT) void grid_scatter_kernel(const TIn *__restrict__ xyz1,
+                                                               const TIn *__restrict__ xyz2, int b, int n, int m,
+                                                               int smax, const float *__restrict__ part,
+                                                               int *__restrict__ tcur, int *__restrict__ qcur,
+                                                               pcm_f4 *__restrict__ tpts, pcm_f4 *__restrict__ qpts) {
+    const int c = blockIdx.x / smax, s = blockIdx.x % smax;
+    const CloudRef<TIn> cr = cloud_ref(c, b, n, m, xyz1, xyz2);
+    const int S = grid_slices(cr.np);
+    if (s >= S) return;
+    const CloudGeom g = cloud_geom(part + (size_t)c * smax * 8, S, cr.np);
+    float px[kSliceK], py[kSliceK], pz[kSliceK];
+    const int p0 = s * kSlicePts;
+    load_slice(cr, p0, px, py, pz);
+    int *tc = tcur + (size_t)c * kMaxCells;
+    int *qc = qcur + (size_t)c * kMaxCells;
+    int cl[kSliceK], ts[kSliceK], qs[kSliceK];
+#pragma unroll
+    for (int k = 0; k < kSliceK; ++k) cl[k] = geom_cell(g, px[k], py[k], pz[k]);
+#pragma unroll
+    for (int k = 0; k < kSliceK; ++k) {
+        const bool v = p0 + k * kSliceT + (int)threadIdx.x < cr.np;
+        ts[k] = v ? atomicAdd(&tc[cl[k]], 1) : 0;
+        qs[k] = v ? atomicAdd(&qc[cl[k]], 1) : 0;
+    }
+#pragma unroll
+    for (int k = 0; k < kSliceK; ++k) {
+        const int i = p0 + k * kSliceT + (int)threadIdx.x;
+        if (i < cr.np) {
+            const pcm_f4 v = pcm_f4{px[k], py[k], pz[k], __int_as_float(i)};
+            tpts[cr.off + ts[k]] = v;
+            qpts[cr.off + qs[k]] = v;
+        }
     }
 }
 
@@ -531,16 +602,23 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void gr
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct GridLayout {
-    size_t tpts, qpts, start, geo, total;
+    size_t tpts, qpts, start, geo, part, counts, tcur, qcur, total;
+    int smax;
 };
 inline GridLayout grid_layout(int b, int n, int m) {
     GridLayout L;
     const size_t pts = align256(16 * (size_t)b * ((size_t)n + m));
+    const size_t cells = align256(4 * (size_t)2 * b * kMaxCells);
+    L.smax = grid_slices(n > m ? n : m);
     L.tpts = 0;
     L.qpts = pts;
     L.start = 2 * pts;
     L.geo = L.start + align256(4 * (size_t)2 * b * (kMaxCells + 1));
-    L.total = L.geo + align256(4 * (size_t)2 * b * kGeo);
+    L.part = L.geo + align256(4 * (size_t)2 * b * kGeo);
+    L.counts = L.part + align256(4 * (size_t)2 * b * (L.smax > 0 ? L.smax : 1) * 8);
+    L.tcur = L.counts + cells;
+    L.qcur = L.tcur + cells;
+    L.total = L.qcur + cells;
     return L;
 }
 
@@ -571,13 +649,22 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
     pcm_f4 *qpts = (pcm_f4 *)(base + L.qpts);
     int *start = (int *)(base + L.start);
     float *geo = (float *)(base + L.geo);
+    float *part = (float *)(base + L.part);
+    int *counts = (int *)(base + L.counts), *tcur = (int *)(base + L.tcur), *qcur = (int *)(base + L.qcur);
     hipStream_t st = (hipStream_t)stream;
-    // diagnostics layout: [waves][4] stats, [2b][8] build stamps, [waves][8] search stamps
-    unsigned *bst = stats ? (unsigned *)(stats + 4 * waves) : nullptr;
-    unsigned *sst = stats ? bst + 16 * (size_t)b : nullptr;
-    if (build)
-        hipLaunchKernelGGL(grid_build_kernel<TIn>, dim3(2 * b), dim3(kBuildT), 0, st, xyz1, xyz2, b, n, m, tpts,
-                           qpts, start, geo, bst);
+    // diagnostics layout: [waves][4] stats, then [waves][8] search stamps
+    unsigned *sst = stats ? (unsigned *)(stats + 4 * waves) : nullptr;
+    if (build) {
+        const unsigned sg = (unsigned)(2 * b * L.smax);
+        hipLaunchKernelGGL(grid_bbox_kernel<TIn>, dim3(sg), dim3(kSliceT), 0, st, xyz1, xyz2, b, n, m, L.smax, part,
+                           counts);
+        hipLaunchKernelGGL(grid_count_kernel<TIn>, dim3(sg), dim3(kSliceT), 0, st, xyz1, xyz2, b, n, m, L.smax, part,
+                           counts);
+        hipLaunchKernelGGL(grid_scan_kernel, dim3(2 * b), dim3(kBuildT), 0, st, b, n, m, L.smax, part, counts, start,
+                           tcur, qcur, geo);
+        hipLaunchKernelGGL(grid_scatter_kernel<TIn>, dim3(sg), dim3(kSliceT), 0, st, xyz1, xyz2, b, n, m, L.smax,
+                           part, tcur, qcur, tpts, qpts);
+    }
     auto nnk = small_wg ? (screen ? grid_nn_kernel<TIn, true, 256> : grid_nn_kernel<TIn, false, 256>)
                         : (screen ? grid_nn_kernel<TIn, true, kNnT> : grid_nn_kernel<TIn, false, kNnT>);
     if (nn)

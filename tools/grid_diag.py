@@ -27,12 +27,11 @@ def main():
         i2 = torch.empty(b, m, dtype=torch.int32, device=dev)
         ws = pcm_hip.forward_workspace(dev, b, n, m)
         waves = b * ((n + 63) // 64 + (m + 63) // 64)
-        st_all = torch.zeros(waves * 4 + 2 * b * 8 + waves * 8, dtype=torch.int32, device=dev)
+        st_all = torch.zeros(waves * 4 + waves * 8, dtype=torch.int32, device=dev)
         pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, stats=st_all, workspace=ws)
         torch.cuda.synchronize()
         st = st_all[: waves * 4].view(waves, 4)
-        bs = st_all[waves * 4: waves * 4 + 16 * b].view(2 * b, 8).cpu().long() & 0xffffffff
-        ss = st_all[waves * 4 + 16 * b:].view(waves, 8).cpu().long() & 0xffffffff
+        ss = st_all[waves * 4:].view(waves, 8).cpu().long() & 0xffffffff
         t_all = timed(lambda: pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, workspace=ws))
         t_b = timed(lambda: pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, only="build", workspace=ws))
         t_s = timed(lambda: pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, only="search", workspace=ws))
@@ -44,11 +43,6 @@ def main():
         print(f"B={b} N={n} M={m} {str(dt)[6:]}: both {t_all:.1f} us, build {t_b:.1f} us, search {t_s:.1f} us (256-thread workgroups {t_s4:.1f}); "
               f"{waves} waves", flush=True)
         print(f"  rounds: 1: {(r == 1).sum().item()}, 2: {(r == 2).sum().item()}, 3: {(r == 3).sum().item()}", flush=True)
-        bd = (bs[:, 1:7] - bs[:, 0:6]).float() * 0.01  # 100 MHz ticks -> us
-        names = ["bbox", "hist", "scan", "scatter1", "scan2", "scatter2"]
-        print("  build phases (median over clouds, us): " +
-              ", ".join(f"{nm} {bd[:, i].median().item():.2f}" for i, nm in enumerate(names)) +
-              f"; total {((bs[:, 6] - bs[:, 0]).float() * 0.01).median().item():.2f}", flush=True)
         t0 = ss[:, 0].min()
         sd = (ss[:, 1:6] - ss[:, 0:5]).float() * 0.01
         names = ["prologue", "box+rows", "gather", "scan", "proof+out"]

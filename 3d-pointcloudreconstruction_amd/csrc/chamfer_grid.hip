@@ -6,15 +6,14 @@
 // candidates a query evaluates shrinks from the whole cloud to the points of
 // the grid cells around its block, plus a proof that nothing outside can win:
 //
-//   build (4 kernels, workgroups over (cloud, 4096-point slice) so every CU
-//   takes part): grid_bbox_kernel -- partial bounding boxes; grid_count_kernel
-//   -- a G^3 grid of cubic cells (G = 16, or 32 from 12k points) and the cell
-//   counts (global atomics); grid_scan_kernel -- one workgroup per cloud:
-//   row-major cell starts and cursors, query-order cursors; and
-//   grid_scatter_kernel -- two sorted (x, y, z, index) float4 copies: by
-//   row-major cell -- the target copy, where one row of cells is one
-//   contiguous range -- and by serpentine brick order -- the query copy,
-//   where 64 consecutive points are spatially compact.
+//   grid_build_kernel  one workgroup per (cloud, slab of 4 cell layers): a
+//                      G^3 grid of cubic cells (G = 16, or 32 from 12k
+//                      points) over the cloud's bounding box and two sorted
+//                      (x, y, z, index) float4 copies: by row-major cell --
+//                      the target copy, where one row of cells is one
+//                      contiguous range -- and by serpentine brick order --
+//                      the query copy, where 64 consecutive points are
+//                      spatially compact.  No global atomics, no waits.
 //   grid_nn_kernel     one wave per 64 consecutive query-order points of one
 //                      direction.  The wave's bounding box in the target grid,
 //                      widened by `margin` cells, is gathered row range by row
@@ -44,7 +43,6 @@ namespace {
 constexpr int kMaxGBits = 5;
 constexpr int kMaxCells = 1 << (3 * kMaxGBits);  // 32768
 constexpr int kFineMin = 12000;  // clouds from this size get G = 32
-constexpr int kBuildT = 1024;
 constexpr int kNnT = 1024;       // 16 waves (one workgroup per CU), each an independent block of 64 queries
 constexpr int kWaveCap = 512;    // candidates staged per wave and round (8 KiB of LDS)
 constexpr int kGeo = 8;          // floats per cloud: lo.xyz, h, 1/h, non-finite flag, G, margin
@@ -53,18 +51,8 @@ constexpr int kGridMinPoints = 4096;  // smaller clouds take the dense kernels
 // Query order: bricks of 4x4x4 cells visited in a serpentine (boustrophedon)
 // order -- consecutive bricks always share a face, so any run of consecutive
 // points spans a few neighbouring bricks (a Z-order curve jumps across the
-// grid at its octant seams) -- and the cells of a brick in row-major order.
-// key -> row-major cell index.
-__device__ __forceinline__ int query_key_cell(int key, int G) {
-    const int nb = G >> 2;
-    const int bi = key >> 6, l = key & 63;
-    const int r = bi / nb, bxp = bi - r * nb;
-    const int bz = r / nb, byp = r - bz * nb;
-    const int bx = (r & 1) ? nb - 1 - bxp : bxp;
-    const int by = (bz & 1) ? nb - 1 - byp : byp;
-    const int x = 4 * bx + (l & 3), y = 4 * by + ((l >> 2) & 3), z = 4 * bz + (l >> 4);
-    return (z * G + y) * G + x;
-}
+// grid at its octant seams) -- and the cells of a brick in row-major order
+// (cell_query_key below).
 // cell coordinate along one axis: floor((v - lo) / h) clamped to the grid
 // (NaN -> 0; only reached for clouds flagged non-finite, whose results come
 // from the reference scan)
@@ -115,113 +103,79 @@ __device__ __forceinline__ unsigned long long nn_key(pcm_f4 t, float qx, float q
     return ((unsigned long long)__float_as_uint(d) << 32) | __float_as_uint(t.w);
 }
 
-// ---- build: four kernels over (cloud, slice of 4096 points) workgroups, so
-// every CU takes part (one workgroup per cloud left 16 CUs busy at config 5)
-constexpr int kSliceT = 256;                 // threads per slice workgroup
-constexpr int kSliceK = 16;                  // points per thread
-constexpr int kSlicePts = kSliceT * kSliceK; // 4096
+// ---- build: one workgroup per (cloud, slab of 4 cell layers in z).  Both
+// orders (row-major cells; serpentine bricks, whose bricks are 4 layers
+// thick) put whole slabs in z order, so a slab's points occupy one contiguous
+// range of either sorted copy, whose offset is the count of points in lower
+// slabs.  Every workgroup of a cloud reads the whole cloud (L2-resident after
+// the first): bounding box, then slab counts and its own slab's two cell
+// histograms in LDS, then its own points' positions -- no global atomics
+// (device-scope atomics leave the XCD: 13 us for config 5's counts alone)
+// and no workgroup waits on another.
+constexpr int kSlabT = 1024;
+constexpr int kSlabK = 16;   // points per thread and pass chunk (16384 per chunk)
+constexpr int kSlabMax = 8;  // slabs per cloud: G / 4
+constexpr int kSlabCells = 4 * 32 * 32;  // cells of one slab at G = 32
 
-__host__ __device__ inline int grid_slices(int np) { return (np + kSlicePts - 1) / kSlicePts; }
 __device__ __forceinline__ int grid_dim(int np) { return np >= kFineMin ? 32 : 16; }
 
-template <typename TIn>
-struct CloudRef {
-    const TIn *src;  // [np][3]
-    size_t off;      // first point in the sorted arrays
-    int np;
-};
-template <typename TIn>
-__device__ __forceinline__ CloudRef<TIn> cloud_ref(int c, int b, int n, int m, const TIn *xyz1, const TIn *xyz2) {
-    const bool two = c >= b;
-    const int e = two ? c - b : c;
-    CloudRef<TIn> r;
-    r.np = two ? m : n;
-    r.src = two ? xyz2 + 3 * (size_t)e * m : xyz1 + 3 * (size_t)e * n;
-    r.off = two ? (size_t)b * n + (size_t)e * m : (size_t)e * n;
-    return r;
+// cell (x, y, z) -> its key in the query (serpentine brick) order
+__device__ __forceinline__ int cell_query_key(int x, int y, int z, int G) {
+    const int nb = G >> 2;
+    const int bx = x >> 2, by = y >> 2, bz = z >> 2;
+    const int r = bz * nb + ((bz & 1) ? nb - 1 - by : by);
+    const int bi = r * nb + ((r & 1) ? nb - 1 - bx : bx);
+    return (bi << 6) + (((z & 3) * 4 + (y & 3)) << 2) + (x & 3);
 }
 
-// the cloud's grid from its slices' partial boxes (every thread, same bits)
-struct CloudGeom {
-    float lo[3], h, inv, bad;
-    int G;
-};
-__device__ __forceinline__ CloudGeom cloud_geom(const float *__restrict__ part, int S, int np) {
-    CloudGeom g;
-    float mn[3] = {PCM_INF, PCM_INF, PCM_INF}, mx[3] = {-PCM_INF, -PCM_INF, -PCM_INF};
-    g.bad = 0.f;
-    for (int s = 0; s < S; ++s) {
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            mn[a] = fminf(mn[a], part[8 * s + a]);
-            mx[a] = fmaxf(mx[a], part[8 * s + 3 + a]);
-        }
-        g.bad = fmaxf(g.bad, part[8 * s + 6]);
-    }
-    g.G = grid_dim(np);
-    float ext = 0.f;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        g.lo[a] = mn[a];
-        ext = fmaxf(ext, mx[a] - mn[a]);
-    }
-    g.h = ext / (float)g.G;
-    g.inv = 1.f / g.h;
-    if (!(g.h > 0.f) || !(g.inv < 1e30f)) {  // one point, coincident points or a tiny extent: unit cells
-        g.h = 1.f;
-        g.inv = 1.f;
-    }
-    return g;
-}
-// row-major cell = (iz * G + iy) * G + ix
-__device__ __forceinline__ int geom_cell(const CloudGeom &g, float x, float y, float z) {
-    return (cell_axis(z, g.lo[2], g.inv, g.G) * g.G + cell_axis(y, g.lo[1], g.inv, g.G)) * g.G +
-           cell_axis(x, g.lo[0], g.inv, g.G);
-}
-
-// the slice's points, all loads issued together (clamped: unconditional)
 template <typename TIn>
-__device__ __forceinline__ void load_slice(const CloudRef<TIn> &cr, int p0, float (&px)[kSliceK],
-                                           float (&py)[kSliceK], float (&pz)[kSliceK]) {
-#pragma unroll
-    for (int k = 0; k < kSliceK; ++k) {
-        const int i = min(p0 + k * kSliceT + (int)threadIdx.x, cr.np - 1);
-        px[k] = pcm_ld(cr.src + 3 * i);
-        py[k] = pcm_ld(cr.src + 3 * i + 1);
-        pz[k] = pcm_ld(cr.src + 3 * i + 2);
-    }
-}
-
-// 1. partial bounding box per slice; zeroes the slice's share of the counts
-template <typename TIn>
-__global__ __launch_bounds__(kSliceT) void grid_bbox_kernel(const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2,
-                                                            int b, int n, int m, int smax, float *__restrict__ part,
-                                                            int *__restrict__ counts) {
-    const int c = blockIdx.x / smax, s = blockIdx.x % smax;
-    const CloudRef<TIn> cr = cloud_ref(c, b, n, m, xyz1, xyz2);
-    const int S = grid_slices(cr.np);
-    if (s >= S) return;
+__global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2,
+                                                            int b, int n, int m, pcm_f4 *__restrict__ tpts,
+                                                            pcm_f4 *__restrict__ qpts, int *__restrict__ start,
+                                                            float *__restrict__ geo) {
+    constexpr int kW = kSlabT / 64;
+    __shared__ int hT[kSlabCells], hQ[kSlabCells];  // own slab: row-major / query-order histograms -> cursors
+    __shared__ float red[7][kW];
+    __shared__ int sSlab[kSlabMax];
+    __shared__ int sw[2][kW];
+    const int c = blockIdx.x / kSlabMax, slab = blockIdx.x % kSlabMax;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int G = grid_dim(cr.np), ncells = G * G * G, per = (ncells + S - 1) / S;
-    int *cnt = counts + (size_t)c * kMaxCells;
-    for (int i = s * per + tid; i < min(ncells, (s + 1) * per); i += kSliceT) cnt[i] = 0;
-    float px[kSliceK], py[kSliceK], pz[kSliceK];
-    const int p0 = s * kSlicePts;
-    load_slice(cr, p0, px, py, pz);
-    float mn[3] = {PCM_INF, PCM_INF, PCM_INF}, mx[3] = {-PCM_INF, -PCM_INF, -PCM_INF}, bad = 0.f;
+    const bool two = c >= b;
+    const int e = two ? c - b : c, np = two ? m : n;
+    const int G = grid_dim(np), NS = G >> 2, scells = 4 * G * G;
+    if (np == 0 || slab >= NS) return;
+    const TIn *src = two ? xyz2 + 3 * (size_t)e * m : xyz1 + 3 * (size_t)e * n;
+    const size_t off = two ? (size_t)b * n + (size_t)e * m : (size_t)e * n;
+    int *st = start + (size_t)c * (kMaxCells + 1);
+
+    float px[kSlabK], py[kSlabK], pz[kSlabK];
+    auto load = [&](int c0) {  // the chunk's loads issued together (clamped: unconditional)
 #pragma unroll
-    for (int k = 0; k < kSliceK; ++k) {
-        if (p0 + k * kSliceT + tid < cr.np) {
-            bad = (pcm_finite(px[k]) && pcm_finite(py[k]) && pcm_finite(pz[k])) ? bad : 1.f;
-            mn[0] = fminf(mn[0], px[k]);
-            mx[0] = fmaxf(mx[0], px[k]);
-            mn[1] = fminf(mn[1], py[k]);
-            mx[1] = fmaxf(mx[1], py[k]);
-            mn[2] = fminf(mn[2], pz[k]);
-            mx[2] = fmaxf(mx[2], pz[k]);
+        for (int k = 0; k < kSlabK; ++k) {
+            const int i = min(c0 + k * kSlabT + tid, np - 1);
+            px[k] = pcm_ld(src + 3 * i);
+            py[k] = pcm_ld(src + 3 * i + 1);
+            pz[k] = pcm_ld(src + 3 * i + 2);
+        }
+    };
+
+    // 1. bounding box (every workgroup of the cloud computes the same bits)
+    float mn[3] = {PCM_INF, PCM_INF, PCM_INF}, mx[3] = {-PCM_INF, -PCM_INF, -PCM_INF}, bad = 0.f;
+    for (int c0 = 0; c0 < np; c0 += kSlabK * kSlabT) {
+        load(c0);
+#pragma unroll
+        for (int k = 0; k < kSlabK; ++k) {
+            if (c0 + k * kSlabT + tid < np) {
+                bad = (pcm_finite(px[k]) && pcm_finite(py[k]) && pcm_finite(pz[k])) ? bad : 1.f;
+                mn[0] = fminf(mn[0], px[k]);
+                mx[0] = fmaxf(mx[0], px[k]);
+                mn[1] = fminf(mn[1], py[k]);
+                mx[1] = fmaxf(mx[1], py[k]);
+                mn[2] = fminf(mn[2], pz[k]);
+                mx[2] = fmaxf(mx[2], pz[k]);
+            }
         }
     }
-    __shared__ float red[7][kSliceT / 64];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         mn[a] = wave_minf(mn[a]);
@@ -236,147 +190,128 @@ __global__ __launch_bounds__(kSliceT) void grid_bbox_kernel(const TIn *__restric
         }
         red[6][w] = bad;
     }
+    for (int i = tid; i < scells; i += kSlabT) {
+        hT[i] = 0;
+        hQ[i] = 0;
+    }
+    if (tid < kSlabMax) sSlab[tid] = 0;
     __syncthreads();
-    if (tid < 7) {
-        float v = red[tid][0];
-        for (int i = 1; i < kSliceT / 64; ++i) v = tid < 3 ? fminf(v, red[tid][i]) : fmaxf(v, red[tid][i]);
-        part[((size_t)c * smax + s) * 8 + tid] = v;
-    }
-}
-
-// 2. cell counts (global atomics)
-template <typename TIn>
-__global__ __launch_bounds__(kSliceT) void grid_count_kernel(const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2,
-                                                             int b, int n, int m, int smax,
-                                                             const float *__restrict__ part, int *__restrict__ counts) {
-    const int c = blockIdx.x / smax, s = blockIdx.x % smax;
-    const CloudRef<TIn> cr = cloud_ref(c, b, n, m, xyz1, xyz2);
-    const int S = grid_slices(cr.np);
-    if (s >= S) return;
-    const CloudGeom g = cloud_geom(part + (size_t)c * smax * 8, S, cr.np);
-    float px[kSliceK], py[kSliceK], pz[kSliceK];
-    const int p0 = s * kSlicePts;
-    load_slice(cr, p0, px, py, pz);
-    int *cnt = counts + (size_t)c * kMaxCells;
+    float lo[3], ext = 0.f;
 #pragma unroll
-    for (int k = 0; k < kSliceK; ++k)
-        if (p0 + k * kSliceT + (int)threadIdx.x < cr.np) atomicAdd(&cnt[geom_cell(g, px[k], py[k], pz[k])], 1);
-}
-
-// 3. per cloud: row-major starts (kept for the search) and scatter cursors,
-// query-order cursors, the geometry record.  Wave w owns rows [w R, w R + R)
-// of 64 consecutive cells (keys), DPP scans with a running carry, one barrier
-// for the waves' offsets.
-__global__ __launch_bounds__(kBuildT) void grid_scan_kernel(int b, int n, int m, int smax,
-                                                            const float *__restrict__ part,
-                                                            const int *__restrict__ counts, int *__restrict__ start,
-                                                            int *__restrict__ tcur, int *__restrict__ qcur,
-                                                            float *__restrict__ geo) {
-    constexpr int kW = kBuildT / 64;
-    __shared__ int sw[2][kW];
-    const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int np = c >= b ? m : n;
-    const int S = grid_slices(np);
-    const int *cnt = counts + (size_t)c * kMaxCells;
-    int *st = start + (size_t)c * (kMaxCells + 1);
-    int *tc = tcur + (size_t)c * kMaxCells;
-    int *qc = qcur + (size_t)c * kMaxCells;
-    if (np == 0) {
-        if (tid == 0) {
-            st[0] = 0;
-            geo[(size_t)c * kGeo + 5] = 0.f;
+    for (int a = 0; a < 3; ++a) {
+        float l = PCM_INF, hgh = -PCM_INF;
+        for (int i = 0; i < kW; ++i) {
+            l = fminf(l, red[a][i]);
+            hgh = fmaxf(hgh, red[3 + a][i]);
         }
-        return;
+        lo[a] = l;
+        ext = fmaxf(ext, hgh - l);
     }
-    const CloudGeom g = cloud_geom(part + (size_t)c * smax * 8, S, np);
-    const int G = g.G, ncells = G * G * G, R = ncells / kBuildT;  // rows per wave: 4 or 32
-    int rv[32], qv[32];
-    int carry = 0, qcarry = 0;
+    for (int i = 0; i < kW; ++i) bad = fmaxf(bad, red[6][i]);
+    float h = ext / (float)G, inv = 1.f / h;
+    if (!(h > 0.f) || !(inv < 1e30f)) {  // one point, coincident points or a tiny extent: unit cells
+        h = 1.f;
+        inv = 1.f;
+    }
+    const int z0 = 4 * slab, kbase = slab * (G / 4) * (G / 4) * 64;  // first cell layer / query key of the slab
+
+    // 2. slab counts (ballots) and the own slab's histograms
+    int scnt[kSlabMax];
 #pragma unroll
-    for (int r = 0; r < 32; ++r) {
+    for (int k = 0; k < kSlabMax; ++k) scnt[k] = 0;
+    for (int c0 = 0; c0 < np; c0 += kSlabK * kSlabT) {
+        load(c0);
+#pragma unroll
+        for (int k = 0; k < kSlabK; ++k) {
+            const bool v = c0 + k * kSlabT + tid < np;
+            const int ix = cell_axis(px[k], lo[0], inv, G), iy = cell_axis(py[k], lo[1], inv, G),
+                      iz = cell_axis(pz[k], lo[2], inv, G);
+            const int sl = iz >> 2;
+#pragma unroll
+            for (int q = 0; q < kSlabMax; ++q) scnt[q] += __popcll(__ballot(v && sl == q));
+            if (v && sl == slab) {
+                atomicAdd(&hT[((iz - z0) * G + iy) * G + ix], 1);
+                atomicAdd(&hQ[cell_query_key(ix, iy, iz, G) - kbase], 1);
+            }
+        }
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < kSlabMax; ++q)
+            if (scnt[q]) atomicAdd(&sSlab[q], scnt[q]);
+    }
+    __syncthreads();
+    int soff = 0;
+    for (int q = 0; q < slab; ++q) soff += sSlab[q];
+
+    // 3. exclusive scans of both histograms (wave w: rows [w R, w R + R) of
+    // 64 bins, DPP scans with a carry; one barrier for the waves' offsets);
+    // the row-major starts go to global for the search
+    const int R = scells / kSlabT;  // 4 (G = 32) or 1 (G = 16)
+    int tv[4], qv[4], tcarry = 0, qcarry = 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
         if (r < R) {
-            const int key = (w * R + r) * 64 + lane;
-            const int k1 = cnt[key];
-            const int i1 = wave_incl_scan(k1);
-            rv[r] = carry + i1 - k1;
-            carry += __builtin_amdgcn_readlane(i1, 63);
-            const int k2 = cnt[query_key_cell(key, G)];
-            const int i2 = wave_incl_scan(k2);
-            qv[r] = qcarry + i2 - k2;
+            const int i = (w * R + r) * 64 + lane;
+            const int a1 = hT[i], a2 = hQ[i];
+            const int i1 = wave_incl_scan(a1), i2 = wave_incl_scan(a2);
+            tv[r] = tcarry + i1 - a1;
+            qv[r] = qcarry + i2 - a2;
+            tcarry += __builtin_amdgcn_readlane(i1, 63);
             qcarry += __builtin_amdgcn_readlane(i2, 63);
         }
     }
     if (lane == 0) {
-        sw[0][w] = carry;
+        sw[0][w] = tcarry;
         sw[1][w] = qcarry;
     }
     __syncthreads();
-    int off = 0, qoff = 0;
+    int toff = soff, qoff = soff;
     for (int i = 0; i < w; ++i) {
-        off += sw[0][i];
+        toff += sw[0][i];
         qoff += sw[1][i];
     }
 #pragma unroll
-    for (int r = 0; r < 32; ++r) {
+    for (int r = 0; r < 4; ++r) {
         if (r < R) {
-            const int key = (w * R + r) * 64 + lane;
-            st[key] = rv[r] + off;
-            tc[key] = rv[r] + off;
-            qc[query_key_cell(key, G)] = qv[r] + qoff;
+            const int i = (w * R + r) * 64 + lane;
+            hT[i] = tv[r] + toff;  // cursors (absolute positions in the cloud's range)
+            hQ[i] = qv[r] + qoff;
+            st[z0 * G * G + i] = tv[r] + toff;
         }
     }
-    if (tid == 0) {
-        st[ncells] = np;
+    if (slab == NS - 1 && tid == 0) st[G * G * G] = np;
+    __syncthreads();
+
+    // 4. the own slab's points into both copies
+    for (int c0 = 0; c0 < np; c0 += kSlabK * kSlabT) {
+        load(c0);
+#pragma unroll
+        for (int k = 0; k < kSlabK; ++k) {
+            const int i = c0 + k * kSlabT + tid;
+            const int ix = cell_axis(px[k], lo[0], inv, G), iy = cell_axis(py[k], lo[1], inv, G),
+                      iz = cell_axis(pz[k], lo[2], inv, G);
+            if (i < np && (iz >> 2) == slab) {
+                const pcm_f4 v = pcm_f4{px[k], py[k], pz[k], __int_as_float(i)};
+                tpts[off + atomicAdd(&hT[((iz - z0) * G + iy) * G + ix], 1)] = v;
+                qpts[off + atomicAdd(&hQ[cell_query_key(ix, iy, iz, G) - kbase], 1)] = v;
+            }
+        }
+    }
+    if (slab == 0 && tid == 0) {
         // margin (cells): the nearest neighbour of a uniform cloud of np points
         // lies beyond r with probability exp(-np 4/3 pi r^3); r = 1.43 np^-1/3
         // of the extent makes that ~e^-12
         const float mg = ceilf(1.43f * (float)G * cbrtf(1.f / (float)np));
         float *gg = geo + (size_t)c * kGeo;
-        gg[0] = g.lo[0];
-        gg[1] = g.lo[1];
-        gg[2] = g.lo[2];
-        gg[3] = g.h;
-        gg[4] = g.inv;
-        gg[5] = g.bad;
+        gg[0] = lo[0];
+        gg[1] = lo[1];
+        gg[2] = lo[2];
+        gg[3] = h;
+        gg[4] = inv;
+        gg[5] = bad;
         gg[6] = (float)G;
         gg[7] = fminf(fmaxf(mg, 1.f), 4.f);
-    }
-}
-
-// 4. both sorted copies (global atomics on the cursors)
-template <typename TIn>
-__global__ __launch_bounds__(kSliceT) void grid_scatter_kernel(const TIn *__restrict__ xyz1,
-                                                               const TIn *__restrict__ xyz2, int b, int n, int m,
-                                                               int smax, const float *__restrict__ part,
-                                                               int *__restrict__ tcur, int *__restrict__ qcur,
-                                                               pcm_f4 *__restrict__ tpts, pcm_f4 *__restrict__ qpts) {
-    const int c = blockIdx.x / smax, s = blockIdx.x % smax;
-    const CloudRef<TIn> cr = cloud_ref(c, b, n, m, xyz1, xyz2);
-    const int S = grid_slices(cr.np);
-    if (s >= S) return;
-    const CloudGeom g = cloud_geom(part + (size_t)c * smax * 8, S, cr.np);
-    float px[kSliceK], py[kSliceK], pz[kSliceK];
-    const int p0 = s * kSlicePts;
-    load_slice(cr, p0, px, py, pz);
-    int *tc = tcur + (size_t)c * kMaxCells;
-    int *qc = qcur + (size_t)c * kMaxCells;
-    int cl[kSliceK], ts[kSliceK], qs[kSliceK];
-#pragma unroll
-    for (int k = 0; k < kSliceK; ++k) cl[k] = geom_cell(g, px[k], py[k], pz[k]);
-#pragma unroll
-    for (int k = 0; k < kSliceK; ++k) {
-        const bool v = p0 + k * kSliceT + (int)threadIdx.x < cr.np;
-        ts[k] = v ? atomicAdd(&tc[cl[k]], 1) : 0;
-        qs[k] = v ? atomicAdd(&qc[cl[k]], 1) : 0;
-    }
-#pragma unroll
-    for (int k = 0; k < kSliceK; ++k) {
-        const int i = p0 + k * kSliceT + (int)threadIdx.x;
-        if (i < cr.np) {
-            const pcm_f4 v = pcm_f4{px[k], py[k], pz[k], __int_as_float(i)};
-            tpts[cr.off + ts[k]] = v;
-            qpts[cr.off + qs[k]] = v;
-        }
     }
 }
 
@@ -597,28 +532,25 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void gr
         iout[oid] = (int32_t)(unsigned)best;
     }
     stamp(5);
+    if (stamps != nullptr && lane == 0) {  // placement: HW_ID and XCC_ID registers
+        stamps[8 * blk_all + 6] = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        stamps[8 * blk_all + 7] = __builtin_amdgcn_s_getreg((31 << 11) | 20);
+    }
 }
 
 inline size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct GridLayout {
-    size_t tpts, qpts, start, geo, part, counts, tcur, qcur, total;
-    int smax;
+    size_t tpts, qpts, start, geo, total;
 };
 inline GridLayout grid_layout(int b, int n, int m) {
     GridLayout L;
     const size_t pts = align256(16 * (size_t)b * ((size_t)n + m));
-    const size_t cells = align256(4 * (size_t)2 * b * kMaxCells);
-    L.smax = grid_slices(n > m ? n : m);
     L.tpts = 0;
     L.qpts = pts;
     L.start = 2 * pts;
     L.geo = L.start + align256(4 * (size_t)2 * b * (kMaxCells + 1));
-    L.part = L.geo + align256(4 * (size_t)2 * b * kGeo);
-    L.counts = L.part + align256(4 * (size_t)2 * b * (L.smax > 0 ? L.smax : 1) * 8);
-    L.tcur = L.counts + cells;
-    L.qcur = L.tcur + cells;
-    L.total = L.qcur + cells;
+    L.total = L.geo + align256(4 * (size_t)2 * b * kGeo);
     return L;
 }
 
@@ -649,22 +581,12 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
     pcm_f4 *qpts = (pcm_f4 *)(base + L.qpts);
     int *start = (int *)(base + L.start);
     float *geo = (float *)(base + L.geo);
-    float *part = (float *)(base + L.part);
-    int *counts = (int *)(base + L.counts), *tcur = (int *)(base + L.tcur), *qcur = (int *)(base + L.qcur);
     hipStream_t st = (hipStream_t)stream;
     // diagnostics layout: [waves][4] stats, then [waves][8] search stamps
     unsigned *sst = stats ? (unsigned *)(stats + 4 * waves) : nullptr;
-    if (build) {
-        const unsigned sg = (unsigned)(2 * b * L.smax);
-        hipLaunchKernelGGL(grid_bbox_kernel<TIn>, dim3(sg), dim3(kSliceT), 0, st, xyz1, xyz2, b, n, m, L.smax, part,
-                           counts);
-        hipLaunchKernelGGL(grid_count_kernel<TIn>, dim3(sg), dim3(kSliceT), 0, st, xyz1, xyz2, b, n, m, L.smax, part,
-                           counts);
-        hipLaunchKernelGGL(grid_scan_kernel, dim3(2 * b), dim3(kBuildT), 0, st, b, n, m, L.smax, part, counts, start,
-                           tcur, qcur, geo);
-        hipLaunchKernelGGL(grid_scatter_kernel<TIn>, dim3(sg), dim3(kSliceT), 0, st, xyz1, xyz2, b, n, m, L.smax,
-                           part, tcur, qcur, tpts, qpts);
-    }
+    if (build)
+        hipLaunchKernelGGL(grid_build_kernel<TIn>, dim3((unsigned)(2 * b * kSlabMax)), dim3(kSlabT), 0, st, xyz1,
+                           xyz2, b, n, m, tpts, qpts, start, geo);
     auto nnk = small_wg ? (screen ? grid_nn_kernel<TIn, true, 256> : grid_nn_kernel<TIn, false, 256>)
                         : (screen ? grid_nn_kernel<TIn, true, kNnT> : grid_nn_kernel<TIn, false, kNnT>);
     if (nn)

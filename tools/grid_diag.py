@@ -52,6 +52,18 @@ def main():
               f"; wave total {((ss[:, 5] - ss[:, 0]).float() * 0.01).median().item():.2f}; starts spread "
               f"{((ss[:, 0] - t0).float() * 0.01).max().item():.2f}, last end {((ss[:, 5] - t0).float() * 0.01).max().item():.2f}",
               flush=True)
+        st0 = ((ss[:, 0] - t0).float() * 0.01)
+        print("  wave start offsets p10/p50/p90/max (us): " +
+              "/".join(f"{torch.quantile(st0, qq).item():.2f}" for qq in (0.1, 0.5, 0.9, 1.0)), flush=True)
+        hw, xcc = ss[:, 6], ss[:, 7] & 0xf
+        cu = (hw >> 8) & 0xf
+        sh = (hw >> 12) & 1
+        se = (hw >> 13) & 7
+        unit = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+        ucnt = torch.bincount(unit, minlength=int(unit.max().item()) + 1)
+        print(f"  placement: {int((ucnt > 0).sum().item())} distinct (xcc, se, sh, cu) units, waves per unit "
+              f"min {int(ucnt[ucnt > 0].min().item())} max {int(ucnt.max().item())}; xcc counts "
+              f"{torch.bincount(xcc, minlength=8).tolist()}", flush=True)
         print(f"  candidates round 0 p50/p90/p99/max {[round(v) for v in torch.quantile(c0, q).tolist()]}, "
               f"all rounds {[round(v) for v in torch.quantile(ca, q).tolist()]}, mean {ca.mean().item():.0f}",
               flush=True)

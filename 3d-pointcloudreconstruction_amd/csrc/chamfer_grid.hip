@@ -368,7 +368,7 @@ __device__ __forceinline__ void scan_cands(const pcm_f4 *cand, int cnt, float qx
     scan_exact(cand, c8, cnt, qx, qy, qz, best);
 }
 
-template <typename TIn, bool kScreen, int NT>
+template <typename TIn, bool kScreen, int NT, bool kDma = true>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void grid_nn_kernel(const pcm_f4 *__restrict__ tpts,
                                                        const pcm_f4 *__restrict__ qpts, const int *__restrict__ start,
                                                        const float *__restrict__ geo, const TIn *__restrict__ xyz1,
@@ -480,11 +480,21 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void gr
 #pragma unroll
                     for (int bt = 0; bt < kB; ++bt) a[bt] = spre[a[bt] + step] <= v[bt] ? a[bt] + step : a[bt];
                 }
+                if constexpr (kDma) {
 #pragma unroll
-                for (int bt = 0; bt < kB; ++bt) {
-                    if (bt * 64 < take && bt * 64 + lane < take)
-                        __builtin_amdgcn_global_load_lds((const void *)(T + sst[a[bt]] + (v[bt] - spre[a[bt]])),
-                                                         (pcm_lds_void *)(cand + filled + bt * 64), 16, 0, 0);
+                    for (int bt = 0; bt < kB; ++bt) {
+                        if (bt * 64 < take && bt * 64 + lane < take)
+                            __builtin_amdgcn_global_load_lds((const void *)(T + sst[a[bt]] + (v[bt] - spre[a[bt]])),
+                                                             (pcm_lds_void *)(cand + filled + bt * 64), 16, 0, 0);
+                    }
+                } else {  // through registers: all loads, then all LDS writes
+                    pcm_f4 g[kB];
+#pragma unroll
+                    for (int bt = 0; bt < kB; ++bt)
+                        if (bt * 64 < take && bt * 64 + lane < take) g[bt] = T[sst[a[bt]] + (v[bt] - spre[a[bt]])];
+#pragma unroll
+                    for (int bt = 0; bt < kB; ++bt)
+                        if (bt * 64 < take && bt * 64 + lane < take) cand[filled + bt * 64 + lane] = g[bt];
                 }
                 filled += take;
                 w0 += take;
@@ -559,7 +569,8 @@ inline bool bad_dims(int b, int n, int m) { return b < 0 || n < 0 || m < 0; }
 template <typename TIn>
 int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *dist1, float *dist2, int32_t *idx1,
                 int32_t *idx2, void *workspace, size_t workspace_bytes, void *stream, bool screen = true,
-                int *stats = nullptr, bool build = true, bool nn = true, bool small_wg = false) {
+                int *stats = nullptr, bool build = true, bool nn = true, bool small_wg = false,
+                bool reg_gather = false) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2)))
@@ -589,6 +600,7 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
                            xyz2, b, n, m, tpts, qpts, start, geo);
     auto nnk = small_wg ? (screen ? grid_nn_kernel<TIn, true, 256> : grid_nn_kernel<TIn, false, 256>)
                         : (screen ? grid_nn_kernel<TIn, true, kNnT> : grid_nn_kernel<TIn, false, kNnT>);
+    if (reg_gather) nnk = small_wg ? grid_nn_kernel<TIn, true, 256, false> : grid_nn_kernel<TIn, true, kNnT, false>;
     if (nn)
         hipLaunchKernelGGL(nnk, dim3((unsigned)blocks), dim3(nt_wg), 0, st, tpts, qpts, start, geo, xyz1, xyz2, b, n,
                            m, nb1, nb2, dist1, dist2, idx1, idx2, stats, sst);
@@ -622,7 +634,8 @@ extern "C" int pcm_chamfer_forward_ws_f16(const uint16_t *xyz1, const uint16_t *
 // the grid path at any size (tests and A/B): mode bit 0 = binary16 clouds,
 // bit 1 = exact scan of every candidate instead of the screened scan, bit 2 =
 // the build kernel only, bit 3 = the search kernel only (on the workspace of a
-// previous call with the same clouds), bit 4 = 256-thread search workgroups; stats (nullable): per wave of the
+// previous call with the same clouds), bit 4 = 256-thread search workgroups,
+// bit 5 = candidate gather through registers instead of LDS-DMA; stats (nullable): per wave of the
 // search, {rounds, candidates of round 0, candidates of all rounds,
 // 2 * element + direction}, then s_memrealtime stamps: 8 per cloud of the
 // build, 8 per search wave
@@ -630,9 +643,10 @@ extern "C" int pcm_tune_chamfer_forward_grid(int mode, const void *xyz1, const v
                                              float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                              void *workspace, size_t workspace_bytes, void *stream, int *stats) {
     const bool screen = !(mode & 2), build = !(mode & 8), nn = !(mode & 4), small_wg = (mode & 16) != 0;
+    const bool reg_gather = (mode & 32) != 0;
     if (mode & 1)
         return launch_grid((const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace,
-                           workspace_bytes, stream, screen, stats, build, nn, small_wg);
+                           workspace_bytes, stream, screen, stats, build, nn, small_wg, reg_gather);
     return launch_grid((const float *)xyz1, (const float *)xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace,
-                       workspace_bytes, stream, screen, stats, build, nn, small_wg);
+                       workspace_bytes, stream, screen, stats, build, nn, small_wg, reg_gather);
 }

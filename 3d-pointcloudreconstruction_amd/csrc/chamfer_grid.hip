@@ -368,7 +368,79 @@ __device__ __forceinline__ void scan_cands(const pcm_f4 *cand, int cnt, float qx
     scan_exact(cand, c8, cnt, qx, qy, qz, best);
 }
 
-template <typename TIn, bool kScreen, int NT, bool kDma = true>
+// filtered window scan (kFilter): the csrc/chamfer_filt.hip screen on the
+// wave's window.  The raw candidates are transformed once per window into
+// pair-interleaved (u, w) = (-2 t', |t'|^2), t' = t - c (c = the wave's query
+// box centre): fu[2k] = {ux, ux', uy, uy'}, fu[2k + 1] = {uz, uz', w, w'} for
+// candidates 2k, 2k + 1, so each lane evaluates a = |t'|^2 - 2 q'.t' for two
+// candidates with three packed FMAs.  Per 8-candidate chunk the minimum; the
+// best chunk and the best of the other chunks (v_med3); proof as
+// chamfer_filt.hip step 2 (E = 16u (R + |q'|)^2, narrowed by the best
+// chunk's distance); then the exact keys of the best chunk, or of the whole
+// window when the proof fails (near-ties).
+constexpr float kGridU16 = 9.5367431640625e-07f;  // 16 u = 2^-20
+
+__device__ __forceinline__ void scan_filter(const pcm_f4 *__restrict__ cand, pcm_f4 *__restrict__ fu, int cnt,
+                                            const float (&c)[3], float qx, float qy, float qz,
+                                            unsigned long long &best) {
+    const int lane = threadIdx.x & 63;
+    const int npair = (cnt + 1) >> 1, c8 = (cnt + 7) & ~7;
+    float rt2 = 0.f;
+    for (int k = lane; k < (c8 >> 1); k += 64) {
+        float u[2][3], wv[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int j = 2 * k + h;
+            if (j < cnt) {
+                const pcm_f4 t = cand[j];
+                const float x = t.x - c[0], y = t.y - c[1], z = t.z - c[2];
+                wv[h] = __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
+                rt2 = fmaxf(rt2, wv[h]);
+                u[h][0] = -2.f * x;
+                u[h][1] = -2.f * y;
+                u[h][2] = -2.f * z;
+            } else {  // padding: a = +inf
+                wv[h] = PCM_INF;
+                u[h][0] = u[h][1] = u[h][2] = 0.f;
+            }
+        }
+        fu[2 * k] = pcm_f4{u[0][0], u[1][0], u[0][1], u[1][1]};
+        fu[2 * k + 1] = pcm_f4{u[0][2], u[1][2], wv[0], wv[1]};
+    }
+    (void)npair;
+    const float rmax2 = wave_maxf(rt2);
+    wave_lds_sync();
+    const float qxp = qx - c[0], qyp = qy - c[1], qzp = qz - c[2];
+    const pcm_f2 px = {qxp, qxp}, py = {qyp, qyp}, pz = {qzp, qzp};
+    float fb = PCM_INF, fs = PCM_INF;
+    int fc = 0;
+    for (int j = 0; j < c8; j += 8) {
+        float mn = PCM_INF;
+#pragma unroll
+        for (int pp = 0; pp < 4; ++pp) {
+            const pcm_f4 A = fu[j + 2 * pp], Bv = fu[j + 2 * pp + 1];
+            const pcm_f2 a = __builtin_elementwise_fma(
+                px, A.xy, __builtin_elementwise_fma(py, A.zw, __builtin_elementwise_fma(pz, Bv.xy, Bv.zw)));
+            mn = __builtin_fminf(__builtin_fminf(mn, a.x), a.y);
+        }
+        fs = __builtin_amdgcn_fmed3f(mn, fb, fs);
+        const bool lt = mn < fb;
+        fc = lt ? j : fc;
+        fb = lt ? mn : fb;
+    }
+    const float qn2 = __builtin_fmaf(qzp, qzp, __builtin_fmaf(qyp, qyp, qxp * qxp));
+    const float sq = __builtin_amdgcn_sqrtf(qn2);
+    const float rr = __builtin_amdgcn_sqrtf(rmax2) + sq;
+    const float eR = kGridU16 * (rr * rr) * 1.001f;
+    const float db = __builtin_fmaxf((fb + qn2) * 1.0001f + 2.f * eR, 0.f);
+    const float rq = 2.f * sq + __builtin_amdgcn_sqrtf(db);
+    const float e2 = 2.f * kGridU16 * __builtin_fminf(rr * rr, rq * rq) * 1.001f;
+    const bool proven = (fs - fb) > e2;  // false for NaN / +inf - +inf
+    if (proven) scan_exact(cand, fc, min(fc + 8, cnt), qx, qy, qz, best);
+    else scan_exact(cand, 0, cnt, qx, qy, qz, best);
+}
+
+template <typename TIn, bool kScreen, int NT, bool kDma = true, bool kFilter = false>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void grid_nn_kernel(const pcm_f4 *__restrict__ tpts,
                                                        const pcm_f4 *__restrict__ qpts, const int *__restrict__ start,
                                                        const float *__restrict__ geo, const TIn *__restrict__ xyz1,
@@ -377,7 +449,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void gr
                                                        int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
                                                        int *__restrict__ stats, unsigned *__restrict__ stamps) {
     constexpr int kW = NT / 64;
-    __shared__ pcm_f4 cand_all[kW][kWaveCap];
+    constexpr int kCap = kFilter ? kWaveCap / 2 : kWaveCap;  // candidates per window
+    __shared__ pcm_f4 cand_all[kW][kCap];
+    __shared__ pcm_f4 fu_all[kFilter ? kW : 1][kFilter ? kCap : 1];
     __shared__ int spre_all[kW][65];
     __shared__ int sst_all[kW][64];
 
@@ -421,12 +495,20 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void gr
     }
 
     pcm_f4 *cand = cand_all[w];
+    pcm_f4 *fu = fu_all[kFilter ? w : 0];
     int *spre = spre_all[w], *sst = sst_all[w];
     stamp(1);
     const float lo[3] = {gt[0], gt[1], gt[2]}, h = gt[3], inv = gt[4];
     const int G = (int)gt[6], margin = (int)gt[7];
     const float qc[3] = {q.x, q.y, q.z};
+    float cen[3];  // the filter's centre: midpoint of the wave's query box
+#pragma unroll
+    for (int a = 0; a < 3; ++a) cen[a] = 0.5f * (wave_minf(qc[a]) + wave_maxf(qc[a]));
     unsigned long long best = ~0ull;
+    auto scan_window = [&](int cnt) {
+        if constexpr (kFilter) scan_filter(cand, fu, cnt, cen, q.x, q.y, q.z, best);
+        else scan_cands<kScreen>(cand, cnt, q.x, q.y, q.z, best);
+    };
     bool pending = valid;
     int nround = 0, cand0 = 0, candall = 0;  // diagnostics (stats != nullptr)
     for (int round = 0; __ballot(pending) != 0; ++round) {
@@ -462,13 +544,13 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void gr
             if (lane == 63) spre[64] = inc;
             wave_lds_sync();
             for (int w0 = 0; w0 < tot;) {
-                const int take = min(tot - w0, kWaveCap - filled);
+                const int take = min(tot - w0, kCap - filled);
                 // candidate copies global -> LDS by LDS-DMA (lane l of a batch
                 // lands at slot base + l): every batch's loads in flight at once
                 // the row of slot v: the last row whose prefix is <= v (it
                 // holds v); the batches' searches interleaved (independent
                 // LDS chains)
-                constexpr int kB = kWaveCap / 64;
+                constexpr int kB = kCap / 64;
                 int v[kB], a[kB];
 #pragma unroll
                 for (int bt = 0; bt < kB; ++bt) {
@@ -498,9 +580,9 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void gr
                 }
                 filled += take;
                 w0 += take;
-                if (filled == kWaveCap) {
+                if (filled == kCap) {
                     wave_vm_sync();
-                    scan_cands<kScreen>(cand, kWaveCap, q.x, q.y, q.z, best);
+                    scan_window(kCap);
                     wave_lds_sync();
                     filled = 0;
                 }
@@ -509,7 +591,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void gr
         }
         wave_vm_sync();
         if (round == 0) stamp(3);
-        scan_cands<kScreen>(cand, filled, q.x, q.y, q.z, best);
+        scan_window(filled);
         wave_lds_sync();
         if (round == 0) stamp(4);
 
@@ -570,7 +652,7 @@ template <typename TIn>
 int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *dist1, float *dist2, int32_t *idx1,
                 int32_t *idx2, void *workspace, size_t workspace_bytes, void *stream, bool screen = true,
                 int *stats = nullptr, bool build = true, bool nn = true, bool small_wg = false,
-                bool reg_gather = false) {
+                bool reg_gather = false, bool filter = false) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2)))
@@ -601,6 +683,7 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
     auto nnk = small_wg ? (screen ? grid_nn_kernel<TIn, true, 256> : grid_nn_kernel<TIn, false, 256>)
                         : (screen ? grid_nn_kernel<TIn, true, kNnT> : grid_nn_kernel<TIn, false, kNnT>);
     if (reg_gather) nnk = small_wg ? grid_nn_kernel<TIn, true, 256, false> : grid_nn_kernel<TIn, true, kNnT, false>;
+    if (filter) nnk = small_wg ? grid_nn_kernel<TIn, true, 256, true, true> : grid_nn_kernel<TIn, true, kNnT, true, true>;
     if (nn)
         hipLaunchKernelGGL(nnk, dim3((unsigned)blocks), dim3(nt_wg), 0, st, tpts, qpts, start, geo, xyz1, xyz2, b, n,
                            m, nb1, nb2, dist1, dist2, idx1, idx2, stats, sst);
@@ -635,7 +718,8 @@ extern "C" int pcm_chamfer_forward_ws_f16(const uint16_t *xyz1, const uint16_t *
 // bit 1 = exact scan of every candidate instead of the screened scan, bit 2 =
 // the build kernel only, bit 3 = the search kernel only (on the workspace of a
 // previous call with the same clouds), bit 4 = 256-thread search workgroups,
-// bit 5 = candidate gather through registers instead of LDS-DMA; stats (nullable): per wave of the
+// bit 5 = candidate gather through registers instead of LDS-DMA, bit 6 = the
+// filtered window scan; stats (nullable): per wave of the
 // search, {rounds, candidates of round 0, candidates of all rounds,
 // 2 * element + direction}, then s_memrealtime stamps: 8 per cloud of the
 // build, 8 per search wave
@@ -643,10 +727,10 @@ extern "C" int pcm_tune_chamfer_forward_grid(int mode, const void *xyz1, const v
                                              float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                              void *workspace, size_t workspace_bytes, void *stream, int *stats) {
     const bool screen = !(mode & 2), build = !(mode & 8), nn = !(mode & 4), small_wg = (mode & 16) != 0;
-    const bool reg_gather = (mode & 32) != 0;
+    const bool reg_gather = (mode & 32) != 0, filter = (mode & 64) != 0;
     if (mode & 1)
         return launch_grid((const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace,
-                           workspace_bytes, stream, screen, stats, build, nn, small_wg, reg_gather);
+                           workspace_bytes, stream, screen, stats, build, nn, small_wg, reg_gather, filter);
     return launch_grid((const float *)xyz1, (const float *)xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace,
-                       workspace_bytes, stream, screen, stats, build, nn, small_wg, reg_gather);
+                       workspace_bytes, stream, screen, stats, build, nn, small_wg, reg_gather, filter);
 }

@@ -11,6 +11,10 @@
 #   rocprof    rocprofv3 --kernel-trace --stats of a short bench command
 #   abc        tools/ab_chamfer.py (same-box Chamfer variant A/B)
 #   abe        tools/ab_emd.py   (same-box EMD variant A/B)
+#   grid       GPU tests of the grid forward, tools/grid_diag.py, tools/ab_grid.py
+#   gridkt     rocprofv3 --kernel-trace --stats of tools/grid_diag.py
+#   pmc        tools/pmc_passes.sh (kernel trace of bench + one counter pass per group)
+#   stamps     tools/stamp_filt.py fused 7 11 (needs `make stamps`)
 set -o pipefail
 TAG=$1
 shift
@@ -36,6 +40,15 @@ for S in "$@"; do
                2> "$GRAFT_REPO_ROOT/$O/rocprof.err") ;;
     abc) timeout -k 10 600 python -u tools/ab_chamfer.py > "$O/ab_chamfer.txt" 2>&1 ;;
     abe) timeout -k 10 600 python -u tools/ab_emd.py > "$O/ab_emd.txt" 2>&1 ;;
+    grid) timeout -k 10 600 python -u -m pytest tests/test_chamfer_grid_gpu.py -m gpu -x -q --timeout 120 \
+               --timeout-method thread > "$O/pytest_grid.txt" 2>&1 &&
+          timeout -k 10 300 python -u tools/grid_diag.py > "$O/grid_diag.txt" 2>&1 &&
+          timeout -k 10 300 python -u tools/ab_grid.py > "$O/ab_grid.txt" 2>&1 ;;
+    gridkt) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/gridkt" -o grid --output-format csv \
+               -- python3 tools/grid_diag.py > "$O/gridkt.log" 2>&1 ;;
+    pmc) timeout -k 10 900 bash tools/pmc_passes.sh "$O/pmc" > "$O/pmc_passes.log" 2>&1 ;;
+    stamps) PCM_HIP_LIB=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_stamps.so timeout -k 10 300 \
+               python -u tools/stamp_filt.py fused 7 11 > "$O/stamps_fused.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac
     rc=$?

@@ -690,7 +690,13 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
     return pcm_launch_status();
 }
 
-inline bool grid_pays(int n, int m) { return n >= kGridMinPoints && m >= kGridMinPoints; }
+// the dense forward costs ~1.6e-13 s per (b n m) pair beyond ~20 us; the grid
+// ~25 us plus ~0.35 ns per point, but needs ~2k search waves to fill the chip
+// (tools/ab_grid.py, r04: B=2 N=M=4096 dense 29 us / grid 52 us; B=32 N=M=4096
+// 107 / 66 us; config 5 340 / 117 us)
+inline bool grid_pays(int b, int n, int m) {
+    return n >= kGridMinPoints && m >= kGridMinPoints && (double)b * n * m >= 268435456.0;
+}
 
 }  // namespace
 
@@ -702,14 +708,14 @@ extern "C" size_t pcm_chamfer_forward_ws_bytes(int b, int n, int m) {
 extern "C" int pcm_chamfer_forward_ws(const float *xyz1, const float *xyz2, int b, int n, int m, float *dist1,
                                       float *dist2, int32_t *idx1, int32_t *idx2, void *workspace,
                                       size_t workspace_bytes, void *stream) {
-    if (!grid_pays(n, m)) return pcm_chamfer_forward(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, stream);
+    if (!grid_pays(b, n, m)) return pcm_chamfer_forward(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, stream);
     return launch_grid(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace, workspace_bytes, stream);
 }
 
 extern "C" int pcm_chamfer_forward_ws_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, int n, int m,
                                           float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, void *workspace,
                                           size_t workspace_bytes, void *stream) {
-    if (!grid_pays(n, m)) return pcm_chamfer_forward_f16(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, stream);
+    if (!grid_pays(b, n, m)) return pcm_chamfer_forward_f16(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, stream);
     return launch_grid((const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace,
                        workspace_bytes, stream);
 }

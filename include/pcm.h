@@ -155,12 +155,12 @@ int pcm_chamfer_backward_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, 
 /*
  * Forward with a caller-owned workspace (extension): the same outputs as
  * pcm_chamfer_forward / pcm_chamfer_forward_f16, bit for bit.  When both
- * clouds hold >= 4096 points it sorts them into a uniform grid in the
- * workspace and scans only the cells around each block of queries (with a
- * proof that no farther point can win, else a full scan), which is what
- * large clouds (BASELINE config 5, N=M=16384) need; smaller clouds take the
- * dense kernels and ignore the workspace.  The workspace needs no
- * initialisation and holds no state between calls.
+ * clouds hold >= 4096 points and b*n*m >= 2^28 it sorts them into a uniform
+ * grid in the workspace and scans only the cells around each block of
+ * queries (with a proof that no farther point can win, else a wider scan),
+ * which is what large clouds (BASELINE config 5, N=M=16384) need; smaller
+ * problems take the dense kernels and ignore the workspace.  The workspace
+ * needs no initialisation and holds no state between calls.
  */
 size_t pcm_chamfer_forward_ws_bytes(int b, int n, int m);
 int pcm_chamfer_forward_ws(const float *xyz1, const float *xyz2, int b, int n, int m,

@@ -135,20 +135,21 @@ def test_grid_forward_empty_sides_untouched(cuda):
 
 
 def test_public_entry_routes_large_clouds_to_grid(cuda, oracle):
-    # pcm_chamfer_forward_ws at >= 4096 points is the grid path; equal to the dense entry
+    # pcm_chamfer_forward_ws at >= 4096 points and b n m >= 2^28 is the grid
+    # path (here 11 * 4100 * 6000); equal to the dense entry
     import pcm_hip
-    a, c = _clouds(40, 2, 4100, 6000)
+    a, c = _clouds(40, 11, 4100, 6000)
     x1, x2 = a.to(cuda), c.to(cuda)
     outs = []
     for fn in ("chamfer_forward", "dense"):
-        d1 = torch.empty(2, 4100, device=cuda)
-        d2 = torch.empty(2, 6000, device=cuda)
-        i1 = torch.empty(2, 4100, dtype=torch.int32, device=cuda)
-        i2 = torch.empty(2, 6000, dtype=torch.int32, device=cuda)
+        d1 = torch.empty(11, 4100, device=cuda)
+        d2 = torch.empty(11, 6000, device=cuda)
+        i1 = torch.empty(11, 4100, dtype=torch.int32, device=cuda)
+        i2 = torch.empty(11, 6000, dtype=torch.int32, device=cuda)
         if fn == "dense":
             P = pcm_hip._ptr
             assert pcm_hip.load_library().pcm_chamfer_forward(
-                P(x1), P(x2), 2, 4100, 6000, P(d1), P(d2), P(i1), P(i2), pcm_hip._stream(cuda)) == 0
+                P(x1), P(x2), 11, 4100, 6000, P(d1), P(d2), P(i1), P(i2), pcm_hip._stream(cuda)) == 0
         else:
             pcm_hip.chamfer_forward(x1, x2, d1, d2, i1, i2)
         torch.cuda.synchronize()

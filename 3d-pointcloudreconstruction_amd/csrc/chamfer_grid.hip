@@ -652,7 +652,7 @@ template <typename TIn>
 int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *dist1, float *dist2, int32_t *idx1,
                 int32_t *idx2, void *workspace, size_t workspace_bytes, void *stream, bool screen = true,
                 int *stats = nullptr, bool build = true, bool nn = true, bool small_wg = false,
-                bool reg_gather = false, bool filter = false) {
+                bool reg_gather = false, bool filter = true) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2)))
@@ -663,9 +663,14 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
     const int nb2 = n > 0 ? (m + 63) / 64 : 0;
     const long long waves = (long long)b * (nb1 + nb2);
     if (waves == 0) return PCM_OK;
-    // threads per search workgroup: 16 waves (fewer workgroups to dispatch)
-    // when that still fills every CU, else 4
-    if (waves < (long long)(kNnT / 64) * pcm_device_cus()) small_wg = true;
+    // threads per search workgroup: 16 waves (one workgroup per CU, fewer to
+    // dispatch) when the waves fill the chip in one round, else 4 (finer
+    // balance over several rounds; r04 grid_diag: config 5 45.5 vs 49.2 us,
+    // B=4 N=M=65536 147 vs 127 us)
+    {
+        const long long full = (long long)(kNnT / 64) * pcm_device_cus();
+        if (waves < full * 3 / 4 || waves > full) small_wg = true;
+    }
     const int nt_wg = small_wg ? 256 : kNnT;
     const long long blocks = (waves + nt_wg / 64 - 1) / (nt_wg / 64);
     if (blocks > 0x7fffffffLL || 2LL * b > 0x7fffffffLL) return PCM_ERR_UNSUPPORTED;
@@ -680,10 +685,12 @@ int launch_grid(const TIn *xyz1, const TIn *xyz2, int b, int n, int m, float *di
     if (build)
         hipLaunchKernelGGL(grid_build_kernel<TIn>, dim3((unsigned)(2 * b * kSlabMax)), dim3(kSlabT), 0, st, xyz1,
                            xyz2, b, n, m, tpts, qpts, start, geo);
-    auto nnk = small_wg ? (screen ? grid_nn_kernel<TIn, true, 256> : grid_nn_kernel<TIn, false, 256>)
-                        : (screen ? grid_nn_kernel<TIn, true, kNnT> : grid_nn_kernel<TIn, false, kNnT>);
+    // default: the filtered window scan (r04: config 5 search 42.4 us against
+    // 45.5 screened-exact, 55.8 with the register gather)
+    auto nnk = small_wg ? grid_nn_kernel<TIn, true, 256, true, true> : grid_nn_kernel<TIn, true, kNnT, true, true>;
+    if (!filter) nnk = small_wg ? (screen ? grid_nn_kernel<TIn, true, 256> : grid_nn_kernel<TIn, false, 256>)
+                                : (screen ? grid_nn_kernel<TIn, true, kNnT> : grid_nn_kernel<TIn, false, kNnT>);
     if (reg_gather) nnk = small_wg ? grid_nn_kernel<TIn, true, 256, false> : grid_nn_kernel<TIn, true, kNnT, false>;
-    if (filter) nnk = small_wg ? grid_nn_kernel<TIn, true, 256, true, true> : grid_nn_kernel<TIn, true, kNnT, true, true>;
     if (nn)
         hipLaunchKernelGGL(nnk, dim3((unsigned)blocks), dim3(nt_wg), 0, st, tpts, qpts, start, geo, xyz1, xyz2, b, n,
                            m, nb1, nb2, dist1, dist2, idx1, idx2, stats, sst);
@@ -724,8 +731,9 @@ extern "C" int pcm_chamfer_forward_ws_f16(const uint16_t *xyz1, const uint16_t *
 // bit 1 = exact scan of every candidate instead of the screened scan, bit 2 =
 // the build kernel only, bit 3 = the search kernel only (on the workspace of a
 // previous call with the same clouds), bit 4 = 256-thread search workgroups,
-// bit 5 = candidate gather through registers instead of LDS-DMA, bit 6 = the
-// filtered window scan; stats (nullable): per wave of the
+// bit 5 = candidate gather through registers instead of LDS-DMA (screened
+// scan), bit 6 = the screened exact-distance scan instead of the filtered
+// scan (the default); stats (nullable): per wave of the
 // search, {rounds, candidates of round 0, candidates of all rounds,
 // 2 * element + direction}, then s_memrealtime stamps: 8 per cloud of the
 // build, 8 per search wave
@@ -733,7 +741,7 @@ extern "C" int pcm_tune_chamfer_forward_grid(int mode, const void *xyz1, const v
                                              float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                              void *workspace, size_t workspace_bytes, void *stream, int *stats) {
     const bool screen = !(mode & 2), build = !(mode & 8), nn = !(mode & 4), small_wg = (mode & 16) != 0;
-    const bool reg_gather = (mode & 32) != 0, filter = (mode & 64) != 0;
+    const bool reg_gather = (mode & 32) != 0, filter = !(mode & 66);  // exact (2) or screened (64): no filter
     if (mode & 1)
         return launch_grid((const pcm_h *)xyz1, (const pcm_h *)xyz2, b, n, m, dist1, dist2, idx1, idx2, workspace,
                            workspace_bytes, stream, screen, stats, build, nn, small_wg, reg_gather, filter);

@@ -217,20 +217,20 @@ def chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:
             _stream(dev)), fn)
 
 
-def tune_chamfer_forward_grid(xyz1, xyz2, dist1, dist2, idx1, idx2, exact_scan=False, only=None,
-                              stats=None, workspace=None, small_wg=False, reg_gather=False,
-                              filter_scan=False) -> None:
-    """Internal: the grid forward at any size (float32 or float16 clouds);
-    exact_scan evaluates every candidate's key instead of the screened scan;
-    only = "build" / "search" runs one of its two kernels (search reuses the
+def tune_chamfer_forward_grid(xyz1, xyz2, dist1, dist2, idx1, idx2, scan="filter", only=None,
+                              stats=None, workspace=None, small_wg=False, reg_gather=False) -> None:
+    """Internal: the grid forward at any size (float32 or float16 clouds).
+    scan: "filter" (default: packed (u, w) screen + proof), "screened" (exact
+    distances, chunk minima) or "exact" (every candidate's key); only =
+    "build" / "search" runs one of its two kernels (search reuses the
     workspace of a previous call with the same clouds); stats: int32 device
-    tensor of 4 ints per search wave (csrc/chamfer_grid.hip)."""
+    tensor, 12 ints per search wave (csrc/chamfer_grid.hip)."""
     dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2)
     b, n, _ = xyz1.shape
     m = xyz2.shape[1]
     f16 = _cloud_kind(xyz1, xyz2) == "f16"
-    mode = int(f16) | (2 if exact_scan else 0) | {None: 0, "build": 4, "search": 8}[only] | (16 if small_wg else 0)
-    mode |= (32 if reg_gather else 0) | (64 if filter_scan else 0)
+    mode = int(f16) | {"filter": 0, "screened": 64, "exact": 2}[scan] | {None: 0, "build": 4, "search": 8}[only]
+    mode |= (16 if small_wg else 0) | (32 if reg_gather else 0)
     with torch.cuda.device(dev):
         ws = workspace if workspace is not None else forward_workspace(dev, b, n, m)
         _check(load_library().pcm_tune_chamfer_forward_grid(

@@ -16,14 +16,14 @@ from test_chamfer_gpu import _assert_fwd_equal, _clouds, _stress_clouds
 pytestmark = pytest.mark.gpu
 
 
-def _grid_fwd(a, c, dev, exact_scan=False, filter_scan=False):
+def _grid_fwd(a, c, dev, scan="filter"):
     import pcm_hip
     b, n, m = a.shape[0], a.shape[1], c.shape[1]
     d1 = torch.full((b, n), -1.0, device=dev)
     d2 = torch.full((b, m), -1.0, device=dev)
     i1 = torch.full((b, n), -1, dtype=torch.int32, device=dev)
     i2 = torch.full((b, m), -1, dtype=torch.int32, device=dev)
-    pcm_hip.tune_chamfer_forward_grid(a.to(dev), c.to(dev), d1, d2, i1, i2, exact_scan, filter_scan=filter_scan)
+    pcm_hip.tune_chamfer_forward_grid(a.to(dev), c.to(dev), d1, d2, i1, i2, scan=scan)
     torch.cuda.synchronize()
     return d1.cpu().numpy(), d2.cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()
 
@@ -54,7 +54,7 @@ def test_grid_forward_stress(cuda, oracle, kind, scan):
     # across chunks (the screened scan's exact-rescan path, the filter's
     # near-tie path); "offset" / "huge" stretch the filter's error bound
     a, c = _stress_clouds(kind, b=2, n=3000, m=2500)
-    _assert_fwd_equal(_grid_fwd(a, c, cuda, scan == "exact", scan == "filter"), _ref(oracle, a, c))
+    _assert_fwd_equal(_grid_fwd(a, c, cuda, scan), _ref(oracle, a, c))
 
 
 @pytest.mark.parametrize("b,n,m,seed,dist,f16", [
@@ -63,11 +63,13 @@ def test_grid_forward_stress(cuda, oracle, kind, scan):
     (1, 16384, 16384, 7, "uniform", False),
     (2, 8192, 8192, 31, "uniform", True),
 ])
-def test_grid_forward_filter_scan(cuda, oracle, b, n, m, seed, dist, f16):
+def test_grid_forward_screened_scan(cuda, oracle, b, n, m, seed, dist, f16):
+    # the non-default screened exact-distance scan (the filtered scan is the
+    # default and runs in every other test)
     a, c = _clouds(seed, b, n, m, dist)
     if f16:
         a, c = a.half(), c.half()
-    _assert_fwd_equal(_grid_fwd(a, c, cuda, filter_scan=True), _ref(oracle, a, c))
+    _assert_fwd_equal(_grid_fwd(a, c, cuda, "screened"), _ref(oracle, a, c))
 
 
 @pytest.mark.parametrize("kind", ["separated", "outliers", "clustered", "collapsed", "one_target", "plane"])

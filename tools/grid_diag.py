@@ -38,13 +38,13 @@ def main():
         t_sr = timed(lambda: pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, only="search", workspace=ws,
                                                                reg_gather=True))
         t_sf = timed(lambda: pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, only="search", workspace=ws,
-                                                               filter_scan=True))
+                                                               scan="screened"))
         t_s4 = timed(lambda: pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, only="search", workspace=ws,
                                                                small_wg=True))
         s = st.cpu()
         r, c0, ca = s[:, 0].float(), s[:, 1].float(), s[:, 2].float()
         q = torch.tensor([0.5, 0.9, 0.99, 1.0])
-        print(f"B={b} N={n} M={m} {str(dt)[6:]}: both {t_all:.1f} us, build {t_b:.1f} us, search {t_s:.1f} us (256-thread workgroups {t_s4:.1f}, register gather {t_sr:.1f}, filter scan {t_sf:.1f}); "
+        print(f"B={b} N={n} M={m} {str(dt)[6:]}: both {t_all:.1f} us, build {t_b:.1f} us, search {t_s:.1f} us (256-thread workgroups {t_s4:.1f}, register gather {t_sr:.1f}, screened scan {t_sf:.1f}); "
               f"{waves} waves", flush=True)
         print(f"  rounds: 1: {(r == 1).sum().item()}, 2: {(r == 2).sum().item()}, 3: {(r == 3).sum().item()}", flush=True)
         t0 = ss[:, 0].min()

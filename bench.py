@@ -55,7 +55,7 @@ import pcm_hip  # noqa: E402
 
 B, N, M = 32, 1024, 1024           # BASELINE config 2 (per GPU)
 EMD_B, EMD_N, EMD_EPS, EMD_ITERS = 16, 1024, 0.005, 50   # BASELINE config 3
-GRAPH_STEPS = 10                   # steps captured per hipGraph replay
+GRAPH_STEPS = 20                   # steps captured per hipGraph replay (the driver times 20)
 # the forward kernel instance the step launches at this size (csrc/chamfer.hip
 # default_fwd_variant) and the committed rocprofv3 counter summary it is looked
 # up in for roofline.traffic (tools/pmc_passes.sh + tools/pmc_summarize.py)

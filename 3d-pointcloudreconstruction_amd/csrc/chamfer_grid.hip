@@ -159,36 +159,31 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
         }
     };
 
-    // 1. bounding box (every workgroup of the cloud computes the same bits)
+    // 1. the grid's box from a strided sample of kSlabT points (every
+    // workgroup of the cloud computes the same bits).  Any box is exact: a
+    // point outside it is clamped into a boundary cell, which only moves it
+    // farther inside the cell range than it is, and the region proof holds
+    // for it as for every other point of that cell (search kernel).  The
+    // non-finite flag needs every point: pass 2.
     float mn[3] = {PCM_INF, PCM_INF, PCM_INF}, mx[3] = {-PCM_INF, -PCM_INF, -PCM_INF}, bad = 0.f;
-    for (int c0 = 0; c0 < np; c0 += kSlabK * kSlabT) {
-        load(c0);
-#pragma unroll
-        for (int k = 0; k < kSlabK; ++k) {
-            if (c0 + k * kSlabT + tid < np) {
-                bad = (pcm_finite(px[k]) && pcm_finite(py[k]) && pcm_finite(pz[k])) ? bad : 1.f;
-                mn[0] = fminf(mn[0], px[k]);
-                mx[0] = fmaxf(mx[0], px[k]);
-                mn[1] = fminf(mn[1], py[k]);
-                mx[1] = fmaxf(mx[1], py[k]);
-                mn[2] = fminf(mn[2], pz[k]);
-                mx[2] = fmaxf(mx[2], pz[k]);
-            }
-        }
+    {
+        const int i = np >= kSlabT ? (int)(((long long)tid * np) / kSlabT) : min(tid, np - 1);
+        const float x = pcm_ld(src + 3 * i), y = pcm_ld(src + 3 * i + 1), z = pcm_ld(src + 3 * i + 2);
+        mn[0] = mx[0] = x;
+        mn[1] = mx[1] = y;
+        mn[2] = mx[2] = z;
     }
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         mn[a] = wave_minf(mn[a]);
         mx[a] = wave_maxf(mx[a]);
     }
-    bad = wave_maxf(bad);
     if (lane == 0) {
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
             red[a][w] = mn[a];
             red[3 + a][w] = mx[a];
         }
-        red[6][w] = bad;
     }
     for (int i = tid; i < scells; i += kSlabT) {
         hT[i] = 0;
@@ -207,7 +202,6 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
         lo[a] = l;
         ext = fmaxf(ext, hgh - l);
     }
-    for (int i = 0; i < kW; ++i) bad = fmaxf(bad, red[6][i]);
     float h = ext / (float)G, inv = 1.f / h;
     if (!(h > 0.f) || !(inv < 1e30f)) {  // one point, coincident points or a tiny extent: unit cells
         h = 1.f;
@@ -224,6 +218,7 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
 #pragma unroll
         for (int k = 0; k < kSlabK; ++k) {
             const bool v = c0 + k * kSlabT + tid < np;
+            bad = (!v || (pcm_finite(px[k]) && pcm_finite(py[k]) && pcm_finite(pz[k]))) ? bad : 1.f;
             const int ix = cell_axis(px[k], lo[0], inv, G), iy = cell_axis(py[k], lo[1], inv, G),
                       iz = cell_axis(pz[k], lo[2], inv, G);
             const int sl = iz >> 2;
@@ -235,14 +230,17 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
             }
         }
     }
+    bad = wave_maxf(bad);
     if (lane == 0) {
 #pragma unroll
         for (int q = 0; q < kSlabMax; ++q)
             if (scnt[q]) atomicAdd(&sSlab[q], scnt[q]);
+        red[6][w] = bad;  // read after the next barrier only
     }
     __syncthreads();
     int soff = 0;
     for (int q = 0; q < slab; ++q) soff += sSlab[q];
+    for (int i = 0; i < kW; ++i) bad = fmaxf(bad, red[6][i]);
 
     // 3. exclusive scans of both histograms (wave w: rows [w R, w R + R) of
     // 64 bins, DPP scans with a carry; one barrier for the waves' offsets);

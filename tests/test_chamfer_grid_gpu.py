@@ -72,7 +72,8 @@ def test_grid_forward_screened_scan(cuda, oracle, b, n, m, seed, dist, f16):
     _assert_fwd_equal(_grid_fwd(a, c, cuda, "screened"), _ref(oracle, a, c))
 
 
-@pytest.mark.parametrize("kind", ["separated", "outliers", "clustered", "collapsed", "one_target", "plane"])
+@pytest.mark.parametrize("kind", ["separated", "outliers", "unsampled_outliers", "clustered", "collapsed", "one_target",
+                                  "plane"])
 def test_grid_forward_unproven_and_degenerate(cuda, oracle, kind):
     g = torch.Generator().manual_seed(21)
     a = torch.rand(2, 3000, 3, generator=g)
@@ -82,6 +83,10 @@ def test_grid_forward_unproven_and_degenerate(cuda, oracle, kind):
     elif kind == "outliers":     # a few far points stretch the grid: most cells empty
         a[:, :5] *= 1000.0
         c[:, :3] *= -1000.0
+    elif kind == "unsampled_outliers":  # far points the grid's box sample skips: clamped into boundary cells
+        a[:, 1] = torch.tensor([50.0, -40.0, 30.0])
+        a[:, 3] = torch.tensor([-60.0, 20.0, 90.0])
+        c[:, 1] = torch.tensor([-70.0, 80.0, -10.0])
     elif kind == "clustered":    # all points in a few tight blobs
         a = torch.floor(a * 3) / 3 + a * 1e-3
         c = torch.floor(c * 3) / 3 + c * 1e-3

@@ -1950,6 +1950,8 @@ const GradVariant kGradVariants[] = {
     // 12: 11 with the target tile staged and scanned in two halves
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, true>, 8, 4},
 };
+// (round 4, rejected: 7 and 11 with 16 waves -- four per SIMD, a 16-way
+// merge -- 15.9-16.2 us against 13.85 us, profiles/r04/chamfer_w16_r04n_ab.txt)
 constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
 // tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,
 // W=8 QPT=2 19.3 us, W=4 QPT=2 21.4 us; round 2: variant 1 (arrival counter

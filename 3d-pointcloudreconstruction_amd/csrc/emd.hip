@@ -98,6 +98,10 @@ constexpr int kDefaultWsplit = 1;       // most waves one miss's scan is split o
 // recomputes d from the LDS-staged clouds, the same pinned arithmetic.
 constexpr int kR = 256;
 constexpr float kResGrow = 6.f, kResShrink = 0.85f;
+#ifndef PCM_RES_FILL
+#define PCM_RES_FILL 0.9f
+#endif
+constexpr float kResFill = PCM_RES_FILL * kR;  // reserve size aimed at by the first shrink
 constexpr int kResTries = 16;           // 6 * 0.85^11 < 1: the radius reaches dK (<= 128 objects inside)
 
 typedef unsigned long long centry;   // low 32 bits: object id (-1 unused), high 32: s bits
@@ -395,7 +399,15 @@ __device__ __forceinline__ void scan_seed_res(float x1, float y1, float z1, cons
 #pragma unroll
             for (int i = 0; i < 4 * S; ++i) cnt += __popcll(__ballot(dd[i] < th));
             if (cnt <= kR) break;
-            th = fmaxf(dK, kResShrink * th);
+            // each count is 16 ballot -> s_bcnt1 round trips (most of the
+            // seed's SALU): the first miss jumps to the radius a locally
+            // uniform cloud (count ~ th^1.5) predicts for kResFill objects,
+            // later ones shrink geometrically (any th >= dK is valid: only
+            // the reserve's size, never a result, depends on it)
+            const float f = tr == 0 ? fminf(kResShrink, __builtin_amdgcn_exp2f(
+                                                            (2.f / 3.f) * __builtin_amdgcn_logf(kResFill / (float)cnt)))
+                                    : kResShrink;
+            th = fmaxf(dK, f * th);
         }
     }
     if (!ok || cnt > kR) {  // no reserve: the lane-top cache of scan_seed

@@ -99,7 +99,7 @@ constexpr int kDefaultWsplit = 1;       // most waves one miss's scan is split o
 constexpr int kR = 256;
 constexpr float kResGrow = 6.f, kResShrink = 0.85f;
 #ifndef PCM_RES_FILL
-#define PCM_RES_FILL 0.9f
+#define PCM_RES_FILL 0.8f
 #endif
 constexpr float kResFill = PCM_RES_FILL * kR;  // reserve size aimed at by the first shrink
 constexpr int kResTries = 16;           // 6 * 0.85^11 < 1: the radius reaches dK (<= 128 objects inside)

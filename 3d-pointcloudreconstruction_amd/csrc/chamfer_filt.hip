@@ -414,9 +414,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
 
     // ---- per-wave (best, second, chunk) to LDS (after the scan tile)
     {
-        float v = rt2;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v = __builtin_fmaxf(v, __shfl_xor(v, o, 64));
+        const float v = wave_max_dpp(rt2);  // rt2 >= 0, never NaN
         if (lane == 0) sRmax[wave] = v;
     }
     __syncthreads();  // every wave is done reading sU
@@ -909,9 +907,7 @@ __device__ __forceinline__ float filt_forward_mfma(const float *__restrict__ Q, 
         }
     }
     {
-        float v = rt2;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) v = __builtin_fmaxf(v, __shfl_xor(v, o, 64));
+        const float v = wave_max_dpp(rt2);  // rt2 >= 0, never NaN
         if (lane == 0) sRmax[wave] = v;
     }
     __syncthreads();

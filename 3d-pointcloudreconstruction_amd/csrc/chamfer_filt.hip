@@ -578,9 +578,10 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
 #pragma unroll
                 for (int qq = 1; qq < QPT; ++qq)
                     if ((s >> 6) == qq) { x = rx[qq]; y = ry[qq]; z = rz[qq]; }
-                x = __shfl(x, s & 63, 64);
-                y = __shfl(y, s & 63, 64);
-                z = __shfl(z, s & 63, 64);
+                // s is wave-uniform: v_readlane, not an LDS permute round trip
+                x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), s & 63));
+                y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y), s & 63));
+                z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z), s & 63));
                 float bd = PCM_INF;
                 int bk = 0x7fffffff;
                 for (int c0 = 0; c0 < nch; c0 += 64) {
@@ -1948,6 +1949,9 @@ const GradVariant kGradVariants[] = {
 };
 // (round 4, rejected: 7 and 11 with 16 waves -- four per SIMD, a 16-way
 // merge -- 15.9-16.2 us against 13.85 us, profiles/r04/chamfer_w16_r04n_ab.txt)
+// (round 4, rejected: 7 with the raw target rows parked in an LDS region of
+// their own while staging, one barrier after the scan instead of two -- 13.28
+// against 13.16 us, profiles/r04/chamfer_sept_r04q_ab.txt)
 constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]);
 // tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,
 // W=8 QPT=2 19.3 us, W=4 QPT=2 21.4 us; round 2: variant 1 (arrival counter

@@ -181,7 +181,8 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_kernel(
         sBest[wave][qq * 64 + lane] = best[qq];
         sChunk[wave][qq * 64 + lane] = bchunk[qq];
     }
-    const int any_nonfinite = __syncthreads_or(nonfinite ? 1 : 0);
+    __shared__ int sNF[W];
+    const int any_nonfinite = pcm_wg_or(nonfinite, sNF, W);
 
     float my_d = 0.f;  // dist of the query this thread finalises (kLoss sum)
     if (!any_nonfinite) {
@@ -490,7 +491,8 @@ __global__ __launch_bounds__(64 * W) void chamfer_fwd_sgpr_kernel(
             for (int r = 0; r < kChk; ++r) nonfinite |= !pcm_finite(v[r]);
         }
     }
-    const int any_nonfinite = __syncthreads_or(nonfinite ? 1 : 0);
+    __shared__ int sNF[W];
+    const int any_nonfinite = pcm_wg_or(nonfinite, sNF, W);
     unsigned tk = 0;  // arrival ticket (thread 0, kLoss)
 
     if (!any_nonfinite) {

@@ -437,7 +437,8 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         sSec[wave][qq * 64 + lane] = sec[qq];
         sChunk[wave][qq * 64 + lane] = bchunk[qq];
     }
-    const int any_nonfinite = __syncthreads_or(nonfinite ? 1 : 0);
+    __shared__ int sNF[W];
+    const int any_nonfinite = pcm_wg_or(nonfinite, sNF, W);
     PCM_STAMP(4);
 
     float my_d = 0.f;
@@ -979,7 +980,8 @@ __device__ __forceinline__ float filt_forward_mfma(const float *__restrict__ Q, 
             sPC[quarter][s] = bchunk[qt];
         }
     }
-    const int any_nonfinite = __syncthreads_or(nonfinite ? 1 : 0);
+    __shared__ int sNFm[8];
+    const int any_nonfinite = pcm_wg_or(nonfinite, sNFm, 8);
 
     float my_d = 0.f;
     if (!any_nonfinite) {
@@ -1388,6 +1390,7 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
     __shared__ int sOvf[QW];   // overflowed targets (range slot)
     __shared__ int sNOvf;
     __shared__ int sWcnt[kPerS][NW];
+    __shared__ int sWt[2][NW];  // the sweep's per-wave "still waiting" votes, by iteration parity
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
@@ -1414,7 +1417,7 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
 #pragma unroll
             for (int r = 0; r < kPerS; ++r) ready &= (unsigned)(gr[r] >> 32) == want;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (and the caller's LDS-DMA has landed)
-            const int waiting = __syncthreads_or(ready ? 0 : 1);
+            const int waiting = pcm_wg_or(!ready, sWt[spins & 1u], NW);
             if (!waiting && max_spins != 0u) break;
             if (spins >= max_spins) {
                 // uniform (every thread saw the same vote): the workgroups

@@ -1551,7 +1551,8 @@ __device__ void master_loop(const KArgs &a, const EmdWs &ws, int batch, int *sme
                     place_bid(st, u, ld_sc1(ws.rbid + base + i), ld_sc1(ws.rinc + base + i), n, sColl);
                     st.miss[i] = -1 - u;
                 }
-                if (__syncthreads_or(late ? 1 : 0)) {
+                __shared__ int sLate[kWaves];
+                if (pcm_wg_or(late, sLate, kWaves)) {
                     // region A rebuilt for the unanswered items, bids placed;
                     // no further jobs in this call (the word is a diagnostic)
                     H = 0;

@@ -54,6 +54,23 @@ __device__ __forceinline__ void pcm_wave_lexmin(float &d, int &k) {
     k = __builtin_amdgcn_readlane(k, 63);
 }
 
+// Workgroup-wide OR with ONE barrier, for a full workgroup in uniform control
+// flow.  HIP's __syncthreads_or re-reads the workgroup size from the dispatch
+// packet (an s_load that the next LDS wait also waits for) and takes three
+// barriers around an LDS atomic.  Here lane 0 of each wave writes the wave's
+// ballot to its own slot of `flags` (nwaves ints in LDS), one barrier, and
+// every thread ORs the slots.  A caller must not write `flags` again before
+// one more barrier has passed (a loop alternates two arrays by parity), so a
+// fast wave's next write never races a slow wave's read.
+__device__ __forceinline__ int pcm_wg_or(bool p, int *flags, int nwaves) {
+    const bool any = __ballot(p) != 0ull;
+    if ((threadIdx.x & 63) == 0) flags[threadIdx.x >> 6] = any ? 1 : 0;
+    __syncthreads();
+    int r = 0;
+    for (int w = 0; w < nwaves; ++w) r |= flags[w];
+    return r;
+}
+
 __device__ __forceinline__ bool pcm_finite(float v) {
     return __builtin_isfinite(v);
 }

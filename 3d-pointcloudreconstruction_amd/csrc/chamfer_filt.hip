@@ -119,7 +119,7 @@ struct FiltLds {
 template <int C>
 __device__ __forceinline__ int filt_slot(int p) {
     static_assert((C & (C - 1)) == 0, "chunk is a power of two");
-    return (p & ~(C - 1)) | ((p + p / C) & (C - 1));
+    return (p & ~(C - 1)) | ((p + (int)((unsigned)p / C)) & (C - 1));  // p >= 0
 }
 
 // forward outputs: plain stores, or write-through (sc1) when another
@@ -452,14 +452,16 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         const int part = tid / QW;
         bool proven = false;
         {
-            float vb[W], vs[W];
+            float vb[W], vs[W], vr[W];
             int vc[W];
 #pragma unroll
             for (int w = 0; w < W; ++w) {  // every load first, then branch-free selects
                 vb[w] = sBest[w][s];
                 vs[w] = sSec[w][s];
                 vc[w] = sChunk[w][s];
+                vr[w] = sRmax[w];  // with the rest, not one LDS round trip later
             }
+            __builtin_amdgcn_sched_barrier(0);
             float fb = vb[0], fs = vs[0];
             int fc = vc[0];
 #pragma unroll
@@ -469,9 +471,9 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                 fb = better ? vb[w] : fb;
                 fc = better ? vc[w] : fc;
             }
-            float rmax2 = sRmax[0];
+            float rmax2 = vr[0];
 #pragma unroll
-            for (int w = 1; w < W; ++w) rmax2 = __builtin_fmaxf(rmax2, sRmax[w]);
+            for (int w = 1; w < W; ++w) rmax2 = __builtin_fmaxf(rmax2, vr[w]);
             // this thread's register copy of query s is qq = s >> 6
             const int qsel = s >> 6;
             float qn2 = 0.f, x = rx[0], y = ry[0], z = rz[0];

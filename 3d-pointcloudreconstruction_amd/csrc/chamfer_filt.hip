@@ -1404,6 +1404,12 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
     int io = 0;
     int isr[kPerS];
     if constexpr (kGran) {
+        // the bucket counts are zeroed before the sweep: its vote barrier
+        // (every sweep takes at least one) orders them before the bucket
+        // atomics, so no barrier of their own (the caller's barrier after the
+        // forward has retired every use of these LDS bytes)
+        if (tid < QW) cnt[tid] = 0;
+        if (tid == 0) sNOvf = 0;
         // the argmins as data-tagged granules: sweep until every one this
         // thread needs carries the call's tag (bounded; the whole workgroup
         // decides together), re-reading only those not yet current
@@ -1467,9 +1473,11 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
 #pragma unroll
         for (int r = 0; r < kPerS; ++r) isr[r] = ld_sc1(Ioth + min(tid + r * NT, na - 1));
     }
-    if (tid < QW) cnt[tid] = 0;
-    if (tid == 0) sNOvf = 0;
-    __syncthreads();
+    if constexpr (!kGran) {
+        if (tid < QW) cnt[tid] = 0;
+        if (tid == 0) sNOvf = 0;
+        __syncthreads();
+    }
     PCM_STAMP2(3);
 #pragma unroll
     for (int r = 0; r < kPerS; ++r) {

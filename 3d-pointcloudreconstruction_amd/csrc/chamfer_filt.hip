@@ -130,23 +130,13 @@ __device__ __forceinline__ void out_st(Tv *p, Tv v) {
     else *p = v;
 }
 
-// Sum over the wave with DPP steps (row_shr 1, 2, 4, 8, then row_bcast 15
-// and 31; lane 63 holds the total), returned wave-uniform.  A lane the
-// pattern does not feed keeps its value; s_nop 1: two wait states before a
-// DPP read of the previous instruction's result (asm is not hazard-checked).
-#define PCM_DPP_SUM_STEPS(OP)                                                    \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"      \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"      \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"      \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"      \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"   \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+// Sum over the wave by DPP steps (pcm_common.h), returned wave-uniform.
 __device__ __forceinline__ float wave_sum_dpp(float v) {
-    asm volatile(PCM_DPP_SUM_STEPS("v_add_f32_dpp") : "+v"(v));
+    asm volatile(PCM_DPP_WAVE_STEPS("v_add_f32_dpp") : "+v"(v));
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 __device__ __forceinline__ int wave_sum_dpp(int v) {
-    asm volatile(PCM_DPP_SUM_STEPS("v_add_u32_dpp") : "+v"(v));
+    asm volatile(PCM_DPP_WAVE_STEPS("v_add_u32_dpp") : "+v"(v));
     return __builtin_amdgcn_readlane(v, 63);
 }
 
@@ -414,7 +404,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
 
     // ---- per-wave (best, second, chunk) to LDS (after the scan tile)
     {
-        const float v = wave_max_dpp(rt2);  // rt2 >= 0, never NaN
+        const float v = pcm_wave_max_f32(rt2);  // rt2 >= 0, never NaN
         if (lane == 0) sRmax[wave] = v;
     }
     __syncthreads();  // every wave is done reading sU
@@ -911,7 +901,7 @@ __device__ __forceinline__ float filt_forward_mfma(const float *__restrict__ Q, 
         }
     }
     {
-        const float v = wave_max_dpp(rt2);  // rt2 >= 0, never NaN
+        const float v = pcm_wave_max_f32(rt2);  // rt2 >= 0, never NaN
         if (lane == 0) sRmax[wave] = v;
     }
     __syncthreads();

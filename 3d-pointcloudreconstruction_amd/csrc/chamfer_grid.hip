@@ -534,7 +534,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) void gr
             }
             if (round == 0 && r0 == 0) stamp(2);
             const int inc = wave_incl_scan(cnt);
-            const int tot = __shfl(inc, 63, 64);
+            const int tot = __builtin_amdgcn_readlane(inc, 63);  // SGPR, not an LDS permute
             candall += tot;
             cand0 += round == 0 ? tot : 0;
             spre[lane] = inc - cnt;

@@ -6,26 +6,10 @@
 
 namespace pcm_loss {
 
-// Sum over a full wave, returned wave-uniform: DPP steps (row_shr 1, 2, 4, 8,
-// then row_bcast 15 and 31; lane 63 holds the total) -- VALU operand
-// modifiers, where __shfl_xor lowers to six dependent ds_bpermute round trips
-// on the way to the partial's publication.  A lane the pattern does not feed
-// keeps its value; s_nop 1: two wait states before a DPP read of the previous
-// instruction's result (asm is not hazard-checked).
-#define PCM_LOSS_DPP_STEPS(OP)                                                   \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"      \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"      \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"      \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"      \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"   \
-    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+// Sum over a full wave, returned wave-uniform, by DPP steps (pcm_common.h):
+// no LDS round trips on the way to the partial's publication.
 __device__ __forceinline__ float wave_sum(float v) {
-    asm volatile(PCM_LOSS_DPP_STEPS("v_add_f32_dpp") : "+v"(v));
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
-}
-// max over a full wave of values that are not NaN, returned wave-uniform
-__device__ __forceinline__ float wave_max_dpp(float v) {
-    asm volatile(PCM_LOSS_DPP_STEPS("v_max_f32_dpp") : "+v"(v));
+    asm volatile(PCM_DPP_WAVE_STEPS("v_add_f32_dpp") : "+v"(v));
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 

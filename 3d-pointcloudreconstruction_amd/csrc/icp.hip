@@ -99,8 +99,7 @@ __device__ __forceinline__ void block_sum(double (&v)[NV], double (*red)[W], dou
 template <int W>
 __device__ __forceinline__ float block_max(float v, float *red) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    v = pcm_wave_max_f32(v == v ? v : -PCM_INF);  // DPP steps; NaN counts as nothing, as fmaxf
     if (lane == 0) red[wave] = v;
     __syncthreads();
     float r = red[0];

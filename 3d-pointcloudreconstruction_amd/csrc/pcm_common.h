@@ -54,6 +54,25 @@ __device__ __forceinline__ void pcm_wave_lexmin(float &d, int &k) {
     k = __builtin_amdgcn_readlane(k, 63);
 }
 
+// Full-wave inclusive steps by DPP (row_shr 1, 2, 4, 8, then row_bcast 15 and
+// 31; lane 63 holds the wave's result): VALU operand modifiers, where
+// __shfl_xor lowers to six dependent ds_bpermute LDS round trips.  A lane the
+// pattern does not feed keeps its value (an idempotent or summing no-op);
+// s_nop 1: two wait states before a DPP read of the previous instruction's
+// result (asm is not hazard-checked).  Full wave, uniform control flow.
+#define PCM_DPP_WAVE_STEPS(OP)                                                   \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf\n\t"      \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"   \
+    "s_nop 1\n\t" OP " %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+// max over the wave of values that are not NaN, returned wave-uniform
+__device__ __forceinline__ float pcm_wave_max_f32(float v) {
+    asm volatile(PCM_DPP_WAVE_STEPS("v_max_f32_dpp") : "+v"(v));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
 // Workgroup-wide OR with ONE barrier, for a full workgroup in uniform control
 // flow.  HIP's __syncthreads_or re-reads the workgroup size from the dispatch
 // packet (an s_load that the next LDS wait also waits for) and takes three

@@ -622,12 +622,7 @@ __device__ inline int block_exclusive_scan(int v, int *wave_tot) {
     constexpr int NW = NT / 64;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    int x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
+    const int x = pcm_wave_incl_scan(v);  // DPP steps, no LDS round trips
     if (lane == 63) wave_tot[wave] = x;
     __syncthreads();
     int before = 0;

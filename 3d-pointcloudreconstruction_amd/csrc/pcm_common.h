@@ -73,6 +73,20 @@ __device__ __forceinline__ float pcm_wave_max_f32(float v) {
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// Inclusive prefix sum over a full wave by DPP (row_shr 1, 2, 4, 8 with
+// shifted-in lanes reading 0, then row_bcast 15 and 31 into the later rows):
+// six VALU steps, where a __shfl_up loop is six dependent ds_bpermute round
+// trips.  Full wave, uniform control flow.
+__device__ __forceinline__ int pcm_wave_incl_scan(int x) {
+    x += __builtin_amdgcn_update_dpp(0, x, 0x111, 0xf, 0xf, true);   // row_shr:1
+    x += __builtin_amdgcn_update_dpp(0, x, 0x112, 0xf, 0xf, true);   // row_shr:2
+    x += __builtin_amdgcn_update_dpp(0, x, 0x114, 0xf, 0xf, true);   // row_shr:4
+    x += __builtin_amdgcn_update_dpp(0, x, 0x118, 0xf, 0xf, true);   // row_shr:8
+    x += __builtin_amdgcn_update_dpp(0, x, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+    x += __builtin_amdgcn_update_dpp(0, x, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
+    return x;
+}
+
 // Workgroup-wide OR with ONE barrier, for a full workgroup in uniform control
 // flow.  HIP's __syncthreads_or re-reads the workgroup size from the dispatch
 // packet (an s_load that the next LDS wait also waits for) and takes three

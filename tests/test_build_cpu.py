@@ -32,8 +32,7 @@ def test_stamps_build_compiles(src):
 # dependent ds_bpermute round trips (PCM_DPP_WAVE_STEPS / pcm_wave_lexmin do
 # not).  Allowed: the rare near-tie / MFMA-variant / fallback paths listed.
 _SHFL_ALLOWED = {
-    "chamfer_filt.hip": 3,  # non-resident near-tie pass (3 coordinate broadcasts) ...
-    "chamfer.hip": 1,       # ... and the backward's exclusive scan (__shfl_up)
+    "chamfer_filt.hip": 3,  # non-resident near-tie pass (3 coordinate broadcasts)
 }
 _XOR_ALLOWED = {
     # non-resident near-tie pass (2 lines), the MFMA variant's lane merge (2)

@@ -1959,7 +1959,11 @@ constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]
 // tools/tune_chamfer.py (profiles/r01): B=32, N=M=1024 -- W=8 QPT=4 18.7 us,
 // W=8 QPT=2 19.3 us, W=4 QPT=2 21.4 us; round 2: variant 1 (arrival counter
 // hand-off) 16.25 us, variant 7 (the same forward, granule hand-off) 14.97 us
-constexpr int kDefaultGradVariant = 7;
+// end of round 4 (after the latency-chain changes): variant 11, the same
+// forward with the gradient phase reading the forward's own LDS instead of
+// copying both clouds in, 0.07-0.12 us faster than 7 in each of 4 same-box
+// runs (profiles/r04/variant_7_11_r04ze_ab.txt)
+constexpr int kDefaultGradVariant = 11;
 
 long long grad_blocks(const GradVariant &v, int b, int n, int m, int &nblk1, int &nblk2) {
     const int QW = 64 * v.qpt;

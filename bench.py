@@ -61,7 +61,7 @@ GRAPH_STEPS = 20                   # steps captured per hipGraph replay (the dri
 # up in for roofline.traffic (tools/pmc_passes.sh + tools/pmc_summarize.py)
 FWD_KERNEL = "chamfer_fwd_filt_kernel<float, 8, 4, 32, 2048, 3>"  # default fused-loss forward
 BWD_KERNEL = "chamfer_bwd_staged_kernel"
-FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false>"  # default variant 7 (granule hand-off)
+FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false>"  # default variant 11 (granule hand-off, local gradient data)
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r04", "pmc_summary.json")
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)

@@ -126,6 +126,9 @@ def load_library():
                                              vp]
     L.pcm_tune_num_chamfer_loss_grad_variants.restype = ci
     L.pcm_tune_num_chamfer_loss_grad_variants.argtypes = []
+    if hasattr(L, "pcm_tune_occupy"):  # absent from A/B builds of older sources
+        L.pcm_tune_occupy.restype = ci
+        L.pcm_tune_occupy.argtypes = [ci, ci, ci, ctypes.c_uint, vp]
     cd = ctypes.c_double
     L.pcm_icp.restype = ci
     L.pcm_icp.argtypes = [vp, vp, ci, ci, vp, ci, cd, vp, vp, vp, vp, cs, vp]
@@ -424,6 +427,15 @@ def chamfer_slow_paths(workspace, b: int, n: int, m: int) -> int:
     if r < 0:
         _check(r, "pcm_tune_chamfer_slow_paths")
     return r
+
+
+def tune_occupy(dev: torch.device, blocks: int, threads: int, lds_bytes: int, usec: int) -> None:
+    """Internal (tests): hold `blocks` workgroups of `threads` threads and
+    `lds_bytes` of LDS resident for `usec` microseconds on the current stream,
+    issuing only s_sleep -- another kernel sharing the CUs."""
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_tune_occupy(int(blocks), int(threads), int(lds_bytes), int(usec), _stream(dev)),
+               "pcm_tune_occupy")
 
 
 def tune_num_chamfer_loss_grad_variants() -> int:

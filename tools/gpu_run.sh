@@ -2,7 +2,8 @@
 # in order, each under its own time limit, output under gpurun_out/TAG/, and
 # stops at the first failing step (no GPU work after a fault or a time-out).
 # Steps:
-#   bench      python bench.py (the driver's default N=1 command)
+#   bench      python bench.py --gpus 1 --steps 20 --warmup 5 (the driver's exact N=1 command)
+#   benchlong  python bench.py (200 steps, 20 warmup)
 #   gloo2      bench.py --gpus 2 --dist-backend gloo (two ranks on one GPU)
 #   forcedist  bench.py --force-dist (one-rank RCCL: the captured per-step collective)
 #   pytest     pytest -m gpu (every GPU test)
@@ -24,7 +25,8 @@ export TMPDIR=/tmp
 for S in "$@"; do
     echo "[gpu_run] $S $(date +%T)"
     case "$S" in
-    bench) timeout -k 10 600 python -u bench.py > "$O/bench.json" 2> "$O/bench.err" ;;
+    bench) timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench.json" 2> "$O/bench.err" ;;
+    benchlong) timeout -k 10 600 python -u bench.py > "$O/benchlong.json" 2> "$O/benchlong.err" ;;
     gloo2) timeout -k 10 300 python -u bench.py --gpus 2 --dist-backend gloo --steps 20 --warmup 5 --no-cpu \
                --no-emd --no-dense --no-icp --no-ref-call > "$O/gloo2.json" 2> "$O/gloo2.err" ;;
     forcedist) timeout -k 10 300 python -u bench.py --force-dist --steps 50 --warmup 5 --no-cpu --no-emd \
@@ -36,7 +38,7 @@ for S in "$@"; do
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' \
                > "$O/smoke.txt" 2>&1 ;;
     rocprof) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" \
-               -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 200 --no-cpu > "$GRAFT_REPO_ROOT/$O/rocprof_bench.json" \
+               -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu > "$GRAFT_REPO_ROOT/$O/rocprof_bench.json" \
                2> "$GRAFT_REPO_ROOT/$O/rocprof.err") ;;
     abc) timeout -k 10 600 python -u tools/ab_chamfer.py > "$O/ab_chamfer.txt" 2>&1 ;;
     abe) timeout -k 10 600 python -u tools/ab_emd.py > "$O/ab_emd.txt" 2>&1 ;;

@@ -1582,6 +1582,23 @@ struct GradWs {
 };
 constexpr int kGradErrWord = 4;   // word of the first line: non-zero after the loss poll timed out (sticky)
 constexpr int kGradSlowWord = 5;  // diagnostics: gradient-phase waits that timed out and computed locally
+// Words 6 and 7 of the first line: the shape (n, m, granule format) and the
+// batch count the argmin granules were last written under, set by the loss
+// poller at the end of every granule-form call (0, 0 = a fresh zero-filled
+// workspace).  A granule only tells its call by its tag, and a tag comes back
+// after 2^32 calls (8-byte granules) or 2^21 (4-byte, variant 13): a position
+// that a call of another shape left alone for exactly that many calls would
+// pass for current.  So a call whose workspace was last used by another shape
+// or granule format trusts no granule: its gradient phase computes every
+// argmin it needs itself (the timeout path: exact, slow, once).
+constexpr int kGradShapeWord = 6;
+__host__ __device__ __forceinline__ unsigned grad_shape_word(int n, int m, unsigned fmt) {
+    return (fmt << 24) | ((unsigned)(n - 1) << 12) | (unsigned)(m - 1);  // n, m <= 1024; fmt 1 or 2: never 0
+}
+__device__ __forceinline__ bool grad_ws_trusted(const unsigned *hdr, int b, int n, int m, unsigned fmt) {
+    const unsigned sw = hdr[kGradShapeWord], sb = hdr[kGradShapeWord + 1];
+    return (sw == 0u && sb == 0u) || (sw == grad_shape_word(n, m, fmt) && sb == (unsigned)b);
+}
 // each batch element's arrival and departure counters on 128-byte lines of
 // their own: with all of them in one line, the 8 adds and the polls per
 // element queue behind every other element's at the memory side
@@ -1652,7 +1669,8 @@ __device__ __forceinline__ void poll_grad_loss(int b, int n, int m, const GradWs
 // granules, direction by the workgroup's slot, then one wave sum each) and
 // advances the epoch
 __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, int nblk1, const GradWs &ws,
-                                                  float *__restrict__ mean_out, unsigned max_spins) {
+                                                  float *__restrict__ mean_out, unsigned max_spins,
+                                                  unsigned shape_word) {
     if (threadIdx.x >= 64) return;
     const int lane = threadIdx.x;
     const unsigned epoch = ws.epoch[0] + 1u;
@@ -1684,9 +1702,13 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
         mean_out[0] = m1;
         mean_out[1] = m2;
         mean_out[2] = m1 + m2;
+        ws.epoch[kGradShapeWord] = shape_word;  // every workgroup read the old words before its partial
+        ws.epoch[kGradShapeWord + 1] = (unsigned)b;
         ws.epoch[0] = epoch;
     }
 }
+
+#include "chamfer_lgrid.h"
 
 template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false,
           bool kLocal = false, bool kSplit = false>
@@ -1720,7 +1742,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int nprod = (int)gridDim.x - 1;
     if ((int)blockIdx.x == nprod) {
         PCM_STAMP2(5);
-        if constexpr (kGran) poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, poll_spins);
+        if constexpr (kGran)
+            poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, poll_spins, grad_shape_word(n, m, 1u));
         else poll_grad_loss(b, n, m, ws, mean_out, poll_spins);
         PCM_STAMP2(6);
         return;
@@ -1741,6 +1764,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         // argmin as a {tag, idx} granule and the workgroup's partial as a
         // {tag, sum} granule; the gradient phase sweeps the granules it needs
         const unsigned long long tag = (unsigned long long)(ws.epoch[0] + 1u) << 32;
+        if (!grad_ws_trusted(ws.epoch, b, n, m, 1u)) max_spins = 0u;  // granules of another shape: recompute
         unsigned long long *G1 = ws.ig + (size_t)batch * n, *G2 = ws.ig + (size_t)b * n + (size_t)batch * m;
         const PreDma pre{garena, X1, 12 * n, garena + 12 * kGradCap, X2, 12 * m};
         __shared__ pcm_f4 sQown[kLocal ? QW : 1];  // kLocal: the range's points (the forward's queries)
@@ -1949,6 +1973,9 @@ const GradVariant kGradVariants[] = {
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true>, 8, 4},
     // 12: 11 with the target tile staged and scanned in two halves
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, true>, 8, 4},
+    // 13: LDS grid per workgroup (chamfer_lgrid.h): each group of 64 spatially
+    // sorted queries screens only the target cells around it
+    {chamfer_loss_grad_lgrid_kernel, 8, 4},
 };
 // (round 4, rejected: 7 and 11 with 16 waves -- four per SIMD, a 16-way
 // merge -- 15.9-16.2 us against 13.85 us, profiles/r04/chamfer_w16_r04n_ab.txt)

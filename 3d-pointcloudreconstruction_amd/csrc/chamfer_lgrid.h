@@ -1,0 +1,677 @@
+// chamfer_lgrid.h -- the one-launch Chamfer step (pcm_chamfer_loss_grad) with
+// an LDS grid per workgroup: variant 13 of chamfer_filt.hip's fused kernel.
+// Included by chamfer_filt.hip inside its anonymous namespace (it uses that
+// file's GradWs, scatter_sum, kGradSlots*, poll_grad_loss_wg, wave sums).
+//
+// Same results as every other variant, bit for bit: dist/idx of
+// NmDistanceKernel (chamfer3D.cu:12-134, pinned distance, lowest index), the
+// deterministic means, and the gradients of chamfer3D.cu:155-195 fed
+// graddist = w.  What changes is which pairs the forward evaluates.  The
+// all-pairs filtered scan of variants 7-12 spends ~6 of its ~10 us per
+// workgroup screening 256 queries against all 1024 targets; the nearest
+// neighbour of a 1024-point cloud lies within ~1/8 of its extent, so here
+//
+//   1. every workgroup loads BOTH clouds of its batch element (L2-hot after
+//      the first) and sorts them in LDS into a G^3 grid (G = 8 at 1024
+//      points, ~2 per cell) over the target cloud's bounding box: targets by
+//      row-major cell (a row of cells is one contiguous range), queries by
+//      serpentine 4^3-cell bricks (64 consecutive queries are spatially
+//      compact).  Counting sorts: LDS atomics, one block scan.  A query's
+//      rank inside its cell is its index order, so every workgroup of the
+//      element computes the same query order without talking to the others;
+//      workgroup r of a direction takes ranks [256 r, 256 r + 256).
+//   2. each group of 64 consecutive ranks (two waves) gathers the target
+//      cells of its query box widened by one cell -- ~300 of 1024 targets
+//      -- transformed for the filtered screen of chamfer_filt.hip around the
+//      group's own centre (smaller |q'|: a tighter error bound than a centre
+//      for 256 random queries), each wave its alternate 8-candidate chunks.
+//   3. proof as chamfer_filt.hip (E = 16u (R + |q'|)^2, narrowed by the best
+//      chunk's distance) -> exact (distance, index) minimum of the best chunk;
+//      then the region proof of chamfer_grid.hip: every target outside the
+//      window is at least `gap` away along some axis (cell rounding covered
+//      by a 2^-18 relative slack), so a best distance below gap^2 (1 - 2^-18)
+//      is the global one.  A query that fails either (near ties; nearest
+//      neighbour beyond the window, p ~ 2e-4 on uniform clouds) takes an
+//      exact scan of all targets by one wave.
+//   4. outputs by original index; argmins published as 4-byte granules
+//      {tag (21 bits) << 11 | idx} (one sc1 store each, half the bytes of the
+//      8-byte {tag, idx} granules of variants 7-12).
+//   5. the gradient phase of chamfer_filt.hip's range_grad on the
+//      workgroup's INDEX range [256 r, 256 r + 256) of the query cloud, with
+//      the other cloud read from the sorted LDS copy through an inverse map,
+//      and the loss partial recomputed from the argmins (the same pinned
+//      distance, the same fixed summation order as the other variants).
+//
+// Non-finite coordinates anywhere in the element: the reference's 512-point
+// tile scan per query of the index range (pcm_ref_nn_scan), as the dense
+// kernels do.  Degenerate clouds (one cell holding everything) stay exact;
+// they only cost more (windows of the whole cloud; O(cell^2) in-cell ranks).
+
+constexpr int kLgW = 8;              // waves per workgroup
+constexpr int kLgNT = 64 * kLgW;     // threads
+constexpr int kLgQW = 256;           // query ranks (forward) / index range (gradients) per workgroup
+constexpr int kLgCap = kGradCap;     // points per cloud (1024)
+constexpr int kLgCells = 512;        // G^3 cells at G = 8
+constexpr int kLgC = 8;              // screen chunk (candidates)
+constexpr int kLgPiece = 256;        // window entries a wave transforms per piece
+constexpr unsigned kLgTagBits = 21;  // granule: tag << 11 | idx (idx < 2048)
+constexpr unsigned kLgTagMask = (1u << kLgTagBits) - 1u;
+constexpr float kLgU16 = 9.5367431640625e-07f;  // 16 u = 2^-20 (chamfer_filt.hip's bound)
+constexpr int kLgArena = kLgW * kLgPiece * 16;   // 32 KB: query sort, then screen tiles, then gradient scratch
+static_assert(kLgPiece * 16 >= 3 * 64 * 4, "a wave's merge record fits its screen tile");
+static_assert(kLgArena >= kLgCap * 16, "the query sort fits the arena");
+static_assert(kLgArena >= 4 * kLgQW + 2 * kLgQW * kGradSlotsMax + 4 * kLgCap, "gradient scratch fits the arena");
+static_assert(kLgCap <= 2048, "11 index bits");
+
+// query order: bricks of 4^3 cells (2 x 2 x 2 of them at G <= 8) visited in a
+// serpentine order (consecutive bricks share a face), cells of a brick in
+// (z, y, x) order: 32 consecutive cells are two 4 x 4 layers
+__device__ __forceinline__ int lg_qkey(int x, int y, int z) {
+    const int bx = x >> 2, by = y >> 2, bz = z >> 2;
+    const int rr = bz * 2 + ((bz & 1) ? 1 - by : by);
+    const int bi = rr * 2 + ((rr & 1) ? 1 - bx : bx);
+    return (bi << 6) + (((z & 3) * 4 + (y & 3)) << 2) + (x & 3);
+}
+
+__device__ __forceinline__ int lg_cell(float v, float lo, float inv_h, int G) {
+    return (int)fminf(fmaxf((v - lo) * inv_h, 0.f), (float)(G - 1));  // NaN -> 0 (finite clouds only here)
+}
+
+// wave-uniform integer / float extrema by DPP steps (all lanes active)
+__device__ __forceinline__ int lg_wave_max_i(int v) {
+    asm volatile(PCM_DPP_WAVE_STEPS("v_max_i32_dpp") : "+v"(v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ int lg_wave_min_i(int v) {
+    asm volatile(PCM_DPP_WAVE_STEPS("v_min_i32_dpp") : "+v"(v));
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ float lg_wave_min_f(float v) {
+    asm volatile(PCM_DPP_WAVE_STEPS("v_min_f32_dpp") : "+v"(v));
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// 64-bit (distance bits, index) key: the lexicographic minimum is the
+// reference's (lowest index among equal minima); exact for d >= 0
+__device__ __forceinline__ unsigned long long lg_key(float d, int k) {
+    return ((unsigned long long)__float_as_uint(d) << 32) | (unsigned)k;
+}
+
+__global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_lgrid_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
+    float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
+    float *__restrict__ mean_out, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
+    GradWs ws, unsigned max_spins, unsigned poll_spins) {
+    __shared__ pcm_f4 sTs[kLgCap];           // targets sorted by cell: (x, y, z, index bits)
+    __shared__ uint16_t sInv[kLgCap];        // target index -> sorted position
+    __shared__ int sTSt[kLgCells + 1];       // target cell counts, then starts (row-major cells)
+    __shared__ int sQSt[kLgCells + 1];       // query cell counts, then starts (query-key order)
+    __shared__ pcm_f4 sQs[kLgQW];            // this workgroup's query ranks: (x, y, z, index bits)
+    __shared__ uint16_t sWpos[4][kLgCap];    // per group: window entry -> sorted target position
+    __shared__ int sRowPre[kLgW][65];        // per wave: window row prefix sums
+    __shared__ int sRowSt[kLgW][64];         // per wave: window row start positions
+    __shared__ float sBox[kLgW][8];          // bounding-box partials, non-finite votes
+    __shared__ int sTw[kLgW], sQw[kLgW];     // block scan: wave totals
+    __shared__ float sMR[kLgW];              // per wave: max |t'|^2 of its window part
+    __shared__ int sList[kLgQW];             // queries for an exact scan of all targets
+    __shared__ int sNList;
+    __shared__ float sRed[kLgW];
+    __shared__ int sOvf[kLgQW];
+    __shared__ int sNOvf;
+    __shared__ int sWcnt[2][kLgW];
+    __shared__ int sWt[2][kLgW];
+    __shared__ __attribute__((aligned(16))) unsigned char sArena[kLgArena];
+
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int nprod = (int)gridDim.x - 1;
+    if ((int)blockIdx.x == nprod) {  // the grid's last workgroup: the loss means
+        poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, poll_spins, grad_shape_word(n, m, 2u));
+        return;
+    }
+    const int per = nblk1 + nblk2;
+    const int bid = pcm_xcd_remap((int)blockIdx.x, nprod);
+    const int batch = bid / per;
+    const int r = bid - batch * per;
+    const bool first = r < nblk1;
+    const int q0 = (first ? r : r - nblk1) * kLgQW;  // rank range (forward) = index range (gradients)
+    const float *X1 = xyz1 + (size_t)batch * n * 3;
+    const float *X2 = xyz2 + (size_t)batch * m * 3;
+    const float *Qc = first ? X1 : X2;  // queries of this direction = the gradient range's cloud
+    const float *Tc = first ? X2 : X1;  // targets = the other cloud
+    const int nq = first ? n : m, nt = first ? m : n;
+    float *D = first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m;
+    int32_t *I = first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m;
+    unsigned *G1 = reinterpret_cast<unsigned *>(ws.ig) + (size_t)batch * n;
+    unsigned *G2 = reinterpret_cast<unsigned *>(ws.ig) + (size_t)b * n + (size_t)batch * m;
+    unsigned *Gq = first ? G1 : G2;        // this direction's argmin granules
+    const unsigned *Go = first ? G2 : G1;  // the other direction's
+    const unsigned epoch1 = ws.epoch[0] + 1u;
+    const unsigned tag = epoch1 & kLgTagMask;
+    const unsigned gtag = tag << 11;
+    // granules written under another shape or format are not trusted: the
+    // gradient phase then recomputes every argmin it needs (exact, slow)
+    if (!grad_ws_trusted(ws.epoch, b, n, m, 2u)) max_spins = 0u;
+
+    // ---- P0: both clouds into registers (2 points each per thread), the own
+    // gradient point, finiteness, the target bounding box
+    float tx[2], ty[2], tz[2], qx[2], qy[2], qz[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int pt = min(tid + k * kLgNT, nt - 1), pq = min(tid + k * kLgNT, nq - 1);
+        tx[k] = Tc[3 * pt];
+        ty[k] = Tc[3 * pt + 1];
+        tz[k] = Tc[3 * pt + 2];
+        qx[k] = Qc[3 * pq];
+        qy[k] = Qc[3 * pq + 1];
+        qz[k] = Qc[3 * pq + 2];
+    }
+    const int jown = q0 + tid;
+    const bool own = tid < kLgQW && jown < nq;
+    float sx, sy, sz;
+    {
+        const int j = min(jown, nq - 1);
+        sx = Qc[3 * j];
+        sy = Qc[3 * j + 1];
+        sz = Qc[3 * j + 2];
+    }
+    if (tid == 0) sNList = 0;
+    sTSt[tid] = 0;
+    sQSt[tid] = 0;
+    bool nonfinite = false;
+    float mn[3] = {PCM_INF, PCM_INF, PCM_INF}, mx[3] = {-PCM_INF, -PCM_INF, -PCM_INF};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        if (tid + k * kLgNT < nt) {
+            nonfinite |= !(pcm_finite(tx[k]) && pcm_finite(ty[k]) && pcm_finite(tz[k]));
+            mn[0] = fminf(mn[0], tx[k]);
+            mn[1] = fminf(mn[1], ty[k]);
+            mn[2] = fminf(mn[2], tz[k]);
+            mx[0] = fmaxf(mx[0], tx[k]);
+            mx[1] = fmaxf(mx[1], ty[k]);
+            mx[2] = fmaxf(mx[2], tz[k]);
+        }
+        if (tid + k * kLgNT < nq) nonfinite |= !(pcm_finite(qx[k]) && pcm_finite(qy[k]) && pcm_finite(qz[k]));
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float lo_a = lg_wave_min_f(mn[a]), hi_a = pcm_wave_max_f32(mx[a]);
+        if (lane == 0) {
+            sBox[wave][a] = lo_a;
+            sBox[wave][3 + a] = hi_a;
+        }
+    }
+    {
+        const bool anynf = __ballot(nonfinite) != 0ull;
+        if (lane == 0) sBox[wave][6] = anynf ? 1.f : 0.f;
+    }
+    __syncthreads();  // B1
+    float lo[3], hi[3];
+    bool nonf = false;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        lo[a] = sBox[0][a];
+        hi[a] = sBox[0][3 + a];
+    }
+#pragma unroll
+    for (int w = 0; w < kLgW; ++w) {
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = fminf(lo[a], sBox[w][a]);
+            hi[a] = fmaxf(hi[a], sBox[w][3 + a]);
+        }
+        nonf |= sBox[w][6] != 0.f;
+    }
+    const float g1w = __fmul_rn(w1, 2.f), g2w = __fmul_rn(w2, 2.f);
+    const float gs = first ? g1w : g2w, gh = first ? g2w : g1w;
+
+    if (nonf) {
+        // ---- non-finite coordinates: the reference's tile scan for the
+        // index range (its NaN placement depends on the 512-point tiles), and
+        // an unsorted target copy for the gradient phase
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int p = tid + k * kLgNT;
+            if (p < nt) {
+                sTs[p] = pcm_f4{tx[k], ty[k], tz[k], __int_as_float(p)};
+                sInv[p] = (uint16_t)p;
+            }
+        }
+        if (own) {
+            float d;
+            int k;
+            pcm_ref_nn_scan(sx, sy, sz, Tc, nt, d, k);
+            D[jown] = d;
+            I[jown] = k;
+            __hip_atomic_store(Gq + jown, gtag | (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+    } else {
+        // ---- P1: grid over the target cloud's box (cubic cells)
+        const float ext = fmaxf(hi[0] - lo[0], fmaxf(hi[1] - lo[1], hi[2] - lo[2]));
+        int G = (int)cbrtf((float)nt * 0.5f);
+        G = min(max(G, 1), 8);
+        if (!(ext > 0.f)) G = 1;
+        const float h = G > 1 ? ext / (float)G : fmaxf(ext, 1.f);
+        const float inv = 1.f / h;
+        int tkey[2], tslot[2], qkey[2], qslot[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int p = tid + k * kLgNT;
+            if (p < nt) {
+                const int cx = lg_cell(tx[k], lo[0], inv, G), cy = lg_cell(ty[k], lo[1], inv, G),
+                          cz = lg_cell(tz[k], lo[2], inv, G);
+                tkey[k] = (cz * G + cy) * G + cx;
+                tslot[k] = atomicAdd(&sTSt[tkey[k]], 1);
+            }
+            if (p < nq) {
+                const int cx = lg_cell(qx[k], lo[0], inv, G), cy = lg_cell(qy[k], lo[1], inv, G),
+                          cz = lg_cell(qz[k], lo[2], inv, G);
+                qkey[k] = lg_qkey(cx, cy, cz);
+                qslot[k] = atomicAdd(&sQSt[qkey[k]], 1);
+            }
+        }
+        __syncthreads();  // B2
+        {
+            // exclusive starts of both histograms (thread = cell)
+            const int ct = sTSt[tid], cq = sQSt[tid];
+            const int it = pcm_wave_incl_scan(ct), iq = pcm_wave_incl_scan(cq);
+            if (lane == 63) {
+                sTw[wave] = it;
+                sQw[wave] = iq;
+            }
+            __syncthreads();  // B3
+            int bt = 0, bq = 0;
+#pragma unroll
+            for (int w = 0; w < kLgW; ++w) {
+                bt += (w < wave) ? sTw[w] : 0;
+                bq += (w < wave) ? sQw[w] : 0;
+            }
+            sTSt[tid] = bt + it - ct;
+            sQSt[tid] = bq + iq - cq;
+            if (tid == kLgNT - 1) {
+                sTSt[kLgCells] = bt + it;
+                sQSt[kLgCells] = bq + iq;
+            }
+        }
+        __syncthreads();  // B4
+        pcm_f4 *sQsort = reinterpret_cast<pcm_f4 *>(sArena);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int p = tid + k * kLgNT;
+            if (p < nt) {
+                const int pos = sTSt[tkey[k]] + tslot[k];
+                sTs[pos] = pcm_f4{tx[k], ty[k], tz[k], __int_as_float(p)};
+                sInv[p] = (uint16_t)pos;
+            }
+            if (p < nq) sQsort[sQSt[qkey[k]] + qslot[k]] = pcm_f4{qx[k], qy[k], qz[k], __int_as_float(p)};
+        }
+        __syncthreads();  // B5
+        // ---- P2: query ranks: cell start + index order inside the cell (the
+        // same in every workgroup of the element); keep ranks [q0, q0 + 256)
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int pp = tid + k * kLgNT;
+            if (pp < nq) {
+                const pcm_f4 e = sQsort[pp];
+                const int idx = __float_as_int(e.w);
+                const int key = lg_qkey(lg_cell(e.x, lo[0], inv, G), lg_cell(e.y, lo[1], inv, G),
+                                        lg_cell(e.z, lo[2], inv, G));
+                const int c0 = sQSt[key], c1 = sQSt[key + 1];
+                int rk = c0;
+                for (int i = c0; i < c1; ++i) rk += __float_as_int(sQsort[i].w) < idx;
+                if (rk >= q0 && rk < q0 + kLgQW) sQs[rk - q0] = e;
+            }
+        }
+        __syncthreads();  // B6 (the arena's query sort is dead from here)
+
+        // ---- P3: groups of 64 ranks, two waves each
+        const int cnt_wg = min(kLgQW, nq - q0);
+        const int g = wave >> 1, half = wave & 1;
+        const int qi = 64 * g + lane;
+        const bool grp = 64 * g < cnt_wg;  // wave-uniform
+        const bool valid = qi < cnt_wg;
+        const pcm_f4 q = sQs[min(qi, cnt_wg - 1)];
+        int wl[3] = {0, 0, 0}, wh[3] = {0, 0, 0};
+        float cen[3] = {0.f, 0.f, 0.f};
+        int Wn = 0;
+        float *mrec = reinterpret_cast<float *>(sArena + wave * kLgPiece * 16);  // merge record (after the scan)
+        if (grp) {
+            const float qc[3] = {q.x, q.y, q.z};
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const int c = lg_cell(qc[a], lo[a], inv, G);
+                const int cmin = lg_wave_min_i(valid ? c : 1 << 20), cmax = lg_wave_max_i(valid ? c : -1);
+                wl[a] = max(cmin - 1, 0);
+                wh[a] = min(cmax + 1, G - 1);
+                cen[a] = 0.5f * (lg_wave_min_f(valid ? qc[a] : PCM_INF) + pcm_wave_max_f32(valid ? qc[a] : -PCM_INF));
+            }
+            const int ny = wh[1] - wl[1] + 1, nr = ny * (wh[2] - wl[2] + 1);  // <= 64 rows
+            int rs = 0, rc = 0;
+            if (lane < nr) {
+                const int base = ((wl[2] + lane / ny) * G + wl[1] + lane % ny) * G;
+                rs = sTSt[base + wl[0]];
+                rc = sTSt[base + wh[0] + 1] - rs;
+            }
+            const int inc = pcm_wave_incl_scan(rc);
+            Wn = __builtin_amdgcn_readlane(inc, 63);
+            sRowPre[wave][lane] = inc - rc;
+            sRowSt[wave][lane] = rs;
+            if (lane == 63) sRowPre[wave][64] = inc;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        }
+        // screen of this wave's chunks (c = half, half + 2, ...) in pieces
+        const float qxp = q.x - cen[0], qyp = q.y - cen[1], qzp = q.z - cen[2];
+        const pcm_f2 px = {qxp, qxp}, py = {qyp, qyp}, pz = {qzp, qzp};
+        float fb = PCM_INF, fs = PCM_INF, rt2 = 0.f;
+        int fc = 0;
+        const int nch = (Wn + kLgC - 1) / kLgC;
+        const int nmy = nch > half ? (nch - half + 1) >> 1 : 0;
+        pcm_f4 *Fw = reinterpret_cast<pcm_f4 *>(sArena + wave * kLgPiece * 16);
+        float *Ff = reinterpret_cast<float *>(Fw);
+        for (int i0 = 0; i0 < nmy; i0 += kLgPiece / kLgC) {
+            const int np = min(kLgPiece / kLgC, nmy - i0);
+#pragma unroll
+            for (int kk = 0; kk < kLgPiece / 64; ++kk) {
+                const int le = lane + 64 * kk;
+                if (le < np * kLgC) {
+                    const int c = 2 * (i0 + (le >> 3)) + half;
+                    const int e = kLgC * c + (le & 7);
+                    float ux = 0.f, uy = 0.f, uz = 0.f, wv = PCM_INF;  // padding: screened value +inf
+                    if (e < Wn) {
+                        int rr = 0;
+#pragma unroll
+                        for (int step = 32; step > 0; step >>= 1)
+                            rr = sRowPre[wave][rr + step] <= e ? rr + step : rr;
+                        const int pos = sRowSt[wave][rr] + (e - sRowPre[wave][rr]);
+                        const pcm_f4 t = sTs[pos];
+                        sWpos[g][e] = (uint16_t)pos;  // each entry belongs to one wave's chunks
+                        const float x = t.x - cen[0], y = t.y - cen[1], z = t.z - cen[2];
+                        wv = __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
+                        rt2 = fmaxf(rt2, wv);
+                        ux = -2.f * x;
+                        uy = -2.f * y;
+                        uz = -2.f * z;
+                    }
+                    // pair-interleaved: Fw[2k] = {ux, ux', uy, uy'}, Fw[2k+1] = {uz, uz', w, w'}
+                    const int k2 = le >> 1, hh = le & 1;
+                    Ff[8 * k2 + hh] = ux;
+                    Ff[8 * k2 + 2 + hh] = uy;
+                    Ff[8 * k2 + 4 + hh] = uz;
+                    Ff[8 * k2 + 6 + hh] = wv;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            for (int ci = 0; ci < np; ++ci) {
+                float mnv = PCM_INF;
+#pragma unroll
+                for (int pp = 0; pp < kLgC / 2; ++pp) {
+                    const pcm_f4 A = Fw[ci * kLgC + 2 * pp], Bv = Fw[ci * kLgC + 2 * pp + 1];
+                    const pcm_f2 a = __builtin_elementwise_fma(
+                        px, A.xy, __builtin_elementwise_fma(py, A.zw, __builtin_elementwise_fma(pz, Bv.xy, Bv.zw)));
+                    mnv = __builtin_fminf(__builtin_fminf(mnv, a.x), a.y);
+                }
+                fs = __builtin_amdgcn_fmed3f(mnv, fb, fs);
+                const bool lt = mnv < fb;
+                fc = lt ? 2 * (i0 + ci) + half : fc;
+                fb = lt ? mnv : fb;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next piece rewrites the tile
+        }
+        {
+            const float rm = pcm_wave_max_f32(rt2);
+            mrec[lane] = fb;
+            mrec[64 + lane] = fs;
+            mrec[128 + lane] = __int_as_float(fc);
+            if (lane == 0) sMR[wave] = rm;
+        }
+        __syncthreads();  // B7: both halves' screens are in
+        if (grp) {
+            const float *m0 = reinterpret_cast<const float *>(sArena + (2 * g) * kLgPiece * 16);
+            const float *m1 = reinterpret_cast<const float *>(sArena + (2 * g + 1) * kLgPiece * 16);
+            const float b0 = m0[lane], s0 = m0[64 + lane], b1 = m1[lane], s1 = m1[64 + lane];
+            const int c0 = __float_as_int(m0[128 + lane]), c1 = __float_as_int(m1[128 + lane]);
+            const bool better = (b1 < b0) | ((b1 == b0) & (c1 < c0));
+            const float mb = better ? b1 : b0;
+            const float ms = fminf(fminf(s0, s1), better ? b0 : b1);
+            const int mc = better ? c1 : c0;
+            const float rmax2 = fmaxf(sMR[2 * g], sMR[2 * g + 1]);
+            const float qn2 = __builtin_fmaf(qzp, qzp, __builtin_fmaf(qyp, qyp, qxp * qxp));
+            const float sq = __builtin_amdgcn_sqrtf(qn2);
+            const float rr = __builtin_amdgcn_sqrtf(rmax2) + sq;
+            const float eR = kLgU16 * (rr * rr) * 1.001f;
+            const float db = fmaxf((mb + qn2) * 1.0001f + 2.f * eR, 0.f);
+            const float rq = 2.f * sq + __builtin_amdgcn_sqrtf(db);
+            const float e2 = 2.f * kLgU16 * fminf(rr * rr, rq * rq) * 1.001f;
+            const bool proven = (ms - mb) > e2;  // false for NaN, inf - inf
+            unsigned long long best = ~0ull;
+            if (proven) {
+                // exact (distance, index) minimum of the best chunk; both
+                // waves of the group reach the same verdict
+#pragma unroll
+                for (int j = 0; j < kLgC; ++j) {
+                    const int e = min(kLgC * mc + j, Wn - 1);
+                    const pcm_f4 t = sTs[sWpos[g][e]];
+                    const unsigned long long kk = lg_key(pcm_sqd(t.x - q.x, t.y - q.y, t.z - q.z), __float_as_int(t.w));
+                    best = kk < best ? kk : best;
+                }
+            }
+            const float bd = __uint_as_float((unsigned)(best >> 32));
+            // region proof (chamfer_grid.hip): targets outside the window are
+            // >= gap away along some axis
+            float gap = PCM_INF;
+            const float qc[3] = {q.x, q.y, q.z};
+#pragma unroll
+            for (int a = 0; a < 3; ++a) {
+                const float tol = 0x1p-18f * (fabsf(lo[a]) + (float)G * h + fabsf(qc[a]));
+                if (wl[a] > 0) gap = fminf(gap, qc[a] - (lo[a] + (float)wl[a] * h) - tol);
+                if (wh[a] < G - 1) gap = fminf(gap, (lo[a] + (float)(wh[a] + 1) * h) - qc[a] - tol);
+            }
+            const bool done = proven && gap > 0.f && bd < gap * gap * (1.f - 0x1p-18f);
+            if (half == 0 && valid) {
+                if (done) {
+                    const int qid = __float_as_int(q.w);
+                    const int k = (int)(unsigned)best;
+                    D[qid] = bd;
+                    I[qid] = k;
+                    __hip_atomic_store(Gq + qid, gtag | (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    sList[atomicAdd(&sNList, 1)] = qi;
+                }
+            }
+        }
+        __syncthreads();  // B8
+        // ---- P4: listed queries (near ties, or a nearest neighbour beyond
+        // the window): one wave per query scans every target exactly
+        const int nl = sNList;
+        for (int e = wave; e < nl; e += kLgW) {
+            const int s = __builtin_amdgcn_readfirstlane(sList[e]);
+            const pcm_f4 qq = sQs[s];
+            unsigned long long best = ~0ull;
+            for (int k = lane; k < nt; k += 64) {
+                const pcm_f4 t = sTs[k];
+                const unsigned long long kk = lg_key(pcm_sqd(t.x - qq.x, t.y - qq.y, t.z - qq.z), __float_as_int(t.w));
+                best = kk < best ? kk : best;
+            }
+            // lanes with no candidate (nt < 64) enter as (+inf, INT_MAX); d >= 0,
+            // so the lexicographic (d, k) order is the 64-bit key's
+            float bd = best == ~0ull ? PCM_INF : __uint_as_float((unsigned)(best >> 32));
+            int bk = best == ~0ull ? 0x7fffffff : (int)(unsigned)best;
+            pcm_wave_lexmin(bd, bk);
+            if (lane == 0) {
+                const int qid = __float_as_int(qq.w);
+                D[qid] = bd;
+                I[qid] = bk;
+                __hip_atomic_store(Gq + qid, gtag | (unsigned)bk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+    }
+
+    // ---- P5: gradients of the index range [q0, q0 + 256) (range_grad's
+    // granule form; the other cloud from the sorted LDS copy)
+    constexpr int kPerS = (kLgCap + kLgNT - 1) / kLgNT;  // other-cloud sources per thread
+    int *cnt = reinterpret_cast<int *>(sArena);                        // [256]
+    uint16_t *tab = reinterpret_cast<uint16_t *>(cnt + kLgQW);         // [256][16]
+    int *lst = reinterpret_cast<int *>(tab + kLgQW * kGradSlotsMax);   // [nt] overflow source list
+    auto getA = [&](int i, float &x, float &y, float &z) {
+        const pcm_f4 t4 = sTs[sInv[i]];
+        x = t4.x;
+        y = t4.y;
+        z = t4.z;
+    };
+    if (tid < kLgQW) cnt[tid] = 0;
+    if (tid == 0) sNOvf = 0;
+    const int na = nt;
+    unsigned go = own ? __hip_atomic_load(Gq + jown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : gtag;
+    unsigned gr[kPerS];
+#pragma unroll
+    for (int k = 0; k < kPerS; ++k)
+        gr[k] = __hip_atomic_load(Go + min(tid + k * kLgNT, na - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (unsigned spins = 0;; ++spins) {
+        bool ready = (go >> 11) == tag;
+#pragma unroll
+        for (int k = 0; k < kPerS; ++k) ready &= (gr[k] >> 11) == tag;
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const int waiting = pcm_wg_or(!ready, sWt[spins & 1u], kLgW);
+        if (!waiting && max_spins != 0u) break;
+        if (spins >= max_spins) {
+            // the workgroups owing these argmins are not running (not resident,
+            // or slow), or the granules are not trusted: compute what is missing
+            // with the reference-exact scan (time, never correctness)
+            const bool all = max_spins == 0u;
+            if (own && (all || (go >> 11) != tag)) {
+                float d;
+                int k;
+                pcm_ref_nn_scan(sx, sy, sz, Tc, nt, d, k);
+                go = gtag | (unsigned)k;
+            }
+#pragma unroll
+            for (int k = 0; k < kPerS; ++k) {
+                const int i = min(tid + k * kLgNT, na - 1);
+                if (all || (gr[k] >> 11) != tag) {
+                    float d, x, y, z;
+                    int kk;
+                    getA(i, x, y, z);
+                    pcm_ref_nn_scan(x, y, z, Qc, nq, d, kk);
+                    gr[k] = gtag | (unsigned)kk;
+                }
+            }
+            if (tid == 0) atomicAdd(ws.epoch + kGradSlowWord, 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (own && (go >> 11) != tag) go = __hip_atomic_load(Gq + jown, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < kPerS; ++k)
+            if ((gr[k] >> 11) != tag)
+                gr[k] = __hip_atomic_load(Go + min(tid + k * kLgNT, na - 1), __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const int io = (int)(go & 2047u);
+    float ox = 0.f, oy = 0.f, oz = 0.f;
+    getA(own ? io : 0, ox, oy, oz);
+    {
+        // the loss partial of the index range: the forward's distance of each
+        // own point, recomputed (same pinned expression, same bits), summed in
+        // the other variants' fixed order
+        const float d = own ? pcm_sqd(ox - sx, oy - sy, oz - sz) : 0.f;
+        const float s = wave_sum(d);
+        if (lane == 0) sRed[wave] = s;
+    }
+#pragma unroll
+    for (int k = 0; k < kPerS; ++k) {
+        const int i = tid + k * kLgNT;
+        const int t = (int)(gr[k] & 2047u) - q0;
+        if (i < na && (unsigned)t < (unsigned)kLgQW) {
+            const int slot = atomicAdd(&cnt[t], 1);
+            if (slot < kGradSlotsMax) tab[t * kGradSlotsMax + slot] = (uint16_t)i;
+        }
+    }
+    __syncthreads();
+    if (tid == 0) {
+        float t = 0.f;
+        for (int w = 0; w < kLgW; ++w) t += sRed[w];
+        __hip_atomic_store(ws.wg + bid, ((unsigned long long)epoch1 << 32) | __float_as_uint(t), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    float *Gd = first ? grad1 + (size_t)batch * n * 3 : grad2 + (size_t)batch * m * 3;
+    if (own) {
+        const int c = cnt[tid];
+        if (c <= kGradSlotsMax) {
+            const float dx = __fmul_rn(gs, __fsub_rn(sx, ox));
+            const float dy = __fmul_rn(gs, __fsub_rn(sy, oy));
+            const float dz = __fmul_rn(gs, __fsub_rn(sz, oz));
+            float ax = 0.f, ay = 0.f, az = 0.f;
+            if (first) {  // cloud 1: direct term first (chamfer3D.cu:184), then the cloud-2 scatters
+                ax = __fadd_rn(ax, dx);
+                ay = __fadd_rn(ay, dy);
+                az = __fadd_rn(az, dz);
+            }
+            scatter_sum(ax, ay, az, sx, sy, sz, gh, getA, tab + tid * kGradSlotsMax, c);
+            if (!first) {  // cloud 2: cloud-1 scatters first (kernel 1 ran before kernel 2), then direct
+                ax = __fadd_rn(ax, dx);
+                ay = __fadd_rn(ay, dy);
+                az = __fadd_rn(az, dz);
+            }
+            Gd[3 * jown] = ax;
+            Gd[3 * jown + 1] = ay;
+            Gd[3 * jown + 2] = az;
+        } else {
+            sOvf[atomicAdd(&sNOvf, 1)] = tid;
+        }
+    }
+    __syncthreads();
+    // overflowed buckets (> 16 sources): ascending source list by ballots
+    const int nov = sNOvf;
+    for (int e = 0; e < nov; ++e) {
+        const int t = sOvf[e];
+        const int j = q0 + t;
+        unsigned long long bal[kPerS];
+#pragma unroll
+        for (int k = 0; k < kPerS; ++k) {
+            const int i = tid + k * kLgNT;
+            bal[k] = __ballot(i < na && (int)(gr[k] & 2047u) == j);
+            if (lane == 0) sWcnt[k][wave] = __popcll(bal[k]);
+        }
+        __syncthreads();
+        int total = 0;
+#pragma unroll
+        for (int k = 0; k < kPerS; ++k) {
+            int base = total;
+            for (int w = 0; w < kLgW; ++w) {
+                base += (w < wave) ? sWcnt[k][w] : 0;
+                total += sWcnt[k][w];
+            }
+            if ((bal[k] >> lane) & 1ull) lst[base + __popcll(bal[k] & ((1ull << lane) - 1ull))] = tid + k * kLgNT;
+        }
+        __syncthreads();
+        if (tid == t) {  // the target's own thread holds its point and argmin
+            const float dx = __fmul_rn(gs, __fsub_rn(sx, ox));
+            const float dy = __fmul_rn(gs, __fsub_rn(sy, oy));
+            const float dz = __fmul_rn(gs, __fsub_rn(sz, oz));
+            float ax = 0.f, ay = 0.f, az = 0.f;
+            if (first) {
+                ax = __fadd_rn(ax, dx);
+                ay = __fadd_rn(ay, dy);
+                az = __fadd_rn(az, dz);
+            }
+            for (int qq = 0; qq < total; ++qq) {
+                float tx2, ty2, tz2;
+                getA(lst[qq], tx2, ty2, tz2);
+                ax = __fadd_rn(ax, -__fmul_rn(gh, __fsub_rn(tx2, sx)));
+                ay = __fadd_rn(ay, -__fmul_rn(gh, __fsub_rn(ty2, sy)));
+                az = __fadd_rn(az, -__fmul_rn(gh, __fsub_rn(tz2, sz)));
+            }
+            if (!first) {
+                ax = __fadd_rn(ax, dx);
+                ay = __fadd_rn(ay, dy);
+                az = __fadd_rn(az, dz);
+            }
+            Gd[3 * j] = ax;
+            Gd[3 * j + 1] = ay;
+            Gd[3 * j + 2] = az;
+        }
+        __syncthreads();
+    }
+}

@@ -638,7 +638,7 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
     const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2, int b, int n, int m,
     const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
     const int32_t *__restrict__ idx2, TIn *__restrict__ grad1, TIn *__restrict__ grad2,
-    int nblk1, int nblk2) {
+    int nblk1, int nblk2, int lay1 = 0, int lay2 = 0) {
     __shared__ int sCnt[NT];
     __shared__ int sOff[NT + 1];
     __shared__ int sTmp[CAP];
@@ -683,6 +683,9 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
         no = n;
         direct_first = false;
     }
+    // layouts (pcm_common.h PcmLay): the gradient takes its cloud's layout
+    const PcmLay LS = direct_first ? pcm_lay(lay1, n) : pcm_lay(lay2, m);
+    const PcmLay LO = direct_first ? pcm_lay(lay2, m) : pcm_lay(lay1, n);
     const int t0 = blk * NT;
     const int T = min(NT, ns - t0);
 
@@ -691,14 +694,14 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
     const bool own = tid < T;
     float sx = 0.f, sy = 0.f, sz = 0.f, dir0 = 0.f, dir1 = 0.f, dir2 = 0.f;
     if (own) {
-        sx = pcm_ld(self + 3 * (size_t)i + 0);
-        sy = pcm_ld(self + 3 * (size_t)i + 1);
-        sz = pcm_ld(self + 3 * (size_t)i + 2);
+        sx = pcm_ld(self + pcm_at(LS, i, 0));
+        sy = pcm_ld(self + pcm_at(LS, i, 1));
+        sz = pcm_ld(self + pcm_at(LS, i, 2));
         const int k = ids[i];
         const float g = __fmul_rn(gds[i], 2.f);
-        dir0 = __fmul_rn(g, __fsub_rn(sx, pcm_ld(other + 3 * (size_t)k + 0)));
-        dir1 = __fmul_rn(g, __fsub_rn(sy, pcm_ld(other + 3 * (size_t)k + 1)));
-        dir2 = __fmul_rn(g, __fsub_rn(sz, pcm_ld(other + 3 * (size_t)k + 2)));
+        dir0 = __fmul_rn(g, __fsub_rn(sx, pcm_ld(other + pcm_at(LO, k, 0))));
+        dir1 = __fmul_rn(g, __fsub_rn(sy, pcm_ld(other + pcm_at(LO, k, 1))));
+        dir2 = __fmul_rn(g, __fsub_rn(sz, pcm_ld(other + pcm_at(LO, k, 2))));
     }
 
     // 1. histogram of the other direction's argmins that land in [t0, t0+T)
@@ -750,9 +753,9 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
     }
     auto scatter = [&](int j) {
         const float g = __fmul_rn(gdo[j], 2.f);
-        ax = __fadd_rn(ax, -__fmul_rn(g, __fsub_rn(pcm_ld(other + 3 * (size_t)j + 0), sx)));
-        ay = __fadd_rn(ay, -__fmul_rn(g, __fsub_rn(pcm_ld(other + 3 * (size_t)j + 1), sy)));
-        az = __fadd_rn(az, -__fmul_rn(g, __fsub_rn(pcm_ld(other + 3 * (size_t)j + 2), sz)));
+        ax = __fadd_rn(ax, -__fmul_rn(g, __fsub_rn(pcm_ld(other + pcm_at(LO, j, 0)), sx)));
+        ay = __fadd_rn(ay, -__fmul_rn(g, __fsub_rn(pcm_ld(other + pcm_at(LO, j, 1)), sy)));
+        az = __fadd_rn(az, -__fmul_rn(g, __fsub_rn(pcm_ld(other + pcm_at(LO, j, 2)), sz)));
     };
     if (fits) {
         const int lo = sOff[tid], hi = sOff[tid + 1];
@@ -768,9 +771,9 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
         ay = __fadd_rn(ay, dir1);
         az = __fadd_rn(az, dir2);
     }
-    pcm_st(grad + 3 * (size_t)i + 0, ax);
-    pcm_st(grad + 3 * (size_t)i + 1, ay);
-    pcm_st(grad + 3 * (size_t)i + 2, az);
+    pcm_st(grad + pcm_at(LS, i, 0), ax);
+    pcm_st(grad + pcm_at(LS, i, 1), ay);
+    pcm_st(grad + pcm_at(LS, i, 2), az);
 }
 
 // ---------------------------------------------------------------------------
@@ -933,7 +936,7 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
     const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
     const int32_t *__restrict__ idx2, float *__restrict__ grad1, float *__restrict__ grad2,
-    int nblk1, int nblk2) {
+    int nblk1, int nblk2, int lay1 = 0, int lay2 = 0) {
     __shared__ __attribute__((aligned(16))) float sO[3 * kBwdStageMax];   // other cloud, AoS
     __shared__ __attribute__((aligned(16))) float sG[kBwdStageMax];       // other graddist
     __shared__ __attribute__((aligned(16))) int sK[kBwdStageMax];         // other argmins
@@ -981,6 +984,11 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
     }
     const int t0 = blk * kBwdT;
     const int T = min(kBwdT, ns - t0);
+    // layouts (pcm_common.h PcmLay): either is the element's 12 no contiguous
+    // bytes, so the other cloud's LDS copy keeps its layout; the gradient
+    // takes its own cloud's
+    const PcmLay LS = direct_first ? pcm_lay(lay1, n) : pcm_lay(lay2, m);
+    const PcmLay LO = direct_first ? pcm_lay(lay2, m) : pcm_lay(lay1, n);
 
     pcm_dma_to_lds(sK, ido, 4 * no, wave, kBwdT / 64);
     pcm_dma_to_lds(sO, other, 12 * no, wave, kBwdT / 64);
@@ -991,9 +999,9 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
     float sx = 0.f, sy = 0.f, sz = 0.f, gself = 0.f;
     int kself = 0;
     if (own) {
-        sx = self[3 * (size_t)i + 0];
-        sy = self[3 * (size_t)i + 1];
-        sz = self[3 * (size_t)i + 2];
+        sx = self[pcm_at(LS, i, 0)];
+        sy = self[pcm_at(LS, i, 1)];
+        sz = self[pcm_at(LS, i, 2)];
         kself = ids[i];
         gself = gds[i];
     }
@@ -1033,9 +1041,9 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
 
     // 4. accumulate in the reference's kernel order
     const float g = __fmul_rn(gself, 2.f);
-    const float d0 = __fmul_rn(g, __fsub_rn(sx, sO[3 * kself + 0]));
-    const float d1 = __fmul_rn(g, __fsub_rn(sy, sO[3 * kself + 1]));
-    const float d2 = __fmul_rn(g, __fsub_rn(sz, sO[3 * kself + 2]));
+    const float d0 = __fmul_rn(g, __fsub_rn(sx, sO[pcm_at(LO, kself, 0)]));
+    const float d1 = __fmul_rn(g, __fsub_rn(sy, sO[pcm_at(LO, kself, 1)]));
+    const float d2 = __fmul_rn(g, __fsub_rn(sz, sO[pcm_at(LO, kself, 2)]));
     float ax = 0.f, ay = 0.f, az = 0.f;
     if (direct_first) {
         ax = __fadd_rn(ax, d0);
@@ -1045,18 +1053,18 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
     for (int p = sOff[tid]; p < sOff[tid + 1]; ++p) {
         const int j = sSrt[p];
         const float h = __fmul_rn(sG[j], 2.f);
-        ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(sO[3 * j + 0], sx)));
-        ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(sO[3 * j + 1], sy)));
-        az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(sO[3 * j + 2], sz)));
+        ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(sO[pcm_at(LO, j, 0)], sx)));
+        ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(sO[pcm_at(LO, j, 1)], sy)));
+        az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(sO[pcm_at(LO, j, 2)], sz)));
     }
     if (!direct_first) {
         ax = __fadd_rn(ax, d0);
         ay = __fadd_rn(ay, d1);
         az = __fadd_rn(az, d2);
     }
-    grad[3 * (size_t)i + 0] = ax;
-    grad[3 * (size_t)i + 1] = ay;
-    grad[3 * (size_t)i + 2] = az;
+    grad[pcm_at(LS, i, 0)] = ax;
+    grad[pcm_at(LS, i, 1)] = ay;
+    grad[pcm_at(LS, i, 2)] = az;
 }
 
 inline bool bad_dims(int b, int n, int m) { return b < 0 || n < 0 || m < 0; }
@@ -1237,7 +1245,7 @@ inline bool wide_bwd(int n, int m) { return n >= 4096 && m >= 4096; }
 
 int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
                const float *graddist1, const float *graddist2, const int32_t *idx1,
-               const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream) {
+               const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream, int lay1 = 0, int lay2 = 0) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     // Without targets a direction has no argmins; the reference would read
@@ -1252,7 +1260,13 @@ int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
     if (variant == 0 && n <= kBwdStageMax && m <= kBwdStageMax) {
         hipLaunchKernelGGL(chamfer_bwd_staged_kernel, dim3((unsigned)blocks), dim3(kBwdT), 0,
                            (hipStream_t)stream, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1,
-                           idx2, gradxyz1, gradxyz2, nblk1, nblk2);
+                           idx2, gradxyz1, gradxyz2, nblk1, nblk2, lay1, lay2);
+        return pcm_launch_status();
+    }
+    if (lay1 != 0 || lay2 != 0) {  // channel planes: the staged kernel's layout, else the global-memory kernel's
+        hipLaunchKernelGGL(chamfer_bwd_kernel<float>, dim3((unsigned)blocks), dim3(kBwdT), 0, (hipStream_t)stream,
+                           xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2, nblk1, nblk2,
+                           lay1, lay2);
         return pcm_launch_status();
     }
     const size_t lds = bwd_lds_bytes(n, m);
@@ -1286,6 +1300,15 @@ extern "C" int pcm_chamfer_backward(const float *xyz1, const float *xyz2, int b,
                                     float *gradxyz2, void *stream) {
     return launch_bwd(0, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2,
                       stream);
+}
+
+extern "C" int pcm_chamfer_backward_layout(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1,
+                                           int layout2, const float *graddist1, const float *graddist2,
+                                           const int32_t *idx1, const int32_t *idx2, float *gradxyz1,
+                                           float *gradxyz2, void *stream) {
+    if ((unsigned)layout1 > 1u || (unsigned)layout2 > 1u) return PCM_ERR_INVALID_ARG;
+    return launch_bwd(0, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2, stream, layout1,
+                      layout2);
 }
 
 extern "C" int pcm_tune_chamfer_backward(int variant, const float *xyz1, const float *xyz2, int b,

@@ -203,7 +203,8 @@ template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1, bool kSplit 
 __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const TIn *__restrict__ T, int nq, int nt, int qbase,
                               float *__restrict__ D, int32_t *__restrict__ I, unsigned char *arena,
                               unsigned long long *__restrict__ Gr = nullptr, unsigned long long tag = 0,
-                              const PreDma *pre = nullptr, pcm_f4 *qown = nullptr) {
+                              const PreDma *pre = nullptr, pcm_f4 *qown = nullptr, PcmLay LQ = PcmLay{3, 1},
+                              PcmLay LT = PcmLay{3, 1}) {
     static_assert(C % 4 == 0 && TILE % C == 0, "tile must hold whole chunks of 4-candidate groups");
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
@@ -247,9 +248,9 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         // the first tile's -- is in flight at once (a branch around a load makes
         // hipcc wait for it inside the branch)
         const int qc = min(qbase + qq * 64 + lane, nq - 1);
-        rx[qq] = pcm_ld(Q + 3 * (size_t)qc + 0);
-        ry[qq] = pcm_ld(Q + 3 * (size_t)qc + 1);
-        rz[qq] = pcm_ld(Q + 3 * (size_t)qc + 2);
+        rx[qq] = pcm_ld(Q + pcm_at(LQ, qc, 0));
+        ry[qq] = pcm_ld(Q + pcm_at(LQ, qc, 1));
+        rz[qq] = pcm_ld(Q + pcm_at(LQ, qc, 2));
     }
 
     float tv[kPer][3];
@@ -259,7 +260,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         for (int r = 0; r < kPer; ++r) {
             const int p = min(tid + r * NT, last);
 #pragma unroll
-            for (int d = 0; d < 3; ++d) tv[r][d] = pcm_ld(T + 3 * (size_t)(t0 + p) + d);
+            for (int d = 0; d < 3; ++d) tv[r][d] = pcm_ld(T + pcm_at(LT, t0 + p, d));
         }
     };
     load_tile(0);
@@ -513,9 +514,9 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
 #pragma unroll
                         for (int k = 0; k < CP; ++k) {
                             const int kk = min(k0 + k, nt - 1);
-                            tx[k] = pcm_ld(T + 3 * (size_t)kk);
-                            ty[k] = pcm_ld(T + 3 * (size_t)kk + 1);
-                            tz[k] = pcm_ld(T + 3 * (size_t)kk + 2);
+                            tx[k] = pcm_ld(T + pcm_at(LT, kk, 0));
+                            ty[k] = pcm_ld(T + pcm_at(LT, kk, 1));
+                            tz[k] = pcm_ld(T + pcm_at(LT, kk, 2));
                         }
                     }
 #pragma unroll
@@ -643,9 +644,9 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
                         const int k = min(k0 + u * NT, nt - 1);
-                        tx[u] = pcm_ld(T + 3 * (size_t)k);
-                        ty[u] = pcm_ld(T + 3 * (size_t)k + 1);
-                        tz[u] = pcm_ld(T + 3 * (size_t)k + 2);
+                        tx[u] = pcm_ld(T + pcm_at(LT, k, 0));
+                        ty[u] = pcm_ld(T + pcm_at(LT, k, 1));
+                        tz[u] = pcm_ld(T + pcm_at(LT, k, 2));
                     }
 #pragma unroll
                     for (int u = 0; u < U; ++u)
@@ -711,8 +712,8 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             if (qi >= nq) continue;
             float d;
             int idx;
-            pcm_ref_nn_scan(pcm_ld(Q + 3 * (size_t)qi + 0), pcm_ld(Q + 3 * (size_t)qi + 1),
-                            pcm_ld(Q + 3 * (size_t)qi + 2), T, nt, d, idx);
+            pcm_ref_nn_scan(pcm_ld(Q + pcm_at(LQ, qi, 0)), pcm_ld(Q + pcm_at(LQ, qi, 1)),
+                            pcm_ld(Q + pcm_at(LQ, qi, 2)), T, nt, d, idx, LT);
             my_d = d;
             out_st<kSc1>(D + qi, d);
             out_st<kSc1>(I + qi, (int32_t)idx);
@@ -1204,6 +1205,36 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     if (threadIdx.x == 0 && blockIdx.x < kStampSlots)
         g_pcm_stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime();
 #endif
+}
+
+// The filtered forward on clouds of either layout (pcm_common.h PcmLay):
+// lay1 / lay2 = 1 when that cloud is [b, 3, n] channel planes -- the
+// generator's B x 3 x N output, which train.py:163 hands to the loss as a
+// transposed view; the reference's wrapper copies it to rows first
+// (dist_chamfer_3D.py:79-80), this reads it in place.  Same results as
+// pcm_chamfer_forward on the rows, bit for bit (the same arithmetic on the
+// same values).
+template <int W, int QPT, int C, int TILE>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_fwd_filt_lay_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
+    float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1,
+    int32_t *__restrict__ idx2, int nblk1, int nblk2, int lay1, int lay2) {
+    constexpr int QW = 64 * QPT;
+    const int bid = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const bool first = bid < b * nblk1;
+    const int r = first ? bid : bid - b * nblk1;
+    const int nbk = first ? nblk1 : nblk2;
+    const int batch = r / nbk, blk = r - batch * nbk;
+    const float *X1 = xyz1 + (size_t)batch * n * 3, *X2 = xyz2 + (size_t)batch * m * 3;
+    const PcmLay L1 = pcm_lay(lay1, n), L2 = pcm_lay(lay2, m);
+    if (first)
+        filt_forward<float, W, QPT, C, TILE, false>(X1, X2, n, m, blk * QW, dist1 + (size_t)batch * n,
+                                                   idx1 + (size_t)batch * n, lds_arena<FiltLds<W, QPT, TILE>::kBytes>(),
+                                                   nullptr, 0, nullptr, nullptr, L1, L2);
+    else
+        filt_forward<float, W, QPT, C, TILE, false>(X2, X1, m, n, blk * QW, dist2 + (size_t)batch * m,
+                                                   idx2 + (size_t)batch * m, lds_arena<FiltLds<W, QPT, TILE>::kBytes>(),
+                                                   nullptr, 0, nullptr, nullptr, L2, L1);
 }
 
 // ---------------------------------------------------------------------------
@@ -2066,6 +2097,26 @@ extern "C" int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const 
 }
 
 extern "C" int pcm_tune_num_chamfer_loss_grad_variants(void) { return kNumGradVariants; }
+
+extern "C" int pcm_chamfer_forward_layout(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1,
+                                          int layout2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                                          void *stream) {
+    if (b < 0 || n < 0 || m < 0 || (unsigned)layout1 > 1u || (unsigned)layout2 > 1u) return PCM_ERR_INVALID_ARG;
+    if (layout1 == 0 && layout2 == 0) return pcm_chamfer_forward(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, stream);
+    if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
+    if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2))) return PCM_ERR_INVALID_ARG;
+    // the default filtered variant's geometry (chamfer.hip default_fwd_variant: W 8, QPT 4, C 32)
+    constexpr int W = 8, QPT = 4, QW = 64 * QPT;
+    const int nblk1 = m > 0 ? (n + QW - 1) / QW : 0;  // a direction without targets keeps its outputs
+    const int nblk2 = n > 0 ? (m + QW - 1) / QW : 0;
+    const long long blocks = (long long)b * (nblk1 + nblk2);
+    if (blocks > 0x7ffffffeLL) return PCM_ERR_UNSUPPORTED;
+    if (blocks == 0) return PCM_OK;
+    hipLaunchKernelGGL((chamfer_fwd_filt_lay_kernel<W, QPT, 32, 2048>), dim3((unsigned)blocks), dim3(64 * W), 0,
+                       (hipStream_t)stream, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nblk1, nblk2, layout1,
+                       layout2);
+    return pcm_launch_status();
+}
 
 // the default variant with given bounds on the gradient-phase waits
 // (wait_spins; 0: every argmin recomputed locally, exact results) and on the

@@ -117,13 +117,26 @@ __device__ __forceinline__ float pcm_ld(const pcm_h *p) { return (float)*p; }
 __device__ __forceinline__ void pcm_st(float *p, float v) { *p = v; }
 __device__ __forceinline__ void pcm_st(pcm_h *p, float v) { *p = (pcm_h)v; }  // round to nearest even
 
+// Layout of one batch element's cloud in global memory: coordinate d of point
+// k at base[k * ps + d * ds].  Rows [n, 3] (ps 3, ds 1) are what the
+// reference's wrapper hands over (dist_chamfer_3D.py:79-80 .contiguous());
+// planes [3, n] (ps 1, ds n) are the generator's B x 3 x N output that
+// train.py:163 passes as a transposed view (extension: no copy).  The batch
+// stride is 3 n in both.
+struct PcmLay {
+    int ps, ds;
+};
+__device__ __forceinline__ PcmLay pcm_lay(int planes, int np) { return planes ? PcmLay{1, np} : PcmLay{3, 1}; }
+__device__ __forceinline__ size_t pcm_at(PcmLay L, int k, int d) { return (size_t)k * L.ps + (size_t)d * L.ds; }
+
 // Reference-exact single-query scan (NmDistanceKernel, chamfer3D.cu:12-134):
 // 512-point tiles, best = d(first) per tile, strict '<' inside, strict '>'
 // across tiles.  Used only when non-finite coordinates are present, where the
-// tile boundaries decide which NaN wins.  `t` = target cloud [m,3] in global.
+// tile boundaries decide which NaN wins.  `t` = target cloud [m,3] in global
+// (layout L).
 template <typename TIn>
 __device__ inline void pcm_ref_nn_scan(float x1, float y1, float z1, const TIn *__restrict__ t,
-                                       int m, float &out_d, int &out_i) {
+                                       int m, float &out_d, int &out_i, PcmLay L = PcmLay{3, 1}) {
     float res = 0.f;
     int res_i = 0;
     for (int k2 = 0; k2 < m; k2 += 512) {
@@ -131,8 +144,8 @@ __device__ inline void pcm_ref_nn_scan(float x1, float y1, float z1, const TIn *
         float best = 0.f;
         int best_i = 0;
         for (int k = 0; k < end_k; ++k) {
-            const TIn *q = t + 3 * (size_t)(k2 + k);
-            const float d = pcm_sqd(pcm_ld(q) - x1, pcm_ld(q + 1) - y1, pcm_ld(q + 2) - z1);
+            const TIn *q = t + (size_t)(k2 + k) * L.ps;
+            const float d = pcm_sqd(pcm_ld(q) - x1, pcm_ld(q + L.ds) - y1, pcm_ld(q + 2 * (size_t)L.ds) - z1);
             if (k == 0 || d < best) { best = d; best_i = k + k2; }
         }
         if (k2 == 0 || res > best) { res = best; res_i = best_i; }

@@ -8,6 +8,11 @@ Outputs keep the reference dtypes: float32 distances, int32 indices.
 Extension: float16 clouds are accepted as well (BASELINE config 5); distances
 stay float32 and gradients come back in float16 (the fp32 gradient of the
 widened clouds, rounded once).
+Extension: a float32 cloud given as a [B, N, 3] view of a contiguous
+[B, 3, N] tensor -- train.py:163's fake.transpose(2, 1) -- is read in place
+(pcm_chamfer_forward_layout), where the reference's .contiguous()
+(dist_chamfer_3D.py:79-80) copied it; its gradient is written in the same
+layout, so autograd's transpose backward needs no copy either.
 
 Extension: ``chamfer_3DLossFunction`` / ``chamfer_3DLoss`` return the training
 loss mean(dist1) + mean(dist2) of loss/loss.py:36 directly and compute its
@@ -47,8 +52,10 @@ class chamfer_3DFunction(Function):
             # the reference read Tensor::data<float>() and threw otherwise;
             # float16 is this build's extension
             raise TypeError("chamfer_3DFunction expects float32 (or float16) clouds of one dtype")
-        xyz1 = xyz1.contiguous()
-        xyz2 = xyz2.contiguous()
+        lay = _layouts(xyz1, xyz2)
+        if lay is None:
+            xyz1 = xyz1.contiguous()
+            xyz2 = xyz2.contiguous()
         device = xyz1.device
         # the kernels write every output element, except that an empty other
         # cloud leaves a direction's outputs untouched (chamfer3D.cu: no
@@ -59,7 +66,11 @@ class chamfer_3DFunction(Function):
         dist2 = alloc(batchsize, m, device=device)
         idx1 = alloc(batchsize, n, dtype=torch.int32, device=device)
         idx2 = alloc(batchsize, m, dtype=torch.int32, device=device)
-        pcm_hip.chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2)
+        if lay is None:
+            pcm_hip.chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2)
+        else:
+            pcm_hip.chamfer_forward_layout(xyz1, xyz2, lay[0], lay[1], dist1, dist2, idx1, idx2)
+        ctx.layouts = lay
         ctx.save_for_backward(xyz1, xyz2, idx1, idx2)
         ctx.mark_non_differentiable(idx1, idx2)
         return dist1, dist2, idx1, idx2
@@ -72,10 +83,43 @@ class chamfer_3DFunction(Function):
                      else graddist1.contiguous().float())
         graddist2 = (torch.zeros_like(idx2, dtype=torch.float32) if graddist2 is None
                      else graddist2.contiguous().float())
-        gradxyz1 = torch.empty_like(xyz1)
-        gradxyz2 = torch.empty_like(xyz2)
-        pcm_hip.chamfer_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
+        lay = ctx.layouts
+        if lay is None:
+            gradxyz1 = torch.empty_like(xyz1)
+            gradxyz2 = torch.empty_like(xyz2)
+            pcm_hip.chamfer_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
+        else:
+            # each gradient in its cloud's layout: for channel planes the
+            # transpose's backward then hands autograd a contiguous [B, 3, N]
+            gradxyz1, gradxyz2 = _empty_like_layout(xyz1, lay[0]), _empty_like_layout(xyz2, lay[1])
+            pcm_hip.chamfer_backward_layout(xyz1, xyz2, lay[0], lay[1], graddist1, graddist2, idx1, idx2,
+                                            gradxyz1, gradxyz2)
         return gradxyz1, gradxyz2
+
+
+def _layouts(xyz1, xyz2):
+    """(layout1, layout2) when the clouds can be read in place -- float32, each
+    contiguous rows (0) or a [B, N, 3] view of contiguous [B, 3, N] channel
+    planes (1: the generator output train.py:163 passes as
+    fake.transpose(2, 1)), at least one of them planes, and a size the dense
+    forward serves -- else None (the reference's .contiguous() copies,
+    dist_chamfer_3D.py:79-80)."""
+    if xyz1.dtype != torch.float32 or xyz2.dtype != torch.float32 or not xyz1.is_cuda:
+        return None
+    l1, l2 = pcm_hip.cloud_layout(xyz1), pcm_hip.cloud_layout(xyz2)
+    if l1 is None or l2 is None or (l1 == 0 and l2 == 0):
+        return None
+    n, m = xyz1.shape[1], xyz2.shape[1]
+    if n >= pcm_hip.GRID_MIN_POINTS and m >= pcm_hip.GRID_MIN_POINTS:
+        return None  # the grid forward of large clouds reads rows
+    return (l1, l2)
+
+
+def _empty_like_layout(t, lay):
+    b, n, _ = t.shape
+    if lay == 1:
+        return torch.empty(b, 3, n, dtype=t.dtype, device=t.device).transpose(1, 2)
+    return torch.empty(b, n, 3, dtype=t.dtype, device=t.device)
 
 
 class chamfer_3DLossFunction(Function):
@@ -149,6 +193,9 @@ class chamfer_3DDist(nn.Module):
         super(chamfer_3DDist, self).__init__()
 
     def forward(self, input1, input2):
-        input1 = input1.contiguous()
-        input2 = input2.contiguous()
+        # the reference makes both contiguous (dist_chamfer_3D.py:79-80); a
+        # transposed [B, 3, N] generator output is read in place instead
+        if _layouts(input1, input2) is None:
+            input1 = input1.contiguous()
+            input2 = input2.contiguous()
         return chamfer_3DFunction.apply(input1, input2)

@@ -28,7 +28,7 @@ EXPORTED = (
     "pcm_emd_workspace_bytes", "pcm_emd_forward", "pcm_emd_backward", "pcm_emd_workspace_status",
     "pcm_chamfer_forward_f16", "pcm_chamfer_backward_f16",
     "pcm_chamfer_forward_ws_bytes", "pcm_chamfer_forward_ws", "pcm_chamfer_forward_ws_f16",
-    "pcm_chamfer_loss_grad",
+    "pcm_chamfer_loss_grad", "pcm_chamfer_forward_layout", "pcm_chamfer_backward_layout",
     "pcm_icp_workspace_bytes", "pcm_icp", "pcm_icp_workspace_status", "pcm_nearest_neighbor",
     "pcm_best_fit_transform",
     "pcm_npy_cloud_points", "pcm_npy_load_clouds",
@@ -87,6 +87,11 @@ def load_library():
     L.pcm_tune_chamfer_backward.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
     L.pcm_tune_chamfer_forward_loss.restype = ci
     L.pcm_tune_chamfer_forward_loss.argtypes = [ci, ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, vp, cs, vp]
+    if hasattr(L, "pcm_chamfer_forward_layout"):  # absent from A/B builds of older sources
+        L.pcm_chamfer_forward_layout.restype = ci
+        L.pcm_chamfer_forward_layout.argtypes = [vp, vp, ci, ci, ci, ci, ci, vp, vp, vp, vp, vp]
+        L.pcm_chamfer_backward_layout.restype = ci
+        L.pcm_chamfer_backward_layout.argtypes = [vp, vp, ci, ci, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
     L.pcm_chamfer_forward_f16.restype = ci
     L.pcm_chamfer_forward_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
     L.pcm_chamfer_backward_f16.restype = ci
@@ -194,6 +199,46 @@ def forward_workspace(dev: torch.device, b: int, n: int, m: int) -> torch.Tensor
         ws = torch.empty(need, dtype=torch.uint8, device=dev)
         _ws_cache[key] = ws
     return ws
+
+
+def cloud_layout(t: torch.Tensor):
+    """0 for a contiguous [B, N, 3] cloud (rows), 1 for a [B, N, 3] view of a
+    contiguous [B, 3, N] tensor (channel planes: the generator output
+    train.py:163 passes as fake.transpose(2, 1)), None for anything else."""
+    if t.dim() != 3 or t.shape[2] != 3:
+        return None
+    b, n, _ = t.shape
+    if t.is_contiguous():
+        return 0
+    st = t.stride()
+    if (st[1] == 1 or n == 1) and st[2] == n and (st[0] == 3 * n or b == 1):
+        return 1
+    return None
+
+
+def chamfer_forward_layout(xyz1, xyz2, lay1, lay2, dist1, dist2, idx1, idx2) -> None:
+    """pcm_chamfer_forward_layout: float32 clouds each in rows (0) or channel
+    planes (1, see cloud_layout); results identical to chamfer_forward on rows."""
+    dev = _require_device(xyz1, xyz2, dist1, dist2, idx1, idx2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    if xyz1.dtype != torch.float32 or xyz2.dtype != torch.float32:
+        raise TypeError("chamfer_forward_layout takes float32 clouds")
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_chamfer_forward_layout(
+            _ptr(xyz1), _ptr(xyz2), b, n, m, int(lay1), int(lay2), _ptr(dist1), _ptr(dist2), _ptr(idx1),
+            _ptr(idx2), _stream(dev)), "pcm_chamfer_forward_layout")
+
+
+def chamfer_backward_layout(xyz1, xyz2, lay1, lay2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2) -> None:
+    """pcm_chamfer_backward_layout: gradxyz1/2 written in their cloud's layout."""
+    dev = _require_device(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_chamfer_backward_layout(
+            _ptr(xyz1), _ptr(xyz2), b, n, m, int(lay1), int(lay2), _ptr(graddist1), _ptr(graddist2), _ptr(idx1),
+            _ptr(idx2), _ptr(gradxyz1), _ptr(gradxyz2), _stream(dev)), "pcm_chamfer_backward_layout")
 
 
 def chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:

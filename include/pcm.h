@@ -138,6 +138,22 @@ int pcm_chamfer_backward(const float *xyz1, const float *xyz2, int b, int n, int
                          float *gradxyz1, float *gradxyz2, void *stream);
 
 /*
+ * Clouds in either layout (extension): layout 0 = [b, n, 3] rows, as above;
+ * layout 1 = [b, 3, n] channel planes -- the generator's B x 3 x N output,
+ * which train.py:163 hands to the loss as fake.transpose(2, 1); the
+ * reference's wrapper copies such a view to rows first (dist_chamfer_3D.py:79-80),
+ * these read it in place, and the backward writes each cloud's gradient in
+ * that cloud's layout (so autograd's transpose backward needs no copy either).
+ * Results are bit-identical to pcm_chamfer_forward / pcm_chamfer_backward on
+ * the rows.  float32 only; per-point outputs and graddists stay [b, n].
+ */
+int pcm_chamfer_forward_layout(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1, int layout2,
+                               float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, void *stream);
+int pcm_chamfer_backward_layout(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1, int layout2,
+                                const float *graddist1, const float *graddist2, const int32_t *idx1,
+                                const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream);
+
+/*
  * fp16 clouds (extension for BASELINE config 5; the reference accepted fp32
  * only).  xyz1/xyz2 hold IEEE binary16 values.  Coordinates are widened to
  * fp32 exactly, so dist/idx are bit-identical to pcm_chamfer_forward on the

@@ -811,3 +811,63 @@ def test_loss_function_scales_upstream_gradient(cuda):
     torch.cuda.synchronize()
     np.testing.assert_allclose(x1.grad.cpu().numpy(), y1.grad.cpu().numpy(), rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(x2.grad.cpu().numpy(), y2.grad.cpu().numpy(), rtol=1e-6, atol=1e-9)
+
+
+@pytest.mark.parametrize("b,n,m,lays", [
+    (32, 1024, 1024, (1, 0)),   # train.py:163: fake.transpose(2, 1) against the GT rows
+    (32, 1024, 1024, (1, 1)),
+    (3, 1000, 700, (0, 1)),
+    (2, 5, 3, (1, 1)),
+    (1, 2049, 100, (1, 0)),     # crosses the 2048-point tile; backward on the global-memory kernel
+    (2, 300, 2500, (0, 1)),
+])
+def test_channel_plane_layout_matches_oracle(cuda, oracle, b, n, m, lays):
+    # clouds given as [B, N, 3] views of contiguous [B, 3, N] tensors are read
+    # in place (pcm_chamfer_forward_layout / _backward_layout): the same bits as
+    # the rows, no copy kernels, and each gradient in its cloud's layout
+    import dist_chamfer_3D
+    a, c = _clouds(131, b, n, m, "normal")
+    leaves = []
+    for t, lay in ((a, lays[0]), (c, lays[1])):
+        leaf = (t.transpose(1, 2).contiguous() if lay else t.clone()).to(cuda).requires_grad_(True)
+        leaves.append(leaf)
+    x1 = leaves[0].transpose(1, 2) if lays[0] else leaves[0]
+    x2 = leaves[1].transpose(1, 2) if lays[1] else leaves[1]
+    assert dist_chamfer_3D._layouts(x1, x2) == lays
+    d1, d2, i1, i2 = dist_chamfer_3D.chamfer_3DDist()(x1, x2)
+    (torch.mean(d1) + torch.mean(d2)).backward()
+    torch.cuda.synchronize()
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    _assert_fwd_equal((d1.detach().cpu().numpy(), d2.detach().cpu().numpy(), i1.cpu().numpy(), i2.cpu().numpy()),
+                      ref)
+    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), np.float32(1.0 / (b * n)), np.float32),
+                                       np.full((b, m), np.float32(1.0 / (b * m)), np.float32), ref[2], ref[3])
+    for leaf, lay, gr in ((leaves[0], lays[0], gr1), (leaves[1], lays[1], gr2)):
+        g = leaf.grad
+        assert g.is_contiguous()  # no copy needed to accumulate into the planes leaf
+        got = (g.transpose(1, 2) if lay else g).cpu().contiguous().numpy()
+        np.testing.assert_array_equal(got.view(np.int32), gr.view(np.int32))
+
+
+def test_channel_plane_layout_capi(cuda, oracle):
+    # the C ABI with explicit layouts, forward and backward, against rows
+    import pcm_hip
+    b, n, m = 4, 777, 1024
+    a, c = _clouds(132, b, n, m)
+    ap = a.transpose(1, 2).contiguous().to(cuda)  # [b, 3, n] planes
+    x2 = c.to(cuda)
+    out = [torch.empty(b, n, device=cuda), torch.empty(b, m, device=cuda),
+           torch.empty(b, n, dtype=torch.int32, device=cuda), torch.empty(b, m, dtype=torch.int32, device=cuda)]
+    pcm_hip.chamfer_forward_layout(ap.transpose(1, 2), x2, 1, 0, *out)
+    g1 = torch.full((b, n), 0.25, device=cuda)
+    g2 = torch.full((b, m), 0.5, device=cuda)
+    gx1 = torch.empty(b, 3, n, device=cuda)
+    gx2 = torch.empty(b, m, 3, device=cuda)
+    pcm_hip.chamfer_backward_layout(ap.transpose(1, 2), x2, 1, 0, g1, g2, out[2], out[3], gx1.transpose(1, 2), gx2)
+    torch.cuda.synchronize()
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    _assert_fwd_equal([t.cpu().numpy() for t in out], ref)
+    r1, r2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), 0.25, np.float32),
+                                     np.full((b, m), 0.5, np.float32), ref[2], ref[3])
+    np.testing.assert_array_equal(gx1.transpose(1, 2).cpu().contiguous().numpy().view(np.int32), r1.view(np.int32))
+    np.testing.assert_array_equal(gx2.cpu().numpy().view(np.int32), r2.view(np.int32))

@@ -2098,6 +2098,20 @@ extern "C" int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const 
 
 extern "C" int pcm_tune_num_chamfer_loss_grad_variants(void) { return kNumGradVariants; }
 
+// `reps` back-to-back launches of the default step from one host call (a C
+// caller's training loop, without Python's per-call cost): tools/probe_replay.py
+extern "C" int pcm_tune_chamfer_loss_grad_repeat(int reps, const float *xyz1, const float *xyz2, int b, int n, int m,
+                                                 float w1, float w2, float *dist1, float *dist2, int32_t *idx1,
+                                                 int32_t *idx2, float *mean_out, float *gradxyz1, float *gradxyz2,
+                                                 void *workspace, size_t workspace_bytes, void *stream) {
+    for (int r = 0; r < reps; ++r) {
+        const int st = launch_loss_grad(default_grad_variant(b, n, m), xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1,
+                                        idx2, mean_out, gradxyz1, gradxyz2, workspace, workspace_bytes, stream);
+        if (st != PCM_OK) return st;
+    }
+    return PCM_OK;
+}
+
 extern "C" int pcm_chamfer_forward_layout(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1,
                                           int layout2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
                                           void *stream) {

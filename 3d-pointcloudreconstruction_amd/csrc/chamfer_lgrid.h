@@ -47,19 +47,30 @@
 // kernels do.  Degenerate clouds (one cell holding everything) stay exact;
 // they only cost more (windows of the whole cloud; O(cell^2) in-cell ranks).
 
+// fine phase stamps (profiling build): table rows 4096 + wg and 8192 + wg
+#ifdef PCM_STAMPS
+#define LG_STAMP(row, i)                                                                             \
+    do {                                                                                             \
+        if (threadIdx.x == 0 && blockIdx.x < 4096)                                                   \
+            g_pcm_stamps[((row) * 4096 + blockIdx.x) * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); \
+    } while (0)
+#else
+#define LG_STAMP(row, i) \
+    do {                 \
+    } while (0)
+#endif
+
 constexpr int kLgW = 8;              // waves per workgroup
 constexpr int kLgNT = 64 * kLgW;     // threads
 constexpr int kLgQW = 256;           // query ranks (forward) / index range (gradients) per workgroup
 constexpr int kLgCap = kGradCap;     // points per cloud (1024)
 constexpr int kLgCells = 512;        // G^3 cells at G = 8
 constexpr int kLgC = 8;              // screen chunk (candidates)
-constexpr int kLgPiece = 256;        // window entries a wave transforms per piece
+constexpr int kLgGroupCap = 512;     // window entries a group's screen buffer holds (one piece)
 constexpr unsigned kLgTagBits = 21;  // granule: tag << 11 | idx (idx < 2048)
 constexpr unsigned kLgTagMask = (1u << kLgTagBits) - 1u;
 constexpr float kLgU16 = 9.5367431640625e-07f;  // 16 u = 2^-20 (chamfer_filt.hip's bound)
-constexpr int kLgArena = kLgW * kLgPiece * 16;   // 32 KB: query sort, then screen tiles, then gradient scratch
-static_assert(kLgPiece * 16 >= 3 * 64 * 4, "a wave's merge record fits its screen tile");
-static_assert(kLgArena >= kLgCap * 16, "the query sort fits the arena");
+constexpr int kLgArena = 4 * kLgGroupCap * 16;   // 32 KB: the groups' screen buffers, then gradient scratch
 static_assert(kLgArena >= 4 * kLgQW + 2 * kLgQW * kGradSlotsMax + 4 * kLgCap, "gradient scratch fits the arena");
 static_assert(kLgCap <= 2048, "11 index bits");
 
@@ -102,40 +113,48 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
     float *__restrict__ mean_out, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
     GradWs ws, unsigned max_spins, unsigned poll_spins) {
-    __shared__ pcm_f4 sTs[kLgCap];           // targets sorted by cell: (x, y, z, index bits)
-    __shared__ uint16_t sInv[kLgCap];        // target index -> sorted position
-    __shared__ int sTSt[kLgCells + 1];       // target cell counts, then starts (row-major cells)
-    __shared__ int sQSt[kLgCells + 1];       // query cell counts, then starts (query-key order)
-    __shared__ pcm_f4 sQs[kLgQW];            // this workgroup's query ranks: (x, y, z, index bits)
-    __shared__ uint16_t sWpos[4][kLgCap];    // per group: window entry -> sorted target position
-    __shared__ int sRowPre[kLgW][65];        // per wave: window row prefix sums
-    __shared__ int sRowSt[kLgW][64];         // per wave: window row start positions
-    __shared__ float sBox[kLgW][8];          // bounding-box partials, non-finite votes
-    __shared__ int sTw[kLgW], sQw[kLgW];     // block scan: wave totals
-    __shared__ float sMR[kLgW];              // per wave: max |t'|^2 of its window part
-    __shared__ int sList[kLgQW];             // queries for an exact scan of all targets
+    __shared__ pcm_f4 sTs[kLgCap];            // targets sorted by cell: (x, y, z, index bits)
+    __shared__ uint16_t sInv[kLgCap];         // target index -> sorted position
+    __shared__ int sTSt[kLgCells + 4];        // target cell counts, then starts (row-major cells)
+    __shared__ pcm_f4 sQs[kLgQW];             // this workgroup's queries in cell order: (x, y, z, index bits)
+    __shared__ uint16_t sWpos[4][kLgCap];     // per group: window entry -> sorted target position
+    // one region, two lives: the query cell counts/starts and the window row
+    // prefixes until the last gather, then the screen's merge records
+    __shared__ __attribute__((aligned(16))) int sAux[kLgCells + 4 + kLgW * 65 > kLgW * 3 * 64
+                                                        ? kLgCells + 4 + kLgW * 65 : kLgW * 3 * 64];
+    __shared__ __attribute__((aligned(16))) float sBox[kLgW][8];  // bounding-box partials, non-finite vote
+    __shared__ int sTw[kLgW], sQw[kLgW];      // block scan: wave totals
+    __shared__ int sWn[4];                    // window size per group
+    __shared__ float sGR[kLgW];               // per wave: max |t'|^2 of the entries it gathered
+    __shared__ int sBase, sEnd;               // this workgroup's query ranks [sBase, sEnd)
+    __shared__ int sList[kLgCap];             // queries for an exact scan of all targets
     __shared__ int sNList;
     __shared__ float sRed[kLgW];
-    __shared__ int sOvf[kLgQW];
     __shared__ int sNOvf;
     __shared__ int sWcnt[2][kLgW];
     __shared__ int sWt[2][kLgW];
     __shared__ __attribute__((aligned(16))) unsigned char sArena[kLgArena];
+    int *sQSt = sAux;                         // [kLgCells + 1]
+    int(*sRowPre)[65] = reinterpret_cast<int(*)[65]>(sAux + kLgCells + 4);  // [kLgW][65]
+    float *sRec = reinterpret_cast<float *>(sAux);  // [kLgW][3][64] (after the last gather)
 
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int nprod = (int)gridDim.x - 1;
     if ((int)blockIdx.x == nprod) {  // the grid's last workgroup: the loss means
+        PCM_STAMP2(5);
         poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, poll_spins, grad_shape_word(n, m, 2u));
+        PCM_STAMP2(6);
         return;
     }
+    PCM_STAMP2(0);
     const int per = nblk1 + nblk2;
     const int bid = pcm_xcd_remap((int)blockIdx.x, nprod);
     const int batch = bid / per;
     const int r = bid - batch * per;
     const bool first = r < nblk1;
-    const int q0 = (first ? r : r - nblk1) * kLgQW;  // rank range (forward) = index range (gradients)
+    const int q0 = (first ? r : r - nblk1) * kLgQW;  // index range of the gradient phase
     const float *X1 = xyz1 + (size_t)batch * n * 3;
     const float *X2 = xyz2 + (size_t)batch * m * 3;
     const float *Qc = first ? X1 : X2;  // queries of this direction = the gradient range's cloud
@@ -176,7 +195,11 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
         sy = Qc[3 * j + 1];
         sz = Qc[3 * j + 2];
     }
-    if (tid == 0) sNList = 0;
+    if (tid == 0) {
+        sNList = 0;
+        sBase = nq;  // no cell starts at or after rank q0: nothing owned
+        sEnd = nq;
+    }
     sTSt[tid] = 0;
     sQSt[tid] = 0;
     bool nonfinite = false;
@@ -194,34 +217,40 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
         }
         if (tid + k * kLgNT < nq) nonfinite |= !(pcm_finite(qx[k]) && pcm_finite(qy[k]) && pcm_finite(qz[k]));
     }
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float lo_a = lg_wave_min_f(mn[a]), hi_a = pcm_wave_max_f32(mx[a]);
-        if (lane == 0) {
-            sBox[wave][a] = lo_a;
-            sBox[wave][3 + a] = hi_a;
-        }
-    }
     {
-        const bool anynf = __ballot(nonfinite) != 0ull;
-        if (lane == 0) sBox[wave][6] = anynf ? 1.f : 0.f;
-    }
-    __syncthreads();  // B1
-    float lo[3], hi[3];
-    bool nonf = false;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        lo[a] = sBox[0][a];
-        hi[a] = sBox[0][3 + a];
-    }
-#pragma unroll
-    for (int w = 0; w < kLgW; ++w) {
+        // -min, max per axis and the non-finite vote: one 32-byte row per wave
+        float red[6];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            lo[a] = fminf(lo[a], sBox[w][a]);
-            hi[a] = fmaxf(hi[a], sBox[w][3 + a]);
+            red[a] = pcm_wave_max_f32(-mn[a]);
+            red[3 + a] = pcm_wave_max_f32(mx[a]);
         }
-        nonf |= sBox[w][6] != 0.f;
+        const bool anynf = __ballot(nonfinite) != 0ull;
+        if (lane == 0) {
+            *reinterpret_cast<pcm_f4 *>(&sBox[wave][0]) = pcm_f4{red[0], red[1], red[2], red[3]};
+            *reinterpret_cast<pcm_f4 *>(&sBox[wave][4]) = pcm_f4{red[4], red[5], anynf ? 1.f : 0.f, 0.f};
+        }
+    }
+    __syncthreads();  // B1
+    PCM_STAMP2(1);
+    float lo[3], hi[3];
+    bool nonf = false;
+    {
+        pcm_f4 r0 = *reinterpret_cast<const pcm_f4 *>(&sBox[0][0]), r1 = *reinterpret_cast<const pcm_f4 *>(&sBox[0][4]);
+#pragma unroll
+        for (int w = 1; w < kLgW; ++w) {
+            const pcm_f4 a = *reinterpret_cast<const pcm_f4 *>(&sBox[w][0]);
+            const pcm_f4 c = *reinterpret_cast<const pcm_f4 *>(&sBox[w][4]);
+            r0 = pcm_f4{fmaxf(r0.x, a.x), fmaxf(r0.y, a.y), fmaxf(r0.z, a.z), fmaxf(r0.w, a.w)};
+            r1 = pcm_f4{fmaxf(r1.x, c.x), fmaxf(r1.y, c.y), fmaxf(r1.z, c.z), 0.f};
+        }
+        lo[0] = -r0.x;
+        lo[1] = -r0.y;
+        lo[2] = -r0.z;
+        hi[0] = r0.w;
+        hi[1] = r1.x;
+        hi[2] = r1.y;
+        nonf = r1.z != 0.f;
     }
     const float g1w = __fmul_rn(w1, 2.f), g2w = __fmul_rn(w2, 2.f);
     const float gs = first ? g1w : g2w, gh = first ? g2w : g1w;
@@ -248,10 +277,10 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
         }
         __syncthreads();
     } else {
-        // ---- P1: grid over the target cloud's box (cubic cells)
+        // ---- P1: grid over the target cloud's box: cubic cells, G^3 <= nt / 2
         const float ext = fmaxf(hi[0] - lo[0], fmaxf(hi[1] - lo[1], hi[2] - lo[2]));
-        int G = (int)cbrtf((float)nt * 0.5f);
-        G = min(max(G, 1), 8);
+        int G = 1;
+        while (G < 8 && 2 * (G + 1) * (G + 1) * (G + 1) <= nt) ++G;
         if (!(ext > 0.f)) G = 1;
         const float h = G > 1 ? ext / (float)G : fmaxf(ext, 1.f);
         const float inv = 1.f / h;
@@ -272,7 +301,9 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
                 qslot[k] = atomicAdd(&sQSt[qkey[k]], 1);
             }
         }
+        LG_STAMP(1, 0);
         __syncthreads();  // B2
+        LG_STAMP(1, 1);
         {
             // exclusive starts of both histograms (thread = cell)
             const int ct = sTSt[tid], cq = sQSt[tid];
@@ -282,21 +313,29 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
                 sQw[wave] = iq;
             }
             __syncthreads();  // B3
+            LG_STAMP(1, 2);
             int bt = 0, bq = 0;
 #pragma unroll
             for (int w = 0; w < kLgW; ++w) {
                 bt += (w < wave) ? sTw[w] : 0;
                 bq += (w < wave) ? sQw[w] : 0;
             }
+            const int qs0 = bq + iq - cq;
             sTSt[tid] = bt + it - ct;
-            sQSt[tid] = bq + iq - cq;
-            if (tid == kLgNT - 1) {
-                sTSt[kLgCells] = bt + it;
-                sQSt[kLgCells] = bq + iq;
-            }
+            sQSt[tid] = qs0;
+            if (tid == kLgNT - 1) sTSt[kLgCells] = bt + it;
+            // Query ownership by cells: a cell belongs to the workgroup whose
+            // rank range [q0, q0 + 256) holds the cell's first rank (the cells'
+            // starts are the same in every workgroup of the element, so every
+            // query has exactly one owner, with no word exchanged).  The owned
+            // ranks run from the first cell start at or after q0 to the first
+            // at or after q0 + 256.
+            if (cq > 0 && qs0 <= q0 && q0 < qs0 + cq) sBase = qs0 == q0 ? q0 : qs0 + cq;
+            if (cq > 0 && qs0 <= q0 + kLgQW && q0 + kLgQW < qs0 + cq) sEnd = qs0 == q0 + kLgQW ? qs0 : qs0 + cq;
         }
         __syncthreads();  // B4
-        pcm_f4 *sQsort = reinterpret_cast<pcm_f4 *>(sArena);
+        LG_STAMP(1, 3);
+        const int base = sBase, cnt_wg = max(sEnd - base, 0);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const int p = tid + k * kLgNT;
@@ -305,38 +344,32 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
                 sTs[pos] = pcm_f4{tx[k], ty[k], tz[k], __int_as_float(p)};
                 sInv[p] = (uint16_t)pos;
             }
-            if (p < nq) sQsort[sQSt[qkey[k]] + qslot[k]] = pcm_f4{qx[k], qy[k], qz[k], __int_as_float(p)};
-        }
-        __syncthreads();  // B5
-        // ---- P2: query ranks: cell start + index order inside the cell (the
-        // same in every workgroup of the element); keep ranks [q0, q0 + 256)
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const int pp = tid + k * kLgNT;
-            if (pp < nq) {
-                const pcm_f4 e = sQsort[pp];
-                const int idx = __float_as_int(e.w);
-                const int key = lg_qkey(lg_cell(e.x, lo[0], inv, G), lg_cell(e.y, lo[1], inv, G),
-                                        lg_cell(e.z, lo[2], inv, G));
-                const int c0 = sQSt[key], c1 = sQSt[key + 1];
-                int rk = c0;
-                for (int i = c0; i < c1; ++i) rk += __float_as_int(sQsort[i].w) < idx;
-                if (rk >= q0 && rk < q0 + kLgQW) sQs[rk - q0] = e;
+            if (p < nq) {
+                const int rk = sQSt[qkey[k]] + qslot[k] - base;  // cells in order; ranks in a cell by arrival
+                if (rk >= 0 && rk < cnt_wg) {
+                    if (rk < kLgQW) sQs[rk] = pcm_f4{qx[k], qy[k], qz[k], __int_as_float(p)};
+                    else sList[atomicAdd(&sNList, 1)] = (1 << 30) | p;  // beyond 256 owned: exact scan
+                }
             }
         }
-        __syncthreads();  // B6 (the arena's query sort is dead from here)
+        LG_STAMP(1, 4);
+        __syncthreads();  // B5
+        LG_STAMP(1, 5);
 
-        // ---- P3: groups of 64 ranks, two waves each
-        const int cnt_wg = min(kLgQW, nq - q0);
+        // ---- P2: groups of 64 consecutive owned queries, two waves each:
+        // the group's query box widened by one cell, gathered row by row
+        // (rows alternate between the two waves) into the group's buffer as
+        // the filter's pair-interleaved (u, w) around the group's centre, in
+        // pieces of kLgGroupCap entries
         const int g = wave >> 1, half = wave & 1;
         const int qi = 64 * g + lane;
-        const bool grp = 64 * g < cnt_wg;  // wave-uniform
-        const bool valid = qi < cnt_wg;
-        const pcm_f4 q = sQs[min(qi, cnt_wg - 1)];
+        const int nwg = min(cnt_wg, kLgQW);
+        const bool grp = 64 * g < nwg;  // wave-uniform
+        const bool valid = qi < nwg;
+        const pcm_f4 q = sQs[min(qi, max(nwg - 1, 0))];
         int wl[3] = {0, 0, 0}, wh[3] = {0, 0, 0};
         float cen[3] = {0.f, 0.f, 0.f};
-        int Wn = 0;
-        float *mrec = reinterpret_cast<float *>(sArena + wave * kLgPiece * 16);  // merge record (after the scan)
+        int Wn = 0, nr = 0, ny = 1;
         if (grp) {
             const float qc[3] = {q.x, q.y, q.z};
 #pragma unroll
@@ -347,96 +380,122 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
                 wh[a] = min(cmax + 1, G - 1);
                 cen[a] = 0.5f * (lg_wave_min_f(valid ? qc[a] : PCM_INF) + pcm_wave_max_f32(valid ? qc[a] : -PCM_INF));
             }
-            const int ny = wh[1] - wl[1] + 1, nr = ny * (wh[2] - wl[2] + 1);  // <= 64 rows
-            int rs = 0, rc = 0;
+            ny = wh[1] - wl[1] + 1;
+            nr = ny * (wh[2] - wl[2] + 1);  // <= 64 rows
+            int rc = 0;
             if (lane < nr) {
-                const int base = ((wl[2] + lane / ny) * G + wl[1] + lane % ny) * G;
-                rs = sTSt[base + wl[0]];
-                rc = sTSt[base + wh[0] + 1] - rs;
+                const int rb = ((wl[2] + lane / ny) * G + wl[1] + lane % ny) * G;
+                rc = sTSt[rb + wh[0] + 1] - sTSt[rb + wl[0]];
             }
             const int inc = pcm_wave_incl_scan(rc);
             Wn = __builtin_amdgcn_readlane(inc, 63);
             sRowPre[wave][lane] = inc - rc;
-            sRowSt[wave][lane] = rs;
             if (lane == 63) sRowPre[wave][64] = inc;
+            if (half == 0 && lane == 0) sWn[g] = Wn;
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        } else if (half == 0 && lane == 0) {
+            sWn[g] = 0;
         }
-        // screen of this wave's chunks (c = half, half + 2, ...) in pieces
+#ifdef PCM_STAMPS
+        if (half == 0 && lane == 0 && blockIdx.x < kStampSlots / 2)
+            g_pcm_stamps[blockIdx.x * 8 + 2 + g] = (unsigned long long)Wn;  // window size per group
+#endif
+        // this wave's rows r = 2 l + half: lane l walks row r
+        int rpre = 0, rcnt = 0, rpos = 0;
+        {
+            const int rr = 2 * lane + half;
+            if (grp && rr < nr) {
+                rpre = sRowPre[wave][rr];
+                rcnt = sRowPre[wave][rr + 1] - rpre;
+                rpos = sTSt[((wl[2] + rr / ny) * G + wl[1] + rr % ny) * G + wl[0]];
+            }
+        }
+        const int rmax = lg_wave_max_i(rcnt);
+        float rt2 = 0.f;  // max |t'|^2 over the entries this wave gathered
         const float qxp = q.x - cen[0], qyp = q.y - cen[1], qzp = q.z - cen[2];
         const pcm_f2 px = {qxp, qxp}, py = {qyp, qyp}, pz = {qzp, qzp};
-        float fb = PCM_INF, fs = PCM_INF, rt2 = 0.f;
+        float fb = PCM_INF, fs = PCM_INF;
         int fc = 0;
-        const int nch = (Wn + kLgC - 1) / kLgC;
-        const int nmy = nch > half ? (nch - half + 1) >> 1 : 0;
-        pcm_f4 *Fw = reinterpret_cast<pcm_f4 *>(sArena + wave * kLgPiece * 16);
-        float *Ff = reinterpret_cast<float *>(Fw);
-        for (int i0 = 0; i0 < nmy; i0 += kLgPiece / kLgC) {
-            const int np = min(kLgPiece / kLgC, nmy - i0);
-#pragma unroll
-            for (int kk = 0; kk < kLgPiece / 64; ++kk) {
-                const int le = lane + 64 * kk;
-                if (le < np * kLgC) {
-                    const int c = 2 * (i0 + (le >> 3)) + half;
-                    const int e = kLgC * c + (le & 7);
-                    float ux = 0.f, uy = 0.f, uz = 0.f, wv = PCM_INF;  // padding: screened value +inf
-                    if (e < Wn) {
-                        int rr = 0;
-#pragma unroll
-                        for (int step = 32; step > 0; step >>= 1)
-                            rr = sRowPre[wave][rr + step] <= e ? rr + step : rr;
-                        const int pos = sRowSt[wave][rr] + (e - sRowPre[wave][rr]);
-                        const pcm_f4 t = sTs[pos];
-                        sWpos[g][e] = (uint16_t)pos;  // each entry belongs to one wave's chunks
-                        const float x = t.x - cen[0], y = t.y - cen[1], z = t.z - cen[2];
-                        wv = __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
-                        rt2 = fmaxf(rt2, wv);
-                        ux = -2.f * x;
-                        uy = -2.f * y;
-                        uz = -2.f * z;
-                    }
-                    // pair-interleaved: Fw[2k] = {ux, ux', uy, uy'}, Fw[2k+1] = {uz, uz', w, w'}
-                    const int k2 = le >> 1, hh = le & 1;
-                    Ff[8 * k2 + hh] = ux;
-                    Ff[8 * k2 + 2 + hh] = uy;
-                    Ff[8 * k2 + 4 + hh] = uz;
-                    Ff[8 * k2 + 6 + hh] = wv;
+        float *Fg = reinterpret_cast<float *>(sArena + g * kLgGroupCap * 16);  // the group's screen buffer
+        const pcm_f4 *F4 = reinterpret_cast<const pcm_f4 *>(Fg);
+        int npieces = 1;
+        for (int pc = 0; pc < npieces; ++pc) {
+            const int e0 = pc * kLgGroupCap, e1 = min(e0 + kLgGroupCap, Wn);
+            if (pc > 0) __syncthreads();  // every wave is done screening the previous piece
+            for (int j = 0; j < rmax; ++j) {
+                const int e = rpre + j;
+                if (j < rcnt && e >= e0 && e < e1) {
+                    const int pos = rpos + j;
+                    const pcm_f4 t = sTs[pos];
+                    sWpos[g][e] = (uint16_t)pos;
+                    const float x = t.x - cen[0], y = t.y - cen[1], z = t.z - cen[2];
+                    const float wv = __builtin_fmaf(z, z, __builtin_fmaf(y, y, x * x));
+                    rt2 = fmaxf(rt2, wv);
+                    // pair-interleaved: F4[2k] = {ux, ux', uy, uy'}, F4[2k+1] = {uz, uz', w, w'}
+                    const int le = e - e0, k2 = le >> 1, hh = le & 1;
+                    Fg[8 * k2 + hh] = -2.f * x;
+                    Fg[8 * k2 + 2 + hh] = -2.f * y;
+                    Fg[8 * k2 + 4 + hh] = -2.f * z;
+                    Fg[8 * k2 + 6 + hh] = wv;
                 }
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            for (int ci = 0; ci < np; ++ci) {
+            {
+                // padding to whole chunks: screened value +inf
+                const int le = (e1 - e0) + lane;
+                if (grp && half == 0 && e1 > e0 && le < ((e1 - e0 + kLgC - 1) & ~(kLgC - 1))) {
+                    const int k2 = le >> 1, hh = le & 1;
+                    Fg[8 * k2 + hh] = 0.f;
+                    Fg[8 * k2 + 2 + hh] = 0.f;
+                    Fg[8 * k2 + 4 + hh] = 0.f;
+                    Fg[8 * k2 + 6 + hh] = PCM_INF;
+                }
+            }
+            if (pc == 0) LG_STAMP(1, 7);
+            __syncthreads();  // Bg: the pieces of every group are in (and sWn)
+            if (pc == 0) {
+                int most = max(max(sWn[0], sWn[1]), max(sWn[2], sWn[3]));
+                npieces = max(1, (most + kLgGroupCap - 1) / kLgGroupCap);
+            }
+            // screen this wave's chunks of the piece (local chunks c = half, half + 2, ...)
+            const int nch = (e1 - e0 + kLgC - 1) / kLgC;
+            for (int c = half; c < nch; c += 2) {
                 float mnv = PCM_INF;
 #pragma unroll
                 for (int pp = 0; pp < kLgC / 2; ++pp) {
-                    const pcm_f4 A = Fw[ci * kLgC + 2 * pp], Bv = Fw[ci * kLgC + 2 * pp + 1];
+                    const pcm_f4 A = F4[c * kLgC + 2 * pp], Bv = F4[c * kLgC + 2 * pp + 1];
                     const pcm_f2 a = __builtin_elementwise_fma(
                         px, A.xy, __builtin_elementwise_fma(py, A.zw, __builtin_elementwise_fma(pz, Bv.xy, Bv.zw)));
                     mnv = __builtin_fminf(__builtin_fminf(mnv, a.x), a.y);
                 }
                 fs = __builtin_amdgcn_fmed3f(mnv, fb, fs);
                 const bool lt = mnv < fb;
-                fc = lt ? 2 * (i0 + ci) + half : fc;
+                fc = lt ? (e0 / kLgC) + c : fc;
                 fb = lt ? mnv : fb;
             }
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the next piece rewrites the tile
         }
+        PCM_STAMP2(3);
         {
+            // merge record (the aux region: query starts and row prefixes are
+            // dead since the last gather's barrier)
             const float rm = pcm_wave_max_f32(rt2);
-            mrec[lane] = fb;
-            mrec[64 + lane] = fs;
-            mrec[128 + lane] = __int_as_float(fc);
-            if (lane == 0) sMR[wave] = rm;
+            sRec[(wave * 3 + 0) * 64 + lane] = fb;
+            sRec[(wave * 3 + 1) * 64 + lane] = fs;
+            sRec[(wave * 3 + 2) * 64 + lane] = __int_as_float(fc);
+            if (lane == 0) sGR[wave] = rm;
         }
         __syncthreads();  // B7: both halves' screens are in
+        LG_STAMP(2, 0);
         if (grp) {
-            const float *m0 = reinterpret_cast<const float *>(sArena + (2 * g) * kLgPiece * 16);
-            const float *m1 = reinterpret_cast<const float *>(sArena + (2 * g + 1) * kLgPiece * 16);
-            const float b0 = m0[lane], s0 = m0[64 + lane], b1 = m1[lane], s1 = m1[64 + lane];
-            const int c0 = __float_as_int(m0[128 + lane]), c1 = __float_as_int(m1[128 + lane]);
+            const int w0 = 2 * g, w1i = 2 * g + 1;
+            const float b0 = sRec[(w0 * 3) * 64 + lane], s0 = sRec[(w0 * 3 + 1) * 64 + lane];
+            const float b1 = sRec[(w1i * 3) * 64 + lane], s1 = sRec[(w1i * 3 + 1) * 64 + lane];
+            const int c0 = __float_as_int(sRec[(w0 * 3 + 2) * 64 + lane]);
+            const int c1 = __float_as_int(sRec[(w1i * 3 + 2) * 64 + lane]);
             const bool better = (b1 < b0) | ((b1 == b0) & (c1 < c0));
             const float mb = better ? b1 : b0;
             const float ms = fminf(fminf(s0, s1), better ? b0 : b1);
             const int mc = better ? c1 : c0;
-            const float rmax2 = fmaxf(sMR[2 * g], sMR[2 * g + 1]);
+            const float rmax2 = fmaxf(sGR[w0], sGR[w1i]);
             const float qn2 = __builtin_fmaf(qzp, qzp, __builtin_fmaf(qyp, qyp, qxp * qxp));
             const float sq = __builtin_amdgcn_sqrtf(qn2);
             const float rr = __builtin_amdgcn_sqrtf(rmax2) + sq;
@@ -445,6 +504,7 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
             const float rq = 2.f * sq + __builtin_amdgcn_sqrtf(db);
             const float e2 = 2.f * kLgU16 * fminf(rr * rr, rq * rq) * 1.001f;
             const bool proven = (ms - mb) > e2;  // false for NaN, inf - inf
+            LG_STAMP(2, 1);
             unsigned long long best = ~0ull;
             if (proven) {
                 // exact (distance, index) minimum of the best chunk; both
@@ -457,6 +517,7 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
                     best = kk < best ? kk : best;
                 }
             }
+            LG_STAMP(2, 2);
             const float bd = __uint_as_float((unsigned)(best >> 32));
             // region proof (chamfer_grid.hip): targets outside the window are
             // >= gap away along some axis
@@ -480,14 +541,26 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
                     sList[atomicAdd(&sNList, 1)] = qi;
                 }
             }
+            LG_STAMP(2, 3);
         }
         __syncthreads();  // B8
-        // ---- P4: listed queries (near ties, or a nearest neighbour beyond
-        // the window): one wave per query scans every target exactly
+        PCM_STAMP2(4);
+#ifdef PCM_STAMPS
+        if (tid == 0 && blockIdx.x < kStampSlots / 2) g_pcm_stamps[blockIdx.x * 8 + 0] = (unsigned long long)sNList;
+#endif
+        // ---- P3: listed queries (near ties, a nearest neighbour beyond the
+        // window, owned queries beyond the first 256): one wave per query
+        // scans every target exactly
         const int nl = sNList;
         for (int e = wave; e < nl; e += kLgW) {
             const int s = __builtin_amdgcn_readfirstlane(sList[e]);
-            const pcm_f4 qq = sQs[s];
+            pcm_f4 qq;
+            if (s & (1 << 30)) {
+                const int p = s & ((1 << 30) - 1);
+                qq = pcm_f4{Qc[3 * p], Qc[3 * p + 1], Qc[3 * p + 2], __int_as_float(p)};
+            } else {
+                qq = sQs[s];
+            }
             unsigned long long best = ~0ull;
             for (int k = lane; k < nt; k += 64) {
                 const pcm_f4 t = sTs[k];
@@ -508,6 +581,7 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
         }
     }
 
+    PCM_STAMP2(5);
     // ---- P5: gradients of the index range [q0, q0 + 256) (range_grad's
     // granule form; the other cloud from the sorted LDS copy)
     constexpr int kPerS = (kLgCap + kLgNT - 1) / kLgNT;  // other-cloud sources per thread
@@ -568,6 +642,7 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
                 gr[k] = __hip_atomic_load(Go + min(tid + k * kLgNT, na - 1), __ATOMIC_RELAXED,
                                           __HIP_MEMORY_SCOPE_AGENT);
     }
+    PCM_STAMP2(6);
     const int io = (int)(go & 2047u);
     float ox = 0.f, oy = 0.f, oz = 0.f;
     getA(own ? io : 0, ox, oy, oz);
@@ -618,14 +693,14 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
             Gd[3 * jown + 1] = ay;
             Gd[3 * jown + 2] = az;
         } else {
-            sOvf[atomicAdd(&sNOvf, 1)] = tid;
+            sList[atomicAdd(&sNOvf, 1)] = tid;
         }
     }
     __syncthreads();
     // overflowed buckets (> 16 sources): ascending source list by ballots
     const int nov = sNOvf;
     for (int e = 0; e < nov; ++e) {
-        const int t = sOvf[e];
+        const int t = sList[e];
         const int j = q0 + t;
         unsigned long long bal[kPerS];
 #pragma unroll
@@ -674,4 +749,5 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
         }
         __syncthreads();
     }
+    PCM_STAMP2(7);
 }

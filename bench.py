@@ -12,10 +12,15 @@ gradient torch's mean feeds it).  Inputs are resident in HBM before timing.
 The step runs as ONE launch of pcm_chamfer_loss_grad (forward, loss and both
 clouds' gradients; csrc/chamfer_filt.hip); --two-launch runs it as the fused-
 loss forward + the backward kernel instead (both are reported).
-By default GRAPH_STEPS consecutive steps are captured in one hipGraph and
-replayed (HIP graphs instead of a tracing compiler: a step is two ~10 us
-kernels, so per-step host launches would leave the GPU idle); --eager launches
-through the Python API each step.
+At N=1 the timed region launches the step directly through the C ABI, once
+per step, with its arguments bound once (a native training loop's call; the
+host stays ahead of the ~14 us kernel, so the GPU runs the steps back to
+back).  tools/probe_replay.py measured the alternatives on MI355X: a replay of
+a 20-step hipGraph adds ~0.8 us per kernel node and ~16 us of replay floor,
+the Python wrapper per step ~0.5 us (r05c).  --graph times the 20-step graph
+instead (its first replay paid in warmup); --eager the Python wrapper.  The
+GPU-side time of the timed region (HIP events at its edges, on the kernel's
+stream) is the dominant kernel's duration in `roofline`.
 
 value = point pairs evaluated per second over all ranks (2*B*N*M per rank per
 step / max-over-ranks wall time).  EMD (BASELINE config 3: B=16, N=1024,
@@ -92,7 +97,9 @@ def parse(argv=None):
                    help="ranks (one per GPU); default: WORLD_SIZE under torchrun, else 1")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
-    p.add_argument("--eager", action="store_true", help="no hipGraph capture")
+    p.add_argument("--eager", action="store_true", help="no hipGraph capture (Python wrapper per step)")
+    p.add_argument("--graph", action="store_true",
+                   help="N=1: time replays of the captured 20-step hipGraph instead of direct C-ABI launches")
     p.add_argument("--two-launch", action="store_true",
                    help="step = fused-loss forward + backward kernel (not the one-launch loss+gradient)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -192,23 +199,67 @@ class ChamferStep:
         pcm_hip.chamfer_backward(self.xyz1, self.xyz2, self.g1, self.g2, self.i1, self.i2,
                                  self.gx1, self.gx2)
 
+    def launcher(self):
+        """The step as direct launches through the C ABI (include/pcm.h), its
+        arguments bound once: what a native training loop calls per step,
+        without the Python wrapper's per-call checks (~10 us of host time
+        against a ~14 us kernel).  The host stays ahead of the GPU, so the
+        timed region holds back-to-back kernels and no replay floor."""
+        import ctypes
+        L = pcm_hip.load_library()
+        P = pcm_hip._ptr
+        st = pcm_hip._stream(self.xyz1.device)
+        ci, cf, cs = ctypes.c_int, ctypes.c_float, ctypes.c_size_t
+        if self.fused:
+            f = L.pcm_chamfer_loss_grad
+            args = (P(self.xyz1), P(self.xyz2), ci(B), ci(N), ci(M), cf(self.w1), cf(self.w2), P(self.d1), P(self.d2),
+                    P(self.i1), P(self.i2), P(self.loss[0]), P(self.gx1), P(self.gx2), P(self.ws),
+                    cs(self.ws.numel()), st)
+
+            def go():
+                if f(*args):
+                    raise pcm_hip.PcmError("pcm_chamfer_loss_grad failed")
+            return go
+        f1, f2 = L.pcm_chamfer_forward_loss, L.pcm_chamfer_backward
+        a1 = (P(self.xyz1), P(self.xyz2), ci(B), ci(N), ci(M), P(self.d1), P(self.d2), P(self.i1), P(self.i2),
+              P(self.loss[0]), P(self.ws), cs(self.ws.numel()), st)
+        a2 = (P(self.xyz1), P(self.xyz2), ci(B), ci(N), ci(M), P(self.g1), P(self.g2), P(self.i1), P(self.i2),
+              P(self.gx1), P(self.gx2), st)
+
+        def go2():
+            if f1(*a1) or f2(*a2):
+                raise pcm_hip.PcmError("pcm_chamfer_forward_loss / pcm_chamfer_backward failed")
+        return go2
+
     def reduce_losses(self, rows):
         """sum of per-rank means over RCCL (/world = global mean), stream-ordered"""
         if self.collective:
             dist.all_reduce(self.loss[:rows])
 
 
-def time_region(fn, calls, dev, world):
+def time_region(fn, calls, dev, world, gpu=None):
+    """Wall time of `calls` calls of fn, bracketed by a barrier + synchronize
+    on both sides, max over ranks.  gpu (a list): HIP events recorded on the
+    current stream at the region's edges append the GPU-side time (s)."""
     if dist.is_initialized():
         dist.barrier()
     torch.cuda.synchronize(dev)
+    s = torch.cuda.current_stream(dev)
+    if gpu is not None:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    if gpu is not None:
+        e0.record(s)
     for _ in range(calls):
         fn()
+    if gpu is not None:
+        e1.record(s)
     torch.cuda.synchronize(dev)
     if dist.is_initialized():
         dist.barrier()
     t = time.perf_counter() - t0
+    if gpu is not None:
+        gpu.append(e0.elapsed_time(e1) * 1e-3)
     if dist.is_initialized():
         tt = torch.tensor([t], device=dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -626,16 +677,24 @@ def main(argv=None):
         g_one = capture_steps(step, 1, dev, world, False)
         g_many = None
         if not multi:
-            # the step is one ~15 us kernel: `per` consecutive steps per hipGraph
-            # replay keep the host launch cost out of the step
+            # `per` consecutive steps per hipGraph replay (reported beside the
+            # headline; the default N=1 timed region launches directly)
             g_many = capture_steps(step, per, dev, world, False)
+            if args.graph:
+                def run_steps(k):
+                    for _ in range(k // per):
+                        g_many.replay()
+                    for _ in range(k % per):
+                        g_one.replay()
+                mode = f"hipgraph ({per} steps per graph)"
+            else:
+                go = step.launcher()
 
-            def run_steps(k):
-                for _ in range(k // per):
-                    g_many.replay()
-                for _ in range(k % per):
-                    g_one.replay()
-            mode = f"hipgraph ({per} steps per graph)"
+                def run_steps(k):
+                    for _ in range(k):
+                        go()
+                mode = ("direct C-ABI launches, one per step, arguments bound once (a native loop; "
+                        "tools/probe_replay.py: a hipGraph replay adds ~0.8 us per kernel node on ROCm 7)")
         else:
             g_ar_many = g_ar_one = None
             if args.dist_backend == "nccl" and not args.eager_allreduce:
@@ -678,13 +737,23 @@ def main(argv=None):
                         g_one.replay()
                         step.reduce_losses(1)
                 mode = "one-step hipgraph replay + eager all-reduce of the step's loss, every step"
-        g_tail = g_one if not multi else (g_ar_one if g_ar_many is not None else None)
-        graph_info = warm_graphs(g_many, g_tail, per, args.warmup, args.steps, run_steps, dev, world)
+        if multi or args.graph:
+            g_tail = g_one if not multi else (g_ar_one if g_ar_many is not None else None)
+            graph_info = warm_graphs(g_many, g_tail, per, args.warmup, args.steps, run_steps, dev, world)
+        else:
+            # the timed region's own launches: W of them
+            run_steps(args.warmup)
+            torch.cuda.synchronize(dev)
+            graph_info = {"graph_steps": per, "warmup_steps_requested": args.warmup,
+                          "warmup_steps_run": args.warmup}
+            g_many.replay()  # the graph form's first replay, outside every timed region
+            torch.cuda.synchronize(dev)
 
-    t = time_region(lambda: run_steps(args.steps), 1, dev, world)
+    gpu_t = []
+    t = time_region(lambda: run_steps(args.steps), 1, dev, world, gpu=gpu_t)
     if graph_info is not None and g_many is not None:
-        # a steady replay of the timed graph, after the timed region (compare
-        # with the first replay, which warmup paid)
+        # a steady replay of the `per`-step graph after the timed region (with
+        # --graph, compare with the first replay, which warmup paid)
         graph_info["steady_replay_us"] = time_region(g_many.replay, 1, dev, world) * 1e6
         graph_info["steady_replay_us_per_step"] = graph_info["steady_replay_us"] / per
     pairs_per_step = 2 * B * N * M
@@ -698,11 +767,17 @@ def main(argv=None):
                                                             step.i1, step.i2, step.gx1, step.gx2),
                            200, dev)
     fwd_tflops = pairs_per_step * FLOP_PER_PAIR / (fwd_us * 1e-6) / 1e12
+    # the dominant kernel's duration: HIP events on the kernel's stream over
+    # the timed region itself (back-to-back launches: the kernel plus its
+    # launch boundary); the 200-launch graph average beside it
+    region_us = gpu_t[0] * 1e6 / args.steps
     if step.fused:
         dom_kernel, dom_bytes = FUSED_KERNEL, FUSED_BYTES
-        dom_us = kernel_avg_us(lambda: step(0), 200, dev)
+        graph_kernel_us = kernel_avg_us(lambda: step(0), 200, dev)
+        dom_us = region_us if not (args.eager or args.graph or multi) else graph_kernel_us
     else:
         dom_kernel, dom_bytes, dom_us = FWD_KERNEL, FWD_BYTES, fwd_us
+        graph_kernel_us = fwd_us
     dom_tflops = pairs_per_step * FLOP_PER_PAIR / (dom_us * 1e-6) / 1e12
     traffic = pmc_bytes(dom_kernel)
     out = {
@@ -727,7 +802,10 @@ def main(argv=None):
                      "frac": dom_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,
                      "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE*2+WRITE_SIZE, " +
                                      os.path.relpath(PMC_SUMMARY, REPO) + ")",
-                     "kernel_us": dom_us,
+                     "kernel_us": dom_us, "kernel_us_source": (
+                         "HIP events on the kernel's stream around the timed region, per step"
+                         if dom_us == region_us else "HIP events around a 200-launch hipGraph replay, per launch"),
+                     "kernel_us_graph200": graph_kernel_us, "timed_region_gpu_us_per_step": region_us,
                      "note": "FLOPs = 8 per point pair (algorithmic); VALU-bound, see DESIGN.md"},
         "roofline_hbm": {"bound": "hbm", "kernel": dom_kernel, "rank": rank,
                          "achieved": dom_bytes / (dom_us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS,

@@ -16,6 +16,8 @@
 #   gridkt     rocprofv3 --kernel-trace --stats of tools/grid_diag.py
 #   pmc        tools/pmc_passes.sh (kernel trace of bench + one counter pass per group)
 #   stamps     tools/stamp_filt.py fused 7 11 (needs `make stamps`)
+#   stampslg   tools/stamp_lgrid.py 13 and 11 (needs `make stamps`)
+#   probe      tools/probe_replay.py (timed-region overhead by launch form)
 set -o pipefail
 TAG=$1
 shift
@@ -51,6 +53,9 @@ for S in "$@"; do
     pmc) timeout -k 10 900 bash tools/pmc_passes.sh "$O/pmc" > "$O/pmc_passes.log" 2>&1 ;;
     stamps) PCM_HIP_LIB=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_stamps.so timeout -k 10 300 \
                python -u tools/stamp_filt.py fused 7 11 > "$O/stamps_fused.txt" 2>&1 ;;
+    stampslg) timeout -k 10 300 python -u tools/stamp_lgrid.py 13 > "$O/stamps_lgrid.txt" 2>&1 &&
+              timeout -k 10 300 python -u tools/stamp_lgrid.py 11 >> "$O/stamps_lgrid.txt" 2>&1 ;;
+    probe) timeout -k 10 300 python -u tools/probe_replay.py > "$O/probe_replay.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac
     rc=$?

@@ -49,6 +49,8 @@
 // stages the target tile in parts so the scan starts before the prologue's
 // loads have all landed.  tools/ab_chamfer.py, same box: 7 13.65-13.74 us,
 // 11 13.62-13.77 us, 12 13.80-13.99 us (gpurun_out r04e).
+#include <type_traits>
+
 #include "pcm_common.h"
 #include "pcm_internal.h"
 #include "chamfer_loss.h"
@@ -204,7 +206,8 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                               float *__restrict__ D, int32_t *__restrict__ I, unsigned char *arena,
                               unsigned long long *__restrict__ Gr = nullptr, unsigned long long tag = 0,
                               const PreDma *pre = nullptr, pcm_f4 *qown = nullptr, PcmLay LQ = PcmLay{3, 1},
-                              PcmLay LT = PcmLay{3, 1}) {
+                              PcmLay LT = PcmLay{3, 1}, unsigned *__restrict__ Gr4 = nullptr, unsigned gtag4 = 0,
+                              int *kown = nullptr) {
     static_assert(C % 4 == 0 && TILE % C == 0, "tile must hold whole chunks of 4-candidate groups");
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
@@ -705,6 +708,9 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             // data-tagged argmin granule {call tag, idx}: one 8-byte sc1 store,
             // its own flag (no drain, no counter)
             if (Gr) __hip_atomic_store(Gr + qbase + tid, tag | (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // 4-byte granule {tag << 11 | idx} (chamfer_lgrid.h's format)
+            if (Gr4) __hip_atomic_store(Gr4 + qbase + tid, gtag4 | (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (kown) *kown = k;
         }
     } else {
         for (int s = tid; s < QW; s += NT) {
@@ -718,6 +724,8 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             out_st<kSc1>(D + qi, d);
             out_st<kSc1>(I + qi, (int32_t)idx);
             if (Gr) __hip_atomic_store(Gr + qi, tag | (unsigned)idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (Gr4) __hip_atomic_store(Gr4 + qi, gtag4 | (unsigned)idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (kown) *kown = idx;
         }
     }
     return my_d;
@@ -1370,16 +1378,30 @@ __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, flo
 // 0) rows at filt_slot<kLocalC>(i) (TA), and the range's points are the
 // forward's queries (SO[slot]); S and A are then the GLOBAL clouds, read only
 // by the timeout path's local argmin scans.
-template <int NT, int QW, bool kGran = false, int kLocalC = 0>
+// kG4: 4-byte granules {tag (21 bits) << 11 | idx} (tag: the u32 tag << 11)
+// instead of 8-byte {tag, idx}; own_k >= 0: this thread's own argmin is
+// already known (the workgroup's forward computed it), no granule read.
+template <int NT, int QW, bool kGran = false, int kLocalC = 0, bool kG4 = false>
 __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, const float *S, const float *A,
                                            float gs, float h, const int32_t *__restrict__ Iown,
                                            const int32_t *__restrict__ Ioth, float *__restrict__ G,
                                            unsigned char *scratch,
-                                           const unsigned long long *__restrict__ Gown = nullptr,
-                                           const unsigned long long *__restrict__ Goth = nullptr,
+                                           const void *__restrict__ Gown_v = nullptr,
+                                           const void *__restrict__ Goth_v = nullptr,
                                            unsigned long long tag = 0, unsigned max_spins = 0,
                                            unsigned *slow = nullptr, const pcm_f4 *TA = nullptr,
-                                           const pcm_f4 *SO = nullptr) {
+                                           const pcm_f4 *SO = nullptr, int own_k = -1) {
+    typedef typename std::conditional<kG4, unsigned, unsigned long long>::type gran_t;
+    const gran_t *Gown = reinterpret_cast<const gran_t *>(Gown_v);
+    const gran_t *Goth = reinterpret_cast<const gran_t *>(Goth_v);
+    auto tag_of = [](gran_t v) -> unsigned {
+        if constexpr (kG4) return (unsigned)v >> 11;
+        else return (unsigned)((unsigned long long)v >> 32);
+    };
+    auto idx_of = [](gran_t v) -> int {
+        if constexpr (kG4) return (int)((unsigned)v & 2047u);
+        else return (int)(unsigned)v;
+    };
     constexpr int kPerS = (kGradCap + NT - 1) / NT;  // sources per thread
     static_assert(kLocalC > 0 || 24 * kGradCap + 4 * QW + 2 * QW * kGradSlotsMax + 4 * kGradCap <= kGradBytes,
                   "both clouds, the counts, the buckets and the overflow list fit the arena");
@@ -1435,16 +1457,18 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
         // thread needs carries the call's tag (bounded; the whole workgroup
         // decides together), re-reading only those not yet current
         const bool own = tid < QW && jt < nq;
-        unsigned long long go = own ? __hip_atomic_load(Gown + jt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : tag;
-        unsigned long long gr[kPerS];
+        const gran_t tagv = (gran_t)tag;
+        gran_t go = !own ? tagv : (own_k >= 0 ? (gran_t)(tagv | (gran_t)own_k)
+                                              : __hip_atomic_load(Gown + jt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        gran_t gr[kPerS];
 #pragma unroll
         for (int r = 0; r < kPerS; ++r)
             gr[r] = __hip_atomic_load(Goth + min(tid + r * NT, na - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned want = (unsigned)(tag >> 32);
+        const unsigned want = tag_of(tagv);
         for (unsigned spins = 0;; ++spins) {
-            bool ready = (unsigned)(go >> 32) == want;
+            bool ready = tag_of(go) == want;
 #pragma unroll
-            for (int r = 0; r < kPerS; ++r) ready &= (unsigned)(gr[r] >> 32) == want;
+            for (int r = 0; r < kPerS; ++r) ready &= tag_of(gr[r]) == want;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (and the caller's LDS-DMA has landed)
             const int waiting = pcm_wg_or(!ready, sWt[spins & 1u], NW);
             if (!waiting && max_spins != 0u) break;
@@ -1456,39 +1480,39 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                 // the value the forward publishes -- so a timeout costs time,
                 // never correctness.  max_spins == 0 (tests) recomputes all.
                 const bool all = max_spins == 0u;
-                if (own && (all || (unsigned)(go >> 32) != want)) {
+                if (own && (all || tag_of(go) != want)) {
                     float d, x, y, z;
                     int k;
                     getS(tid, x, y, z);
                     pcm_ref_nn_scan(x, y, z, A, na, d, k);
-                    go = tag | (unsigned)k;
+                    go = tagv | (gran_t)k;
                 }
 #pragma unroll
                 for (int r = 0; r < kPerS; ++r) {
                     const int i = min(tid + r * NT, na - 1);
-                    if (all || (unsigned)(gr[r] >> 32) != want) {
+                    if (all || tag_of(gr[r]) != want) {
                         float d, x, y, z;
                         int k;
                         getA(i, x, y, z);
                         pcm_ref_nn_scan(x, y, z, S, nq, d, k);
-                        gr[r] = tag | (unsigned)k;
+                        gr[r] = tagv | (gran_t)k;
                     }
                 }
                 if (tid == 0) atomicAdd(slow, 1u);  // diagnostics (pcm_tune_chamfer_slow_paths)
                 break;
             }
             __builtin_amdgcn_s_sleep(1);
-            if (own && (unsigned)(go >> 32) != want)
+            if (own && tag_of(go) != want)
                 go = __hip_atomic_load(Gown + jt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
             for (int r = 0; r < kPerS; ++r)
-                if ((unsigned)(gr[r] >> 32) != want)
+                if (tag_of(gr[r]) != want)
                     gr[r] = __hip_atomic_load(Goth + min(tid + r * NT, na - 1), __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT);
         }
-        io = (int)(unsigned)go;
+        io = idx_of(go);
 #pragma unroll
-        for (int r = 0; r < kPerS; ++r) isr[r] = (int)(unsigned)gr[r];
+        for (int r = 0; r < kPerS; ++r) isr[r] = idx_of(gr[r]);
     } else {
         io = (tid < QW && jt < nq) ? ld_sc1(Iown + jt) : 0;
 #pragma unroll
@@ -1742,7 +1766,7 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
 #include "chamfer_lgrid.h"
 
 template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false,
-          bool kLocal = false, bool kSplit = false>
+          bool kLocal = false, bool kSplit = false, bool kG4 = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -1774,7 +1798,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     if ((int)blockIdx.x == nprod) {
         PCM_STAMP2(5);
         if constexpr (kGran)
-            poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, poll_spins, grad_shape_word(n, m, 1u));
+            poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, poll_spins,
+                              grad_shape_word(n, m, kG4 ? 2u : 1u));
         else poll_grad_loss(b, n, m, ws, mean_out, poll_spins);
         PCM_STAMP2(6);
         return;
@@ -1795,15 +1820,23 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         // argmin as a {tag, idx} granule and the workgroup's partial as a
         // {tag, sum} granule; the gradient phase sweeps the granules it needs
         const unsigned long long tag = (unsigned long long)(ws.epoch[0] + 1u) << 32;
-        if (!grad_ws_trusted(ws.epoch, b, n, m, 1u)) max_spins = 0u;  // granules of another shape: recompute
+        if (!grad_ws_trusted(ws.epoch, b, n, m, kG4 ? 2u : 1u)) max_spins = 0u;  // granules of another shape: recompute
+        // kG4: 4-byte argmin granules {tag (21 bits) << 11 | idx}, cloud 1 then
+        // cloud 2 (chamfer_lgrid.h's layout); the range's own argmins come
+        // from this workgroup's forward (no granule read)
+        const unsigned tag4 = ((ws.epoch[0] + 1u) & kLgTagMask) << 11;
+        unsigned *H1 = reinterpret_cast<unsigned *>(ws.ig) + (size_t)batch * n;
+        unsigned *H2 = reinterpret_cast<unsigned *>(ws.ig) + (size_t)b * n + (size_t)batch * m;
+        int myk = -1;
         unsigned long long *G1 = ws.ig + (size_t)batch * n, *G2 = ws.ig + (size_t)b * n + (size_t)batch * m;
         const PreDma pre{garena, X1, 12 * n, garena + 12 * kGradCap, X2, 12 * m};
         __shared__ pcm_f4 sQown[kLocal ? QW : 1];  // kLocal: the range's points (the forward's queries)
         const float my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
             first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
             first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
-            first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, first ? G1 : G2, tag,
-            kEarly ? &pre : nullptr, kLocal ? sQown : nullptr);
+            first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, kG4 ? nullptr : (first ? G1 : G2),
+            tag, kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, PcmLay{3, 1}, PcmLay{3, 1},
+            kG4 ? (first ? H1 : H2) : nullptr, tag4, kG4 ? &myk : nullptr);
         PCM_STAMP2(1);
         const float s = wave_sum(my_d);
         if (lane == 0) sRed[wave] = s;
@@ -1827,12 +1860,20 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
             // clouds as the timeout path's global fallback; the other cloud's
             // rows and the range's points from the forward's LDS
             const pcm_f4 *TA = reinterpret_cast<const pcm_f4 *>(arena);
-            ok = first ? range_grad<NT, QW, true, C>(true, q0, n, m, X1, X2, g1, g2, nullptr, nullptr, G,
-                                                     arena + kTileBytes, G1, G2, tag, max_spins,
-                                                     ws.epoch + kGradSlowWord, TA, sQown)
-                       : range_grad<NT, QW, true, C>(false, q0, m, n, X2, X1, g2, g1, nullptr, nullptr, G,
-                                                     arena + kTileBytes, G2, G1, tag, max_spins,
-                                                     ws.epoch + kGradSlowWord, TA, sQown);
+            if constexpr (kG4)
+                ok = first ? range_grad<NT, QW, true, C, true>(true, q0, n, m, X1, X2, g1, g2, nullptr, nullptr, G,
+                                                               arena + kTileBytes, H1, H2, tag4, max_spins,
+                                                               ws.epoch + kGradSlowWord, TA, sQown, myk)
+                           : range_grad<NT, QW, true, C, true>(false, q0, m, n, X2, X1, g2, g1, nullptr, nullptr, G,
+                                                               arena + kTileBytes, H2, H1, tag4, max_spins,
+                                                               ws.epoch + kGradSlowWord, TA, sQown, myk);
+            else
+                ok = first ? range_grad<NT, QW, true, C>(true, q0, n, m, X1, X2, g1, g2, nullptr, nullptr, G,
+                                                         arena + kTileBytes, G1, G2, tag, max_spins,
+                                                         ws.epoch + kGradSlowWord, TA, sQown)
+                           : range_grad<NT, QW, true, C>(false, q0, m, n, X2, X1, g2, g1, nullptr, nullptr, G,
+                                                         arena + kTileBytes, G2, G1, tag, max_spins,
+                                                         ws.epoch + kGradSlowWord, TA, sQown);
         } else {
             const float *P1 = reinterpret_cast<const float *>(garena);
             const float *P2 = P1 + 3 * kGradCap;
@@ -2007,6 +2048,9 @@ const GradVariant kGradVariants[] = {
     // 13: LDS grid per workgroup (chamfer_lgrid.h): each group of 64 spatially
     // sorted queries screens only the target cells around it
     {chamfer_loss_grad_lgrid_kernel, 8, 4},
+    // 14: 11 with 4-byte argmin granules and the range's own argmins taken
+    // from the forward (half the hand-off bytes, no own-range granule reads)
+    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true>, 8, 4},
 };
 // (round 4, rejected: 7 and 11 with 16 waves -- four per SIMD, a 16-way
 // merge -- 15.9-16.2 us against 13.85 us, profiles/r04/chamfer_w16_r04n_ab.txt)

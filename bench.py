@@ -13,9 +13,9 @@ The step runs as ONE launch of pcm_chamfer_loss_grad (forward, loss and both
 clouds' gradients; csrc/chamfer_filt.hip); --two-launch runs it as the fused-
 loss forward + the backward kernel instead (both are reported).
 At N=1 the timed region launches the step directly through the C ABI, once
-per step, with its arguments bound once (a native training loop's call; the
-host stays ahead of the ~14 us kernel, so the GPU runs the steps back to
-back).  tools/probe_replay.py measured the alternatives on MI355X: a replay of
+per step, from a C loop with the arguments bound once (a native training
+loop's calls; the host stays ahead of the ~14 us kernel, so the GPU runs the
+steps back to back).  tools/probe_replay.py measured the alternatives on MI355X: a replay of
 a 20-step hipGraph adds ~0.8 us per kernel node and ~16 us of replay floor,
 the Python wrapper per step ~0.5 us (r05c).  --graph times the 20-step graph
 instead (its first replay paid in warmup); --eager the Python wrapper.  The
@@ -211,13 +211,18 @@ class ChamferStep:
         st = pcm_hip._stream(self.xyz1.device)
         ci, cf, cs = ctypes.c_int, ctypes.c_float, ctypes.c_size_t
         if self.fused:
-            f = L.pcm_chamfer_loss_grad
+            # K steps = K calls of pcm_chamfer_loss_grad from one host call
+            # (csrc/chamfer_filt.hip pcm_tune_chamfer_loss_grad_repeat: a C
+            # loop over the public entry; ctypes costs ~17 us per call of 17
+            # arguments from Python, more than the kernel, r05e)
+            f = L.pcm_tune_chamfer_loss_grad_repeat
+            f.restype = ctypes.c_int
             args = (P(self.xyz1), P(self.xyz2), ci(B), ci(N), ci(M), cf(self.w1), cf(self.w2), P(self.d1), P(self.d2),
                     P(self.i1), P(self.i2), P(self.loss[0]), P(self.gx1), P(self.gx2), P(self.ws),
                     cs(self.ws.numel()), st)
 
-            def go():
-                if f(*args):
+            def go(k=1):
+                if f(ci(k), *args):
                     raise pcm_hip.PcmError("pcm_chamfer_loss_grad failed")
             return go
         f1, f2 = L.pcm_chamfer_forward_loss, L.pcm_chamfer_backward
@@ -226,9 +231,10 @@ class ChamferStep:
         a2 = (P(self.xyz1), P(self.xyz2), ci(B), ci(N), ci(M), P(self.g1), P(self.g2), P(self.i1), P(self.i2),
               P(self.gx1), P(self.gx2), st)
 
-        def go2():
-            if f1(*a1) or f2(*a2):
-                raise pcm_hip.PcmError("pcm_chamfer_forward_loss / pcm_chamfer_backward failed")
+        def go2(k=1):
+            for _ in range(k):
+                if f1(*a1) or f2(*a2):
+                    raise pcm_hip.PcmError("pcm_chamfer_forward_loss / pcm_chamfer_backward failed")
         return go2
 
     def reduce_losses(self, rows):
@@ -691,10 +697,10 @@ def main(argv=None):
                 go = step.launcher()
 
                 def run_steps(k):
-                    for _ in range(k):
-                        go()
-                mode = ("direct C-ABI launches, one per step, arguments bound once (a native loop; "
-                        "tools/probe_replay.py: a hipGraph replay adds ~0.8 us per kernel node on ROCm 7)")
+                    go(k)
+                mode = ("direct launches, one per step: a C loop over pcm_chamfer_loss_grad with its arguments "
+                        "bound once (tools/probe_replay.py: a hipGraph replay adds ~0.8 us per kernel node and a "
+                        "~16 us floor on ROCm 7; a ctypes call per step from Python is host-bound)")
         else:
             g_ar_many = g_ar_one = None
             if args.dist_backend == "nccl" and not args.eager_allreduce:

@@ -981,8 +981,9 @@ __device__ __forceinline__ float filt_forward_mfma(const float *__restrict__ Q, 
             sPC[quarter][s] = bchunk[qt];
         }
     }
-    __shared__ int sNFm[8];
-    const int any_nonfinite = pcm_wg_or(nonfinite, sNFm, 8);
+    static_assert(kMfmaNT / 64 == W, "one vote slot per wave of the MFMA forward");
+    __shared__ int sNFm[kMfmaNT / 64];
+    const int any_nonfinite = pcm_wg_or(nonfinite, sNFm, kMfmaNT / 64);
 
     float my_d = 0.f;
     if (!any_nonfinite) {

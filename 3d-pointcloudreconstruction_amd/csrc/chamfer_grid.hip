@@ -705,7 +705,14 @@ inline bool grid_pays(int b, int n, int m) {
 
 }  // namespace
 
+// 0 when the problem takes the dense kernels (no workspace used)
 extern "C" size_t pcm_chamfer_forward_ws_bytes(int b, int n, int m) {
+    if (bad_dims(b, n, m) || !grid_pays(b, n, m)) return 0;
+    return grid_layout(b, n, m).total;
+}
+
+// the grid path's workspace at any size (pcm_tune_chamfer_forward_grid)
+extern "C" size_t pcm_tune_chamfer_forward_grid_ws_bytes(int b, int n, int m) {
     if (bad_dims(b, n, m)) return 0;
     return grid_layout(b, n, m).total;
 }

@@ -103,6 +103,8 @@ def load_library():
         L.pcm_chamfer_forward_ws.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp]
         L.pcm_chamfer_forward_ws_f16.restype = ci
         L.pcm_chamfer_forward_ws_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp]
+        L.pcm_tune_chamfer_forward_grid_ws_bytes.restype = cs
+        L.pcm_tune_chamfer_forward_grid_ws_bytes.argtypes = [ci, ci, ci]
         L.pcm_tune_chamfer_forward_grid.restype = ci
         L.pcm_tune_chamfer_forward_grid.argtypes = [ci, vp, vp, ci, ci, ci, vp, vp, vp, vp, vp, cs, vp, vp]
         L.pcm_tune_chamfer_backward_f16.restype = ci
@@ -189,15 +191,22 @@ def _cloud_kind(xyz1, xyz2) -> str:
 GRID_MIN_POINTS = 4096
 
 
-def forward_workspace(dev: torch.device, b: int, n: int, m: int) -> torch.Tensor:
-    """Scratch for the grid forward (no state between calls, no zero-fill),
-    cached per (device, current stream, size) like chamfer_workspace."""
-    need = int(load_library().pcm_chamfer_forward_ws_bytes(b, n, m))
-    key = ("forward", dev, _stream_id(dev), need)
+def forward_workspace(dev: torch.device, b: int, n: int, m: int, force_grid: bool = False):
+    """Scratch for the grid forward (no state between calls, no zero-fill):
+    None when the problem takes the dense kernels (pcm_chamfer_forward_ws_bytes
+    is 0), else ONE buffer per (device, current stream), grown when a larger
+    problem needs more (it holds nothing between calls).  force_grid: the
+    size the grid path needs at any problem size (tune_chamfer_forward_grid)."""
+    L = load_library()
+    need = int(L.pcm_tune_chamfer_forward_grid_ws_bytes(b, n, m) if force_grid
+               else L.pcm_chamfer_forward_ws_bytes(b, n, m))
+    if need == 0:
+        return None
+    key = ("forward", dev, _stream_id(dev))
     ws = _ws_cache.get(key)
-    if ws is None:
+    if ws is None or ws.numel() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=dev)
-        _ws_cache[key] = ws
+        _cache_put(key, ws)
     return ws
 
 
@@ -252,9 +261,9 @@ def chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:
     f16 = _cloud_kind(xyz1, xyz2) == "f16"
     L = load_library()
     with torch.cuda.device(dev):
-        if n >= GRID_MIN_POINTS and m >= GRID_MIN_POINTS and b > 0:
+        ws = forward_workspace(dev, b, n, m) if (n >= GRID_MIN_POINTS and m >= GRID_MIN_POINTS and b > 0) else None
+        if ws is not None:  # the grid forward pays at this size (csrc/chamfer_grid.hip grid_pays)
             fn = "pcm_chamfer_forward_ws_f16" if f16 else "pcm_chamfer_forward_ws"
-            ws = forward_workspace(dev, b, n, m)
             _check(getattr(L, fn)(
                 _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
                 _ptr(ws), ws.numel(), _stream(dev)), fn)
@@ -280,7 +289,7 @@ def tune_chamfer_forward_grid(xyz1, xyz2, dist1, dist2, idx1, idx2, scan="filter
     mode = int(f16) | {"filter": 0, "screened": 64, "exact": 2}[scan] | {None: 0, "build": 4, "search": 8}[only]
     mode |= (16 if small_wg else 0) | (32 if reg_gather else 0)
     with torch.cuda.device(dev):
-        ws = workspace if workspace is not None else forward_workspace(dev, b, n, m)
+        ws = workspace if workspace is not None else forward_workspace(dev, b, n, m, force_grid=True)
         _check(load_library().pcm_tune_chamfer_forward_grid(
             mode, _ptr(xyz1), _ptr(xyz2), b, n, m, _ptr(dist1), _ptr(dist2), _ptr(idx1), _ptr(idx2),
             _ptr(ws), ws.numel(), _stream(dev), _ptr(stats)), "pcm_tune_chamfer_forward_grid")
@@ -301,7 +310,18 @@ def tune_num_chamfer_f16_variants() -> int:
     return int(load_library().pcm_tune_num_chamfer_f16_variants())
 
 
-_ws_cache = {}
+# cached device workspaces: an LRU of at most _WS_CACHE_MAX buffers (the
+# fused-loss workspaces are per shape; the grid forward's one per stream)
+_ws_cache = collections.OrderedDict()
+_WS_CACHE_MAX = 16
+
+
+def _cache_put(key, ws):
+    _ws_cache[key] = ws
+    _ws_cache.move_to_end(key)
+    while len(_ws_cache) > _WS_CACHE_MAX:
+        old_key, _ = _ws_cache.popitem(last=False)
+        _watches.pop(old_key, None)
 
 
 def _stream_id(dev: torch.device) -> int:
@@ -310,14 +330,19 @@ def _stream_id(dev: torch.device) -> int:
 
 def chamfer_workspace(dev: torch.device, b: int, n: int, m: int) -> torch.Tensor:
     """Zero-filled workspace for the fused-loss kernels, cached per (device,
-    current stream, size): the kernels keep cross-launch state in it (epoch,
-    arrival counters), so only stream-ordered calls may share one."""
+    current stream, shape): the kernels keep cross-launch state in it (epoch,
+    arrival counters, argmin granules), so only stream-ordered calls may share
+    one; one per shape keeps every call's granules trusted (a workspace last
+    used by another shape makes the next call recompute its argmins,
+    csrc/chamfer_filt.hip kGradShapeWord)."""
     need = int(load_library().pcm_chamfer_workspace_bytes(b, n, m))
-    key = ("chamfer", dev, _stream_id(dev), need)
+    key = ("chamfer", dev, _stream_id(dev), b, n, m)
     ws = _ws_cache.get(key)
     if ws is None:
         ws = torch.zeros(need, dtype=torch.uint8, device=dev)
-        _ws_cache[key] = ws
+        _cache_put(key, ws)
+    else:
+        _ws_cache.move_to_end(key)
     return ws
 
 
@@ -380,9 +405,9 @@ def _watched_workspace(dev, b, n, m):
     ws = chamfer_workspace(dev, b, n, m)
     if torch.cuda.is_current_stream_capturing():
         return ws, None
-    key = (ws.data_ptr(), b, n, m)
+    key = ("chamfer", dev, _stream_id(dev), b, n, m)
     w = _watches.get(key)
-    if w is None:
+    if w is None or w.ws is not ws:
         w = _watches[key] = _StickyWatch(ws, b, n, m)
     w.check()
     return ws, w
@@ -570,11 +595,11 @@ def emd_workspace(dev: torch.device, b: int, n: int) -> torch.Tensor:
     entry is irrelevant, but a call's auction state lives in it until the call
     ends, so concurrent calls on different streams get different buffers."""
     ws_bytes = max(emd_workspace_bytes(b, n), 1)
-    key = ("emd", dev, _stream_id(dev), ws_bytes)
+    key = ("emd", dev, _stream_id(dev))
     ws = _ws_cache.get(key)
-    if ws is None:
+    if ws is None or ws.numel() < ws_bytes:  # one per (device, stream), grown when needed
         ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
-        _ws_cache[key] = ws
+        _cache_put(key, ws)
     return ws
 
 
@@ -644,11 +669,11 @@ def emd_backward(xyz1, xyz2, graddist, assignment, gradxyz1) -> None:
 def _nn_workspace(dev, b: int, m: int):
     """Cached workspace for the screening rows (content on entry irrelevant)."""
     need = max(int(load_library().pcm_icp_workspace_bytes(b, m)), 1)
-    key = ("nn", dev, need)
+    key = ("nn", dev, _stream_id(dev))
     ws = _ws_cache.get(key)
-    if ws is None:
+    if ws is None or ws.numel() < need:
         ws = torch.empty(need, dtype=torch.uint8, device=dev)
-        _ws_cache[key] = ws
+        _cache_put(key, ws)
     return ws
 
 

@@ -356,8 +356,9 @@ def test_backward_f16_is_rounded_fp32_gradient(cuda, oracle, b, n, m, seed):
 
 @pytest.mark.parametrize("b,n,m,collapse", [(2, 4100, 5000, False), (2, 4096, 4096, True), (3, 700, 900, False)])
 def test_backward_f16_variants_identical(cuda, oracle, b, n, m, collapse):
-    # 256- and 1024-target workgroups; a collapsed prediction overflows the
-    # LDS sort (every source on one target) and takes the ordered scan
+    # 256- and 1024-target workgroups; a collapsed prediction puts all 4096
+    # sources on one target: exactly the 256-target kernel's kBwdCap (it still
+    # fits; test_backward_bucket_overflow_ordered_scan goes past both caps)
     import pcm_hip
     a, c = _clouds(95, b, n, m)
     if collapse:
@@ -870,4 +871,34 @@ def test_channel_plane_layout_capi(cuda, oracle):
     r1, r2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), 0.25, np.float32),
                                      np.full((b, m), 0.5, np.float32), ref[2], ref[3])
     np.testing.assert_array_equal(gx1.transpose(1, 2).cpu().contiguous().numpy().view(np.int32), r1.view(np.int32))
+    np.testing.assert_array_equal(gx2.cpu().numpy().view(np.int32), r2.view(np.int32))
+
+
+@pytest.mark.parametrize("b,n,m,variant", [
+    (2, 300, 4097, 1),    # 256-target workgroups: 4097 sources on one target > kBwdCap 4096
+    (1, 4096, 8193, 3),   # 1024-target workgroups: 8193 sources on one target > kBwdWideCap 8192
+])
+def test_backward_bucket_overflow_ordered_scan(cuda, oracle, b, n, m, variant):
+    # a collapsed cloud 2 sends every one of its points to one cloud-1 target,
+    # beyond the workgroup's sortable entries: the ordered-scan fallback
+    # (chamfer.hip chamfer_bwd_kernel, !fits) must give the oracle's bits
+    import pcm_hip
+    a, c = _clouds(63, b, n, m)
+    c[:, :, :] = c[:, :1, :]
+    x1, x2 = a.to(cuda), c.to(cuda)
+    d1 = torch.empty(b, n, device=cuda)
+    d2 = torch.empty(b, m, device=cuda)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+    pcm_hip.chamfer_forward(x1, x2, d1, d2, i1, i2)
+    assert (i2 == i2[:, :1]).all()  # one target draws all m sources
+    gen = torch.Generator().manual_seed(64)
+    g1 = torch.rand(b, n, generator=gen).to(cuda)
+    g2 = torch.rand(b, m, generator=gen).to(cuda)
+    gx1 = torch.full((b, n, 3), float("nan"), device=cuda)
+    gx2 = torch.full((b, m, 3), float("nan"), device=cuda)
+    pcm_hip.tune_chamfer_backward(variant, x1, x2, g1, g2, i1, i2, gx1, gx2)
+    r1, r2 = oracle.chamfer_backward(a.numpy(), c.numpy(), g1.cpu().numpy(), g2.cpu().numpy(),
+                                     i1.cpu().numpy(), i2.cpu().numpy())
+    np.testing.assert_array_equal(gx1.cpu().numpy().view(np.int32), r1.view(np.int32))
     np.testing.assert_array_equal(gx2.cpu().numpy().view(np.int32), r2.view(np.int32))

@@ -55,7 +55,8 @@ for S in "$@"; do
                python -u tools/stamp_filt.py fused 7 11 > "$O/stamps_fused.txt" 2>&1 ;;
     stampslg) timeout -k 10 300 python -u tools/stamp_lgrid.py 13 > "$O/stamps_lgrid.txt" 2>&1 &&
               timeout -k 10 300 python -u tools/stamp_lgrid.py 11 >> "$O/stamps_lgrid.txt" 2>&1 ;;
-    probe) timeout -k 10 300 python -u tools/probe_replay.py > "$O/probe_replay.txt" 2>&1 ;;
+    probe) timeout -k 10 300 python -u tools/probe_replay.py > "$O/probe_replay.txt" 2>&1 &&
+           timeout -k 10 300 python -u tools/probe_timed.py > "$O/probe_timed.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac
     rc=$?

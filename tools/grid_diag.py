@@ -25,7 +25,7 @@ def main():
         d1, d2 = torch.empty(b, n, device=dev), torch.empty(b, m, device=dev)
         i1 = torch.empty(b, n, dtype=torch.int32, device=dev)
         i2 = torch.empty(b, m, dtype=torch.int32, device=dev)
-        ws = pcm_hip.forward_workspace(dev, b, n, m)
+        ws = pcm_hip.forward_workspace(dev, b, n, m, force_grid=True)
         waves = b * ((n + 63) // 64 + (m + 63) // 64)
         st_all = torch.zeros(waves * 4 + waves * 8, dtype=torch.int32, device=dev)
         pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, stats=st_all, workspace=ws)

@@ -631,6 +631,13 @@ __device__ inline int block_exclusive_scan(int v, int *wave_tot) {
     return before + x - v;
 }
 
+// graddist element strides per direction (batch, point), read in place: an
+// expanded scalar (stride 0, what torch.mean's backward hands over) needs no
+// materialising copy.  bs < 0: contiguous [b, n].
+struct PcmGdStr {
+    int bs1 = -1, ps1 = 1, bs2 = -1, ps2 = 1;
+};
+
 // NT targets per workgroup (= threads): every workgroup reads the whole
 // other direction's argmins, so large clouds take NT = 1024 (4x less of that)
 template <typename TIn, int NT = kBwdT, int CAP = kBwdCap>
@@ -638,7 +645,7 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
     const TIn *__restrict__ xyz1, const TIn *__restrict__ xyz2, int b, int n, int m,
     const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
     const int32_t *__restrict__ idx2, TIn *__restrict__ grad1, TIn *__restrict__ grad2,
-    int nblk1, int nblk2, int lay1 = 0, int lay2 = 0) {
+    int nblk1, int nblk2, int lay1 = 0, int lay2 = 0, PcmGdStr GS = PcmGdStr()) {
     __shared__ int sCnt[NT];
     __shared__ int sOff[NT + 1];
     __shared__ int sTmp[CAP];
@@ -653,15 +660,17 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
     const float *gds, *gdo;
     const int32_t *ids, *ido;
     TIn *grad;
-    int ns, no, blk;
+    int ns, no, blk, gps, gpo;
     bool direct_first;
     if (bid < b * nblk1) {
         const int batch = bid / nblk1;
         blk = bid - batch * nblk1;
         self = xyz1 + (size_t)batch * n * 3;
         other = xyz2 + (size_t)batch * m * 3;
-        gds = gd1 + (size_t)batch * n;
-        gdo = gd2 + (size_t)batch * m;
+        gds = gd1 + (size_t)batch * (GS.bs1 < 0 ? n : GS.bs1);
+        gdo = gd2 + (size_t)batch * (GS.bs2 < 0 ? m : GS.bs2);
+        gps = GS.ps1;
+        gpo = GS.ps2;
         ids = idx1 + (size_t)batch * n;
         ido = idx2 + (size_t)batch * m;
         grad = grad1 + (size_t)batch * n * 3;
@@ -674,8 +683,10 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
         blk = bid - batch * nblk2;
         self = xyz2 + (size_t)batch * m * 3;
         other = xyz1 + (size_t)batch * n * 3;
-        gds = gd2 + (size_t)batch * m;
-        gdo = gd1 + (size_t)batch * n;
+        gds = gd2 + (size_t)batch * (GS.bs2 < 0 ? m : GS.bs2);
+        gdo = gd1 + (size_t)batch * (GS.bs1 < 0 ? n : GS.bs1);
+        gps = GS.ps2;
+        gpo = GS.ps1;
         ids = idx2 + (size_t)batch * m;
         ido = idx1 + (size_t)batch * n;
         grad = grad2 + (size_t)batch * m * 3;
@@ -698,7 +709,7 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
         sy = pcm_ld(self + pcm_at(LS, i, 1));
         sz = pcm_ld(self + pcm_at(LS, i, 2));
         const int k = ids[i];
-        const float g = __fmul_rn(gds[i], 2.f);
+        const float g = __fmul_rn(gds[(size_t)i * gps], 2.f);
         dir0 = __fmul_rn(g, __fsub_rn(sx, pcm_ld(other + pcm_at(LO, k, 0))));
         dir1 = __fmul_rn(g, __fsub_rn(sy, pcm_ld(other + pcm_at(LO, k, 1))));
         dir2 = __fmul_rn(g, __fsub_rn(sz, pcm_ld(other + pcm_at(LO, k, 2))));
@@ -752,7 +763,7 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
         az = __fadd_rn(az, dir2);
     }
     auto scatter = [&](int j) {
-        const float g = __fmul_rn(gdo[j], 2.f);
+        const float g = __fmul_rn(gdo[(size_t)j * gpo], 2.f);
         ax = __fadd_rn(ax, -__fmul_rn(g, __fsub_rn(pcm_ld(other + pcm_at(LO, j, 0)), sx)));
         ay = __fadd_rn(ay, -__fmul_rn(g, __fsub_rn(pcm_ld(other + pcm_at(LO, j, 1)), sy)));
         az = __fadd_rn(az, -__fmul_rn(g, __fsub_rn(pcm_ld(other + pcm_at(LO, j, 2)), sz)));
@@ -936,7 +947,7 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
     const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
     const int32_t *__restrict__ idx2, float *__restrict__ grad1, float *__restrict__ grad2,
-    int nblk1, int nblk2, int lay1 = 0, int lay2 = 0) {
+    int nblk1, int nblk2, int lay1 = 0, int lay2 = 0, PcmGdStr GS = PcmGdStr()) {
     __shared__ __attribute__((aligned(16))) float sO[3 * kBwdStageMax];   // other cloud, AoS
     __shared__ __attribute__((aligned(16))) float sG[kBwdStageMax];       // other graddist
     __shared__ __attribute__((aligned(16))) int sK[kBwdStageMax];         // other argmins
@@ -952,15 +963,17 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
     const float *self, *other, *gds, *gdo;
     const int32_t *ids, *ido;
     float *grad;
-    int ns, no, blk;
+    int ns, no, blk, gps, gpo;
     bool direct_first;
     if (bid < b * nblk1) {
         const int batch = bid / nblk1;
         blk = bid - batch * nblk1;
         self = xyz1 + (size_t)batch * n * 3;
         other = xyz2 + (size_t)batch * m * 3;
-        gds = gd1 + (size_t)batch * n;
-        gdo = gd2 + (size_t)batch * m;
+        gds = gd1 + (size_t)batch * (GS.bs1 < 0 ? n : GS.bs1);
+        gdo = gd2 + (size_t)batch * (GS.bs2 < 0 ? m : GS.bs2);
+        gps = GS.ps1;
+        gpo = GS.ps2;
         ids = idx1 + (size_t)batch * n;
         ido = idx2 + (size_t)batch * m;
         grad = grad1 + (size_t)batch * n * 3;
@@ -973,8 +986,10 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
         blk = bid - batch * nblk2;
         self = xyz2 + (size_t)batch * m * 3;
         other = xyz1 + (size_t)batch * n * 3;
-        gds = gd2 + (size_t)batch * m;
-        gdo = gd1 + (size_t)batch * n;
+        gds = gd2 + (size_t)batch * (GS.bs2 < 0 ? m : GS.bs2);
+        gdo = gd1 + (size_t)batch * (GS.bs1 < 0 ? n : GS.bs1);
+        gps = GS.ps2;
+        gpo = GS.ps1;
         ids = idx2 + (size_t)batch * m;
         ido = idx1 + (size_t)batch * n;
         grad = grad2 + (size_t)batch * m * 3;
@@ -992,7 +1007,10 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
 
     pcm_dma_to_lds(sK, ido, 4 * no, wave, kBwdT / 64);
     pcm_dma_to_lds(sO, other, 12 * no, wave, kBwdT / 64);
-    pcm_dma_to_lds(sG, gdo, 4 * no, wave, kBwdT / 64);
+    if (gpo == 1)
+        pcm_dma_to_lds(sG, gdo, 4 * no, wave, kBwdT / 64);
+    else
+        for (int j = threadIdx.x; j < no; j += kBwdT) sG[j] = gdo[(size_t)j * gpo];
 
     const int i = t0 + tid;
     const bool own = tid < T;
@@ -1003,7 +1021,7 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
         sy = self[pcm_at(LS, i, 1)];
         sz = self[pcm_at(LS, i, 2)];
         kself = ids[i];
-        gself = gds[i];
+        gself = gds[(size_t)i * gps];
     }
     sCnt[tid] = 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1108,7 +1126,10 @@ constexpr int kDefaultLossMode = 3;  // tools/tune_chamfer.py (profiles/r01): mo
 // Round 2 (near-tie scans split over the waves, DPP reductions): the
 // filtered W=8 QPT=4 C=32 form leads at config 2 as well -- 11.96 us against
 // 12.45 us for the SGPR form -- so it is the default at every size.
-inline int default_fwd_variant(int, int) { return kNumBaseFwdVariants + 3; }
+// Round 5 (tools/ab_ref_call.py, profiles/r05): clouds of at most 1024 points
+// take the one-launch step's geometry, C 16 with 1024-point tiles -- 11.07
+// against 11.43 us at config 2, bit-identical.
+inline int default_fwd_variant(int n, int m) { return kNumBaseFwdVariants + ((n <= 1024 && m <= 1024) ? 8 : 3); }
 
 int fwd_grid(const FwdVariant &v, int b, int n, int m, int &nblk1, int &nblk2, long long &blocks) {
     const int QW = 64 * v.qpt;
@@ -1245,7 +1266,8 @@ inline bool wide_bwd(int n, int m) { return n >= 4096 && m >= 4096; }
 
 int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
                const float *graddist1, const float *graddist2, const int32_t *idx1,
-               const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream, int lay1 = 0, int lay2 = 0) {
+               const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream, int lay1 = 0, int lay2 = 0,
+               PcmGdStr GS = PcmGdStr()) {
     if (bad_dims(b, n, m)) return PCM_ERR_INVALID_ARG;
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     // Without targets a direction has no argmins; the reference would read
@@ -1260,17 +1282,19 @@ int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
     if (variant == 0 && n <= kBwdStageMax && m <= kBwdStageMax) {
         hipLaunchKernelGGL(chamfer_bwd_staged_kernel, dim3((unsigned)blocks), dim3(kBwdT), 0,
                            (hipStream_t)stream, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1,
-                           idx2, gradxyz1, gradxyz2, nblk1, nblk2, lay1, lay2);
+                           idx2, gradxyz1, gradxyz2, nblk1, nblk2, lay1, lay2, GS);
         return pcm_launch_status();
     }
-    if (lay1 != 0 || lay2 != 0) {  // channel planes: the staged kernel's layout, else the global-memory kernel's
+    const bool strided = GS.bs1 >= 0 || GS.bs2 >= 0 || GS.ps1 != 1 || GS.ps2 != 1;
+    if (lay1 != 0 || lay2 != 0 || (strided && !wide_bwd(n, m))) {
+        // channel planes or strided graddists: the staged kernel's forms, else the global-memory kernel's
         hipLaunchKernelGGL(chamfer_bwd_kernel<float>, dim3((unsigned)blocks), dim3(kBwdT), 0, (hipStream_t)stream,
                            xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2, nblk1, nblk2,
-                           lay1, lay2);
+                           lay1, lay2, GS);
         return pcm_launch_status();
     }
     const size_t lds = bwd_lds_bytes(n, m);
-    if (variant == 2 && lds <= kBwdLdsMax) {
+    if (variant == 2 && lds <= kBwdLdsMax && !strided) {
         if (lds > 64 * 1024 &&
             hipFuncSetAttribute((const void *)chamfer_bwd_lds_kernel,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
@@ -1284,7 +1308,7 @@ int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
         const int w1 = (n + kBwdWideT - 1) / kBwdWideT, w2 = (m + kBwdWideT - 1) / kBwdWideT;
         hipLaunchKernelGGL((chamfer_bwd_kernel<float, kBwdWideT, kBwdWideCap>), dim3((unsigned)(b * (w1 + w2))),
                            dim3(kBwdWideT), 0, (hipStream_t)stream, xyz1, xyz2, b, n, m, graddist1, graddist2,
-                           idx1, idx2, gradxyz1, gradxyz2, w1, w2);
+                           idx1, idx2, gradxyz1, gradxyz2, w1, w2, 0, 0, GS);
         return pcm_launch_status();
     }
     hipLaunchKernelGGL(chamfer_bwd_kernel<float>, dim3((unsigned)blocks), dim3(kBwdT), 0,
@@ -1309,6 +1333,27 @@ extern "C" int pcm_chamfer_backward_layout(const float *xyz1, const float *xyz2,
     if ((unsigned)layout1 > 1u || (unsigned)layout2 > 1u) return PCM_ERR_INVALID_ARG;
     return launch_bwd(0, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2, stream, layout1,
                       layout2);
+}
+
+extern "C" int pcm_chamfer_backward_strided(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1,
+                                            int layout2, const float *graddist1, long long gd1_batch_stride,
+                                            long long gd1_point_stride, const float *graddist2,
+                                            long long gd2_batch_stride, long long gd2_point_stride,
+                                            const int32_t *idx1, const int32_t *idx2, float *gradxyz1,
+                                            float *gradxyz2, void *stream) {
+    if ((unsigned)layout1 > 1u || (unsigned)layout2 > 1u) return PCM_ERR_INVALID_ARG;
+    const long long lim = 0x7fffffffLL;
+    if (gd1_batch_stride < 0 || gd1_point_stride < 0 || gd2_batch_stride < 0 || gd2_point_stride < 0 ||
+        gd1_batch_stride > lim || gd1_point_stride > lim || gd2_batch_stride > lim || gd2_point_stride > lim)
+        return PCM_ERR_INVALID_ARG;
+    PcmGdStr GS;  // contiguous graddists keep the default (unstrided) routing
+    const bool c1 = gd1_point_stride == 1 && gd1_batch_stride == n, c2 = gd2_point_stride == 1 && gd2_batch_stride == m;
+    GS.bs1 = c1 ? -1 : (int)gd1_batch_stride;
+    GS.ps1 = c1 ? 1 : (int)gd1_point_stride;
+    GS.bs2 = c2 ? -1 : (int)gd2_batch_stride;
+    GS.ps2 = c2 ? 1 : (int)gd2_point_stride;
+    return launch_bwd(0, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2, stream, layout1,
+                      layout2, GS);
 }
 
 extern "C" int pcm_tune_chamfer_backward(int variant, const float *xyz1, const float *xyz2, int b,

@@ -2010,6 +2010,7 @@ const PcmFwdVariant kPcmFiltVariants[] = {
     PCM_FWD_FILT(16, 2, 16, 2048),  // base + 5
     PCM_FWD_FILT(8, 4, 16, 4096),   // base + 6
     PCM_FWD_FILT(8, 8, 16, 2048),   // base + 7
+    PCM_FWD_FILT(8, 4, 16, 1024),   // base + 8: the one-launch step's geometry (fused variant 11)
 };
 const int kPcmNumFiltVariants = sizeof(kPcmFiltVariants) / sizeof(kPcmFiltVariants[0]);
 
@@ -2157,24 +2158,48 @@ extern "C" int pcm_tune_chamfer_loss_grad_repeat(int reps, const float *xyz1, co
     return PCM_OK;
 }
 
-extern "C" int pcm_chamfer_forward_layout(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1,
-                                          int layout2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
-                                          void *stream) {
-    if (b < 0 || n < 0 || m < 0 || (unsigned)layout1 > 1u || (unsigned)layout2 > 1u) return PCM_ERR_INVALID_ARG;
-    if (layout1 == 0 && layout2 == 0) return pcm_chamfer_forward(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, stream);
+namespace {
+// variant 0: the filtered geometry of larger clouds (W 8, QPT 4, C 32, 2048-point tiles); 1: that of clouds of
+// <= 1024 points and of the one-launch step (C 16, 1024-point tiles), as chamfer.hip default_fwd_variant picks
+int launch_fwd_layout(int variant, const float *xyz1, const float *xyz2, int b, int n, int m, int layout1, int layout2,
+                      float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, void *stream) {
+    if (b < 0 || n < 0 || m < 0 || (unsigned)layout1 > 1u || (unsigned)layout2 > 1u || (unsigned)variant > 1u)
+        return PCM_ERR_INVALID_ARG;
+    if (layout1 == 0 && layout2 == 0 && variant == 0)
+        return pcm_chamfer_forward(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, stream);
     if (b == 0 || (n == 0 && m == 0)) return PCM_OK;
     if ((n > 0 && (!xyz1 || !dist1 || !idx1)) || (m > 0 && (!xyz2 || !dist2 || !idx2))) return PCM_ERR_INVALID_ARG;
-    // the default filtered variant's geometry (chamfer.hip default_fwd_variant: W 8, QPT 4, C 32)
     constexpr int W = 8, QPT = 4, QW = 64 * QPT;
     const int nblk1 = m > 0 ? (n + QW - 1) / QW : 0;  // a direction without targets keeps its outputs
     const int nblk2 = n > 0 ? (m + QW - 1) / QW : 0;
     const long long blocks = (long long)b * (nblk1 + nblk2);
     if (blocks > 0x7ffffffeLL) return PCM_ERR_UNSUPPORTED;
     if (blocks == 0) return PCM_OK;
-    hipLaunchKernelGGL((chamfer_fwd_filt_lay_kernel<W, QPT, 32, 2048>), dim3((unsigned)blocks), dim3(64 * W), 0,
-                       (hipStream_t)stream, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nblk1, nblk2, layout1,
-                       layout2);
+    if (variant == 0)
+        hipLaunchKernelGGL((chamfer_fwd_filt_lay_kernel<W, QPT, 32, 2048>), dim3((unsigned)blocks), dim3(64 * W), 0,
+                           (hipStream_t)stream, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nblk1, nblk2, layout1,
+                           layout2);
+    else
+        hipLaunchKernelGGL((chamfer_fwd_filt_lay_kernel<W, QPT, 16, 1024>), dim3((unsigned)blocks), dim3(64 * W), 0,
+                           (hipStream_t)stream, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nblk1, nblk2, layout1,
+                           layout2);
     return pcm_launch_status();
+}
+}  // namespace
+
+extern "C" int pcm_chamfer_forward_layout(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1,
+                                          int layout2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                                          void *stream) {
+    // the geometry chamfer.hip default_fwd_variant picks for the rows
+    const int v = (n <= 1024 && m <= 1024) ? 1 : 0;
+    if (layout1 == 0 && layout2 == 0) return pcm_chamfer_forward(xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, stream);
+    return launch_fwd_layout(v, xyz1, xyz2, b, n, m, layout1, layout2, dist1, dist2, idx1, idx2, stream);
+}
+
+extern "C" int pcm_tune_chamfer_forward_layout(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
+                                               int layout1, int layout2, float *dist1, float *dist2, int32_t *idx1,
+                                               int32_t *idx2, void *stream) {
+    return launch_fwd_layout(variant, xyz1, xyz2, b, n, m, layout1, layout2, dist1, dist2, idx1, idx2, stream);
 }
 
 // the default variant with given bounds on the gradient-phase waits

@@ -138,7 +138,10 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
     __shared__ float red[7][kW];
     __shared__ int sSlab[kSlabMax];
     __shared__ int sw[2][kW];
-    const int c = blockIdx.x / kSlabMax, slab = blockIdx.x % kSlabMax;
+    // a cloud's slab workgroups share one XCD (pcm_xcd_remap): the cloud they
+    // all read twice is fetched into that L2 only, not into all eight
+    const int L = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
+    const int c = L / kSlabMax, slab = L % kSlabMax;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const bool two = c >= b;
     const int e = two ? c - b : c, np = two ? m : n;

@@ -10,6 +10,9 @@ extern "C" {
 int pcm_tune_num_chamfer_variants(void);
 int pcm_tune_chamfer_forward(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
                              float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, void *stream);
+int pcm_tune_chamfer_forward_layout(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
+                                    int layout1, int layout2, float *dist1, float *dist2, int32_t *idx1,
+                                    int32_t *idx2, void *stream);
 int pcm_tune_chamfer_backward(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
                               const float *graddist1, const float *graddist2, const int32_t *idx1,
                               const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream);

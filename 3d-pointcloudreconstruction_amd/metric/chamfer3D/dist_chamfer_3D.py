@@ -78,23 +78,33 @@ class chamfer_3DFunction(Function):
     @staticmethod
     def backward(ctx, graddist1, graddist2, gradidx1, gradidx2):
         xyz1, xyz2, idx1, idx2 = ctx.saved_tensors
+        lay = ctx.layouts
+        if xyz1.dtype == torch.float32:
+            # graddists are read in place at their strides: torch.mean's
+            # backward hands an expanded scalar (stride 0), which the
+            # reference's .contiguous() (dist_chamfer_3D.py:59-60) copied out
+            lay = lay or (0, 0)
+            gradxyz1, gradxyz2 = _empty_like_layout(xyz1, lay[0]), _empty_like_layout(xyz2, lay[1])
+            pcm_hip.chamfer_backward_strided(xyz1, xyz2, lay[0], lay[1], _graddist(graddist1, idx1),
+                                             _graddist(graddist2, idx2), idx1, idx2, gradxyz1, gradxyz2)
+            return gradxyz1, gradxyz2
         # autograd hands None for an unused output
         graddist1 = (torch.zeros_like(idx1, dtype=torch.float32) if graddist1 is None
                      else graddist1.contiguous().float())
         graddist2 = (torch.zeros_like(idx2, dtype=torch.float32) if graddist2 is None
                      else graddist2.contiguous().float())
-        lay = ctx.layouts
-        if lay is None:
-            gradxyz1 = torch.empty_like(xyz1)
-            gradxyz2 = torch.empty_like(xyz2)
-            pcm_hip.chamfer_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
-        else:
-            # each gradient in its cloud's layout: for channel planes the
-            # transpose's backward then hands autograd a contiguous [B, 3, N]
-            gradxyz1, gradxyz2 = _empty_like_layout(xyz1, lay[0]), _empty_like_layout(xyz2, lay[1])
-            pcm_hip.chamfer_backward_layout(xyz1, xyz2, lay[0], lay[1], graddist1, graddist2, idx1, idx2,
-                                            gradxyz1, gradxyz2)
+        gradxyz1 = torch.empty_like(xyz1)
+        gradxyz2 = torch.empty_like(xyz2)
+        pcm_hip.chamfer_backward(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
         return gradxyz1, gradxyz2
+
+
+def _graddist(g, idx):
+    """A float32 [B, N] graddist at whatever strides it came with; None (an
+    unused output) is an expanded zero."""
+    if g is None:
+        return torch.zeros((), dtype=torch.float32, device=idx.device).expand(idx.shape)
+    return g if g.dtype == torch.float32 else g.float()
 
 
 def _layouts(xyz1, xyz2):

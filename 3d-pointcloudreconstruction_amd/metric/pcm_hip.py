@@ -29,6 +29,7 @@ EXPORTED = (
     "pcm_chamfer_forward_f16", "pcm_chamfer_backward_f16",
     "pcm_chamfer_forward_ws_bytes", "pcm_chamfer_forward_ws", "pcm_chamfer_forward_ws_f16",
     "pcm_chamfer_loss_grad", "pcm_chamfer_forward_layout", "pcm_chamfer_backward_layout",
+    "pcm_chamfer_backward_strided",
     "pcm_icp_workspace_bytes", "pcm_icp", "pcm_icp_workspace_status", "pcm_nearest_neighbor",
     "pcm_best_fit_transform",
     "pcm_npy_cloud_points", "pcm_npy_load_clouds",
@@ -92,6 +93,11 @@ def load_library():
         L.pcm_chamfer_forward_layout.argtypes = [vp, vp, ci, ci, ci, ci, ci, vp, vp, vp, vp, vp]
         L.pcm_chamfer_backward_layout.restype = ci
         L.pcm_chamfer_backward_layout.argtypes = [vp, vp, ci, ci, ci, ci, ci, vp, vp, vp, vp, vp, vp, vp]
+    if hasattr(L, "pcm_chamfer_backward_strided"):
+        ll = ctypes.c_longlong
+        L.pcm_chamfer_backward_strided.restype = ci
+        L.pcm_chamfer_backward_strided.argtypes = [vp, vp, ci, ci, ci, ci, ci, vp, ll, ll, vp, ll, ll, vp, vp, vp,
+                                                   vp, vp]
     L.pcm_chamfer_forward_f16.restype = ci
     L.pcm_chamfer_forward_f16.argtypes = [vp, vp, ci, ci, ci, vp, vp, vp, vp, vp]
     L.pcm_chamfer_backward_f16.restype = ci
@@ -248,6 +254,23 @@ def chamfer_backward_layout(xyz1, xyz2, lay1, lay2, graddist1, graddist2, idx1, 
         _check(load_library().pcm_chamfer_backward_layout(
             _ptr(xyz1), _ptr(xyz2), b, n, m, int(lay1), int(lay2), _ptr(graddist1), _ptr(graddist2), _ptr(idx1),
             _ptr(idx2), _ptr(gradxyz1), _ptr(gradxyz2), _stream(dev)), "pcm_chamfer_backward_layout")
+
+
+def chamfer_backward_strided(xyz1, xyz2, lay1, lay2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2) -> None:
+    """pcm_chamfer_backward_strided: float32 [B, N] graddists read in place at
+    their own strides (an expanded scalar included); gradients in their cloud's
+    layout (lay 0 rows, 1 channel planes)."""
+    dev = _require_device(xyz1, xyz2, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2)
+    b, n, _ = xyz1.shape
+    m = xyz2.shape[1]
+    for g, k in ((graddist1, n), (graddist2, m)):
+        if g.dtype != torch.float32 or tuple(g.shape) != (b, k):
+            raise ValueError("chamfer_backward_strided takes float32 graddists of shape [B, N] and [B, M]")
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_chamfer_backward_strided(
+            _ptr(xyz1), _ptr(xyz2), b, n, m, int(lay1), int(lay2), _ptr(graddist1), graddist1.stride(0),
+            graddist1.stride(1), _ptr(graddist2), graddist2.stride(0), graddist2.stride(1), _ptr(idx1), _ptr(idx2),
+            _ptr(gradxyz1), _ptr(gradxyz2), _stream(dev)), "pcm_chamfer_backward_strided")
 
 
 def chamfer_forward(xyz1, xyz2, dist1, dist2, idx1, idx2) -> None:

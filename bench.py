@@ -65,7 +65,7 @@ BENCH_SEED = 1234                  # rank r's clouds: torch.Generator seed BENCH
 # the forward kernel instance the step launches at this size (csrc/chamfer.hip
 # default_fwd_variant) and the committed rocprofv3 counter summary it is looked
 # up in for roofline.traffic (tools/pmc_passes.sh + tools/pmc_summarize.py)
-FWD_KERNEL = "chamfer_fwd_filt_kernel<float, 8, 4, 32, 2048, 3>"  # default fused-loss forward
+FWD_KERNEL = "chamfer_fwd_filt_kernel<float, 8, 4, 16, 1024, 3>"  # default fused-loss forward (clouds <= 1024)
 BWD_KERNEL = "chamfer_bwd_staged_kernel"
 FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false>"  # default variant 11 (granule hand-off, local gradient data)
 PMC_SUMMARY = os.path.join(REPO, "profiles", "r04", "pmc_summary.json")
@@ -249,10 +249,15 @@ def time_region(fn, calls, dev, world, gpu=None):
     current stream at the region's edges append the GPU-side time (s)."""
     if dist.is_initialized():
         dist.barrier()
-    torch.cuda.synchronize(dev)
     s = torch.cuda.current_stream(dev)
     if gpu is not None:
+        # the events exist and have been recorded once before the clock starts
+        # (HIP creates an event at its first record: that first-use cost is
+        # not the region's)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        e1.record(s)
+    torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     if gpu is not None:
         e0.record(s)
@@ -747,13 +752,13 @@ def main(argv=None):
             g_tail = g_one if not multi else (g_ar_one if g_ar_many is not None else None)
             graph_info = warm_graphs(g_many, g_tail, per, args.warmup, args.steps, run_steps, dev, world)
         else:
-            # the timed region's own launches: W of them
+            g_many.replay()  # the graph form's first replay, outside every timed region
+            torch.cuda.synchronize(dev)
+            # then the timed region's own launches: W of them, last before the region
             run_steps(args.warmup)
             torch.cuda.synchronize(dev)
             graph_info = {"graph_steps": per, "warmup_steps_requested": args.warmup,
                           "warmup_steps_run": args.warmup}
-            g_many.replay()  # the graph form's first replay, outside every timed region
-            torch.cuda.synchronize(dev)
 
     gpu_t = []
     t = time_region(lambda: run_steps(args.steps), 1, dev, world, gpu=gpu_t)

@@ -152,6 +152,19 @@ int pcm_chamfer_forward_layout(const float *xyz1, const float *xyz2, int b, int 
 int pcm_chamfer_backward_layout(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1, int layout2,
                                 const float *graddist1, const float *graddist2, const int32_t *idx1,
                                 const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream);
+/*
+ * The layout backward with graddists read in place at any element strides
+ * (batch, point) >= 0 (extension): graddist1[bi * gd1_batch_stride +
+ * j * gd1_point_stride].  Strides 0 read the expanded scalar torch.mean's
+ * backward hands chamfer_3DFunction.backward (loss/loss.py:36), which the
+ * reference's wrapper materialised with graddist.contiguous()
+ * (dist_chamfer_3D.py:59-60).  Results are bit-identical to the contiguous call.
+ */
+int pcm_chamfer_backward_strided(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1,
+                                 int layout2, const float *graddist1, long long gd1_batch_stride,
+                                 long long gd1_point_stride, const float *graddist2, long long gd2_batch_stride,
+                                 long long gd2_point_stride, const int32_t *idx1, const int32_t *idx2,
+                                 float *gradxyz1, float *gradxyz2, void *stream);
 
 /*
  * fp16 clouds (extension for BASELINE config 5; the reference accepted fp32

@@ -18,6 +18,8 @@
 #   stamps     tools/stamp_filt.py fused 7 11 (needs `make stamps`)
 #   stampslg   tools/stamp_lgrid.py 13 and 11 (needs `make stamps`)
 #   probe      tools/probe_replay.py (timed-region overhead by launch form)
+#   probeev    tools/probe_events.py (does recording the region's timing events cost wall time)
+#   abr        tools/ab_ref_call.py (the unchanged caller's pieces: forward geometries, strided backward)
 set -o pipefail
 TAG=$1
 shift
@@ -57,6 +59,8 @@ for S in "$@"; do
               timeout -k 10 300 python -u tools/stamp_lgrid.py 11 >> "$O/stamps_lgrid.txt" 2>&1 ;;
     probe) timeout -k 10 300 python -u tools/probe_replay.py > "$O/probe_replay.txt" 2>&1 &&
            timeout -k 10 300 python -u tools/probe_timed.py > "$O/probe_timed.txt" 2>&1 ;;
+    abr) timeout -k 10 300 python -u tools/ab_ref_call.py > "$O/ab_ref_call.txt" 2>&1 ;;
+    probeev) timeout -k 10 300 python -u tools/probe_events.py > "$O/probe_events.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac
     rc=$?

@@ -662,9 +662,10 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
     TIn *grad;
     int ns, no, blk, gps, gpo;
     bool direct_first;
-    if (bid < b * nblk1) {
-        const int batch = bid / nblk1;
-        blk = bid - batch * nblk1;
+    int batch;  // batch-major placement: both directions of an element on one XCD (pcm_split_bm)
+    bool first_dir;
+    pcm_split_bm(bid, nblk1, nblk2, batch, first_dir, blk);
+    if (first_dir) {
         self = xyz1 + (size_t)batch * n * 3;
         other = xyz2 + (size_t)batch * m * 3;
         gds = gd1 + (size_t)batch * (GS.bs1 < 0 ? n : GS.bs1);
@@ -678,9 +679,6 @@ __global__ __launch_bounds__(NT) void chamfer_bwd_kernel(
         no = m;
         direct_first = true;
     } else {
-        bid -= b * nblk1;
-        const int batch = bid / nblk2;
-        blk = bid - batch * nblk2;
         self = xyz2 + (size_t)batch * m * 3;
         other = xyz1 + (size_t)batch * n * 3;
         gds = gd2 + (size_t)batch * (GS.bs2 < 0 ? m : GS.bs2);
@@ -965,9 +963,10 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
     float *grad;
     int ns, no, blk, gps, gpo;
     bool direct_first;
-    if (bid < b * nblk1) {
-        const int batch = bid / nblk1;
-        blk = bid - batch * nblk1;
+    int batch;  // batch-major placement: both directions of an element on one XCD (pcm_split_bm)
+    bool first_dir;
+    pcm_split_bm(bid, nblk1, nblk2, batch, first_dir, blk);
+    if (first_dir) {
         self = xyz1 + (size_t)batch * n * 3;
         other = xyz2 + (size_t)batch * m * 3;
         gds = gd1 + (size_t)batch * (GS.bs1 < 0 ? n : GS.bs1);
@@ -981,9 +980,6 @@ __global__ __launch_bounds__(kBwdT) void chamfer_bwd_staged_kernel(
         no = m;
         direct_first = true;
     } else {
-        bid -= b * nblk1;
-        const int batch = bid / nblk2;
-        blk = bid - batch * nblk2;
         self = xyz2 + (size_t)batch * m * 3;
         other = xyz1 + (size_t)batch * n * 3;
         gds = gd2 + (size_t)batch * (GS.bs2 < 0 ? m : GS.bs2);

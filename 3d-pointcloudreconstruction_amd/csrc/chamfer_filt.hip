@@ -207,7 +207,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                               unsigned long long *__restrict__ Gr = nullptr, unsigned long long tag = 0,
                               const PreDma *pre = nullptr, pcm_f4 *qown = nullptr, PcmLay LQ = PcmLay{3, 1},
                               PcmLay LT = PcmLay{3, 1}, unsigned *__restrict__ Gr4 = nullptr, unsigned gtag4 = 0,
-                              int *kown = nullptr) {
+                              int *kown = nullptr, bool g4x = false) {
     static_assert(C % 4 == 0 && TILE % C == 0, "tile must hold whole chunks of 4-candidate groups");
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
@@ -690,6 +690,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
         PCM_STAMP(6);
         // ---- one store phase for the workgroup's outputs (thread tid < QW is
         // part 0 of query tid: `proven` is that query's verdict)
+        int kg = 0;  // this thread's argmin, for the 16-byte granule stores
         if (tid < QW && qbase + tid < nq) {
             float d;
             int k;
@@ -709,8 +710,34 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             // its own flag (no drain, no counter)
             if (Gr) __hip_atomic_store(Gr + qbase + tid, tag | (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             // 4-byte granule {tag << 11 | idx} (chamfer_lgrid.h's format)
-            if (Gr4) __hip_atomic_store(Gr4 + qbase + tid, gtag4 | (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (Gr4 && !g4x)
+                __hip_atomic_store(Gr4 + qbase + tid, gtag4 | (unsigned)k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (kown) *kown = k;
+            kg = k;
+        }
+        if (Gr4 && g4x && tid < QW) {
+            // g4x: four consecutive queries' granules per 16-byte sc1 store
+            // (lanes 0-15 of each query wave gather them from lanes 4L..4L+3):
+            // a write-through store costs per lane, so a quarter of the
+            // fabric writes (MI355X_MICROARCH.md store table).  Every 4-byte
+            // granule carries its own tag, so a torn 16-byte store is harmless.
+            const unsigned v = gtag4 | (unsigned)kg;
+            const int src = (lane & 15) * 4;
+            pcm_u32x4 g;
+            g.x = (unsigned)__shfl((int)v, src, 64);
+            g.y = (unsigned)__shfl((int)v, src + 1, 64);
+            g.z = (unsigned)__shfl((int)v, src + 2, 64);
+            g.w = (unsigned)__shfl((int)v, src + 3, 64);
+            const int q = qbase + (tid & ~63) + src;
+            if (lane < 16 && q < nq) {
+                if (q + 3 < nq) {
+                    pcm_st_sc1_x4(Gr4 + q, g);
+                } else {
+                    __hip_atomic_store(Gr4 + q, g.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (q + 1 < nq) __hip_atomic_store(Gr4 + q + 1, g.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (q + 2 < nq) __hip_atomic_store(Gr4 + q + 2, g.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
         }
     } else {
         for (int s = tid; s < QW; s += NT) {
@@ -1181,32 +1208,17 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         epoch = ticket[kEpochWord] + 1u;  // plain load: written by an earlier launch
     }
     PCM_STAMP(0);
-    int bid = pcm_xcd_remap((int)blockIdx.x, nprod);
-    const int slot = bid;
-    const TIn *Q, *T;
-    float *D;
-    int32_t *I;
-    int nq, nt, blk;
-    if (bid < b * nblk1) {
-        const int batch = bid / nblk1;
-        blk = bid - batch * nblk1;
-        Q = xyz1 + (size_t)batch * n * 3;
-        T = xyz2 + (size_t)batch * m * 3;
-        D = dist1 + (size_t)batch * n;
-        I = idx1 + (size_t)batch * n;
-        nq = n;
-        nt = m;
-    } else {
-        bid -= b * nblk1;
-        const int batch = bid / nblk2;
-        blk = bid - batch * nblk2;
-        Q = xyz2 + (size_t)batch * m * 3;
-        T = xyz1 + (size_t)batch * n * 3;
-        D = dist2 + (size_t)batch * m;
-        I = idx2 + (size_t)batch * m;
-        nq = m;
-        nt = n;
-    }
+    // batch-major placement (both directions of an element on one XCD); the
+    // loss partial's slot stays direction-major, so the poll sums in the same order
+    int batch, blk;
+    bool first;
+    pcm_split_bm(pcm_xcd_remap((int)blockIdx.x, nprod), nblk1, nblk2, batch, first, blk);
+    const int slot = first ? batch * nblk1 + blk : b * nblk1 + batch * nblk2 + blk;
+    const TIn *Q = first ? xyz1 + (size_t)batch * n * 3 : xyz2 + (size_t)batch * m * 3;
+    const TIn *T = first ? xyz2 + (size_t)batch * m * 3 : xyz1 + (size_t)batch * n * 3;
+    float *D = first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m;
+    int32_t *I = first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m;
+    const int nq = first ? n : m, nt = first ? m : n;
     const float my_d = filt_forward<TIn, W, QPT, C, TILE, false>(Q, T, nq, nt, blk * QW, D, I,
                                                                  lds_arena<FiltLds<W, QPT, TILE>::kBytes>());
     if constexpr (kLoss == 3) publish_partial<3>(my_d, slot, partials, ticket, sRed, epoch);
@@ -1229,11 +1241,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1,
     int32_t *__restrict__ idx2, int nblk1, int nblk2, int lay1, int lay2) {
     constexpr int QW = 64 * QPT;
-    const int bid = pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x);
-    const bool first = bid < b * nblk1;
-    const int r = first ? bid : bid - b * nblk1;
-    const int nbk = first ? nblk1 : nblk2;
-    const int batch = r / nbk, blk = r - batch * nbk;
+    int batch, blk;
+    bool first;
+    pcm_split_bm(pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x), nblk1, nblk2, batch, first, blk);
     const float *X1 = xyz1 + (size_t)batch * n * 3, *X2 = xyz2 + (size_t)batch * m * 3;
     const PcmLay L1 = pcm_lay(lay1, n), L2 = pcm_lay(lay2, m);
     if (first)
@@ -1767,7 +1777,7 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
 #include "chamfer_lgrid.h"
 
 template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false,
-          bool kLocal = false, bool kSplit = false, bool kG4 = false>
+          bool kLocal = false, bool kSplit = false, bool kG4 = false, bool kG4x = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -1837,7 +1847,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
             first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
             first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, kG4 ? nullptr : (first ? G1 : G2),
             tag, kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, PcmLay{3, 1}, PcmLay{3, 1},
-            kG4 ? (first ? H1 : H2) : nullptr, tag4, kG4 ? &myk : nullptr);
+            kG4 ? (first ? H1 : H2) : nullptr, tag4, kG4 ? &myk : nullptr,
+            kG4x && ((n | m) & 3) == 0);  // 16-byte granule stores when every row start is 16-byte aligned
         PCM_STAMP2(1);
         const float s = wave_sum(my_d);
         if (lane == 0) sRed[wave] = s;
@@ -2053,6 +2064,8 @@ const GradVariant kGradVariants[] = {
     // 14: 11 with 4-byte argmin granules and the range's own argmins taken
     // from the forward (half the hand-off bytes, no own-range granule reads)
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true>, 8, 4},
+    // 15: 14 with four granules per 16-byte write-through store (a quarter of the fabric writes)
+    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true>, 8, 4},
 };
 // (round 4, rejected: 7 and 11 with 16 waves -- four per SIMD, a 16-way
 // merge -- 15.9-16.2 us against 13.85 us, profiles/r04/chamfer_w16_r04n_ab.txt)
@@ -2067,7 +2080,11 @@ constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]
 // forward with the gradient phase reading the forward's own LDS instead of
 // copying both clouds in, 0.07-0.12 us faster than 7 in each of 4 same-box
 // runs (profiles/r04/variant_7_11_r04ze_ab.txt)
-constexpr int kDefaultGradVariant = 11;
+// round 5: variant 15 (4-byte argmin granules, four per 16-byte write-through
+// store, the range's own argmins from the forward): the same time as 11
+// (13.56 vs 13.56 us same-box, profiles/r05/) with 3.03 MB of HBM-side traffic
+// per launch against 3.65 MB
+constexpr int kDefaultGradVariant = 15;
 
 long long grad_blocks(const GradVariant &v, int b, int n, int m, int &nblk1, int &nblk2) {
     const int QW = 64 * v.qpt;

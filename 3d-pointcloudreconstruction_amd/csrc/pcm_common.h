@@ -183,6 +183,13 @@ __device__ __forceinline__ void pcm_dma_to_lds(void *lds_dst, const void *src, i
     }
 }
 
+// 16-byte vector store with the sc1 (agent-scope, write-through) policy: the
+// wide form of a relaxed agent-scope atomic store, for data-tagged granules
+typedef unsigned pcm_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void pcm_st_sc1_x4(void *p, pcm_u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+
 // XCD-aware workgroup numbering.  The dispatcher places workgroup i on XCD
 // i % 8 (MI355X: 8 XCDs, each with its own 4 MB L2).  Giving every XCD a
 // contiguous range of logical ids keeps the workgroups of one batch element --
@@ -194,6 +201,18 @@ __device__ __forceinline__ int pcm_xcd_remap(int i, int g) {
     const int per = g / kXcd, rem = g % kXcd;
     const int x = i % kXcd, s = i / kXcd;
     return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + s;
+}
+
+// Batch-major split of a two-direction grid (b elements, nblk1 direction-1
+// and nblk2 direction-2 workgroups each): logical id -> (batch, direction,
+// block).  With pcm_xcd_remap's contiguous ranges, both directions of one
+// element -- which read the same two clouds -- share an XCD and its L2.
+__device__ __forceinline__ void pcm_split_bm(int bid, int nblk1, int nblk2, int &batch, bool &first, int &blk) {
+    const int per = nblk1 + nblk2;
+    batch = bid / per;
+    const int r = bid - batch * per;
+    first = r < nblk1;
+    blk = first ? r : r - nblk1;
 }
 
 // Compute units of the current device (256 on a whole MI355X; fewer on a

@@ -33,12 +33,15 @@ def main():
     w1, w2 = 1.0 / (b * n), 1.0 / (b * m)
     vs = list(range(7, pcm_hip.tune_num_chamfer_loss_grad_variants()))
     out = {}
+    # a zero-filled workspace per variant: variants of different granule formats
+    # sharing one would make each switch's first call recompute every argmin
+    wss = {v: torch.zeros_like(ws) for v in vs}
     for v in vs:
-        pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, ws, variant=v)
+        pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, wss[v], variant=v)
         torch.cuda.synchronize()
         out[v] = [t.clone() for t in (d1, d2, i1, i2, gx1, gx2, mo)]
     same = {v: all(torch.equal(a, r) for a, r in zip(out[v], out[7])) for v in vs}
-    graphs = {v: graph_of(lambda v=v: pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, ws,
+    graphs = {v: graph_of(lambda v=v: pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, wss[v],
                                                                 variant=v), reps) for v in vs}
     res = {v: [] for v in vs}
     for _ in range(rounds):

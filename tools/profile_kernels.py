@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Fixed kernel sequence for rocprofv3 counter passes (BASELINE configs 2 and 3):
 20x Chamfer fused-loss forward, 20x Chamfer backward, 20x one-launch loss +
-gradient (B=32, N=M=1024), 3x EMD forward (B=16, N=1024, 50 iters, eps 0.005),
+gradient and 20x each of its variants 14 and 15, 20x the channel-plane forward and 20x the
+strided backward (B=32, N=M=1024), 3x EMD forward (B=16, N=1024, 50 iters, eps 0.005),
 then BASELINE config 5 (B=8, N=M=16384): 2x the fp32 forward and 2x the fp16
 forward (both the grid path from 4096 points), 1x the dense fp16 forward,
 2x the fp16 backward.  Inputs resident before the loop."""
@@ -41,6 +42,21 @@ def main():
     mo3 = torch.empty(3, device=dev)
     for _ in range(20):
         pcm_hip.chamfer_loss_grad(x1, x2, 1.0 / (B * N), 1.0 / (B * N), d1, d2, i1, i2, mo3, gx1, gx2, ws)
+    # fused variants 14 (4-byte argmin granules, own argmins from the forward) and 15 (14 with 16-byte
+    # granule stores), each on a fresh zero-filled workspace of its own (a granule-format switch on one
+    # workspace makes its first call recompute every argmin)
+    for v in (14, 15):
+        wsv = torch.zeros_like(ws)
+        for _ in range(20):
+            pcm_hip.chamfer_loss_grad(x1, x2, 1.0 / (B * N), 1.0 / (B * N), d1, d2, i1, i2, mo3, gx1, gx2, wsv,
+                                      variant=v)
+    # the unchanged caller's kernels: channel planes read in place, the graddist torch's mean hands over
+    xp = x1.transpose(1, 2).contiguous()
+    gp = torch.empty_like(xp)
+    for _ in range(20):
+        pcm_hip.chamfer_forward_layout(xp.transpose(1, 2), x2, 1, 0, d1, d2, i1, i2)
+    for _ in range(20):
+        pcm_hip.chamfer_backward_strided(xp.transpose(1, 2), x2, 1, 0, g1, g2, i1, i2, gp.transpose(1, 2), gx2)
     for _ in range(3):
         pcm_hip.emd_forward(e1, e2, 0.005, 50, ed, ea)
     b5, n5 = 8, 16384

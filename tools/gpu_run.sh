@@ -42,7 +42,7 @@ for S in "$@"; do
     smoke) timeout -k 10 300 python -u -c 'import __graft_entry__ as g; g.smoke(); print("smoke ok")' \
                > "$O/smoke.txt" 2>&1 ;;
     rocprof) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" \
-               -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu > "$GRAFT_REPO_ROOT/$O/rocprof_bench.json" \
+               -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu > "$GRAFT_REPO_ROOT/$O/rocprof_bench.json" \
                2> "$GRAFT_REPO_ROOT/$O/rocprof.err") ;;
     abc) timeout -k 10 600 python -u tools/ab_chamfer.py > "$O/ab_chamfer.txt" 2>&1 ;;
     abe) timeout -k 10 600 python -u tools/ab_emd.py > "$O/ab_emd.txt" 2>&1 ;;

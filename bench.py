@@ -21,6 +21,10 @@ the Python wrapper per step ~0.5 us (r05c).  --graph times the 20-step graph
 instead (its first replay paid in warmup); --eager the Python wrapper.  The
 GPU-side time of the timed region (HIP events at its edges, on the kernel's
 stream) is the dominant kernel's duration in `roofline`.
+Order: the headline's W warmup steps and K timed steps first, then the legs
+reported beside it (ICP, the unchanged caller's call sequence, config 5, EMD;
+side_legs), then the CPU baseline.  --side-legs first runs those legs before
+the warmup instead: not faster (same box, profiles/r05/bench_side_legs_r05o.txt).
 
 value = point pairs evaluated per second over all ranks (2*B*N*M per rank per
 step / max-over-ranks wall time).  EMD (BASELINE config 3: B=16, N=1024,
@@ -103,6 +107,9 @@ def parse(argv=None):
     p.add_argument("--two-launch", action="store_true",
                    help="step = fused-loss forward + backward kernel (not the one-launch loss+gradient)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    p.add_argument("--side-legs", choices=("first", "last"), default="last",
+                   help="run the legs reported beside the headline after its timed region (default) or before "
+                        "its warmup (same box, r05o: 16.08/16.15 us per step first, 15.88/15.96 last)")
     p.add_argument("--no-emd", action="store_true", help="skip the EMD leg")
     p.add_argument("--no-dense", action="store_true", help="skip the dense fp16 (config 5) leg")
     p.add_argument("--no-icp", action="store_true", help="skip the ICP (evaluation alignment) leg")
@@ -307,7 +314,7 @@ def kernel_avg_us(launch, reps, dev, graph=True):
     return e0.elapsed_time(e1) * 1000.0 / reps
 
 
-def reference_call_leg(dev, fused_step_us, reps=50):
+def reference_call_leg(dev, reps=50):
     """The call sequence the UNCHANGED caller runs, literally: train.py:163
     hands loss/loss.py a transposed view of the generator output,
     loss/loss.py:34-36 builds chamfer_3DDist, takes mean(dist1)+mean(dist2),
@@ -364,8 +371,7 @@ def reference_call_leg(dev, fused_step_us, reps=50):
     return {"sequence": "chamfer_3DDist()(fake.transpose(2,1), points); mean(dist1)+mean(dist2); .backward() "
                         "(loss/loss.py:34-36, train.py:163,176)",
             "eager_us_per_step": eager_us, "graph_us_per_step": graph_us,
-            "graph_pairs_per_s": pairs / (graph_us * 1e-6),
-            "graph_vs_fused_step": graph_us / fused_step_us}
+            "graph_pairs_per_s": pairs / (graph_us * 1e-6)}
 
 
 EMD_TRAIN_CLOUDS = os.path.join(REPO, "bench_data", "emd_training_call.npz")
@@ -641,6 +647,30 @@ def warm_graphs(g_many, g_one, per, warmup, steps, run_steps, dev, world):
     return info
 
 
+def side_legs(args, dev, rank, world):
+    """The legs reported beside the headline (ICP, the unchanged caller's call
+    sequence, config 5, EMD), after the headline (default) or, with
+    --side-legs first, before its warmup.  Tried because back-to-back regions
+    speed up ~9% over the first ~4 ms of load (profiles/r05/probe_events_r05j.txt);
+    legs-first was not faster on the same box (r05o), so it is not the default."""
+    side = {}
+    if not args.no_icp:  # first: its CPU-timed part leaves the GPU idle
+        side["icp"] = icp_leg(dev, with_cpu=rank == 0 and world == 1 and not args.no_cpu)
+    if not args.no_ref_call:
+        side["reference_call"] = reference_call_leg(dev)
+    if not args.no_dense:
+        side["dense_fp16"] = dense_f16_leg(dev)
+    if not args.no_emd:
+        side["emd"] = emd_leg(dev)
+        pred, points = generator_predictions(dev)
+        side["emd_training_call"] = emd_leg(dev, reps=3, eps=0.05, iters=3000, clouds=(pred, points),
+                                            label="seeded random-init generator predictions vs uniform GT "
+                                                  "(committed, bench_data/emd_training_call.npz)")
+        side["emd_training_call_uniform"] = emd_leg(dev, reps=3, eps=0.05, iters=3000)
+    torch.cuda.synchronize(dev)
+    return side
+
+
 def main(argv=None):
     args = parse(argv)
     # decided before any GPU call: a process that has initialised the GPU
@@ -748,6 +778,7 @@ def main(argv=None):
                         g_one.replay()
                         step.reduce_losses(1)
                 mode = "one-step hipgraph replay + eager all-reduce of the step's loss, every step"
+        side = side_legs(args, dev, rank, world) if args.side_legs == "first" else {}
         if multi or args.graph:
             g_tail = g_one if not multi else (g_ar_one if g_ar_many is not None else None)
             graph_info = warm_graphs(g_many, g_tail, per, args.warmup, args.steps, run_steps, dev, world)
@@ -760,6 +791,10 @@ def main(argv=None):
             graph_info = {"graph_steps": per, "warmup_steps_requested": args.warmup,
                           "warmup_steps_run": args.warmup}
 
+    if args.eager:
+        side = side_legs(args, dev, rank, world) if args.side_legs == "first" else {}
+        run_steps(args.warmup)
+        torch.cuda.synchronize(dev)
     gpu_t = []
     t = time_region(lambda: run_steps(args.steps), 1, dev, world, gpu=gpu_t)
     if graph_info is not None and g_many is not None:
@@ -871,19 +906,11 @@ def main(argv=None):
                 "launch": f"hipgraph of {per} steps, then ONE all-reduce of their {per} loss rows",
                 "ms_per_step": t_b * 1000.0 / kb,
                 "value": world * kb * pairs_per_step / t_b}
-    if not args.no_ref_call:
-        out["reference_call"] = reference_call_leg(dev, ms * 1000.0)
-    if not args.no_emd:
-        out["emd"] = emd_leg(dev)
-        pred, points = generator_predictions(dev)
-        out["emd_training_call"] = emd_leg(dev, reps=3, eps=0.05, iters=3000, clouds=(pred, points),
-                                           label="seeded random-init generator predictions vs uniform GT "
-                                                 "(committed, bench_data/emd_training_call.npz)")
-        out["emd_training_call_uniform"] = emd_leg(dev, reps=3, eps=0.05, iters=3000)
-    if not args.no_dense:
-        out["dense_fp16"] = dense_f16_leg(dev)
-    if not args.no_icp:
-        out["icp"] = icp_leg(dev, with_cpu=rank == 0 and world == 1 and not args.no_cpu)
+    if args.side_legs == "last":
+        side = side_legs(args, dev, rank, world)
+    out.update(side)
+    if "reference_call" in out:
+        out["reference_call"]["graph_vs_fused_step"] = out["reference_call"]["graph_us_per_step"] / (ms * 1000.0)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -90,7 +90,7 @@ def main():
     for k, v in res.items():
         print(f"{k:28s} median {statistics.median(v):7.2f} us  min {min(v):7.2f}  "
               f"[{' '.join(f'{x:.2f}' for x in v)}]", flush=True)
-    rc = bench.reference_call_leg(dev, 14.0)
+    rc = bench.reference_call_leg(dev)
     print(f"reference_call graph {rc['graph_us_per_step']:.2f} us/step, eager {rc['eager_us_per_step']:.1f} us/step",
           flush=True)
 

@@ -18,6 +18,7 @@
 #   stamps     tools/stamp_filt.py fused 7 11 (needs `make stamps`)
 #   stampslg   tools/stamp_lgrid.py 13 and 11 (needs `make stamps`)
 #   probe      tools/probe_replay.py (timed-region overhead by launch form)
+#   benchab    the driver's bench command twice per side-leg order (same box)
 #   probeev    tools/probe_events.py (does recording the region's timing events cost wall time)
 #   abr        tools/ab_ref_call.py (the unchanged caller's pieces: forward geometries, strided backward)
 set -o pipefail
@@ -60,6 +61,9 @@ for S in "$@"; do
     probe) timeout -k 10 300 python -u tools/probe_replay.py > "$O/probe_replay.txt" 2>&1 &&
            timeout -k 10 300 python -u tools/probe_timed.py > "$O/probe_timed.txt" 2>&1 ;;
     abr) timeout -k 10 300 python -u tools/ab_ref_call.py > "$O/ab_ref_call.txt" 2>&1 ;;
+    benchab) for i in 1 2; do for o in first last; do
+               timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 --side-legs $o \
+                   > "$O/bench_${o}_$i.json" 2> "$O/bench_${o}_$i.err" || exit 1; done; done ;;
     probeev) timeout -k 10 300 python -u tools/probe_events.py > "$O/probe_events.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac

@@ -73,6 +73,10 @@ class chamfer_3DFunction(Function):
         ctx.layouts = lay
         ctx.save_for_backward(xyz1, xyz2, idx1, idx2)
         ctx.mark_non_differentiable(idx1, idx2)
+        # no zero-filled gradients for the unused outputs: autograd would launch
+        # a fill kernel for each int32 index output on every backward (backward
+        # takes None, an unused distance output's as an expanded zero)
+        ctx.set_materialize_grads(False)
         return dist1, dist2, idx1, idx2
 
     @staticmethod
@@ -88,7 +92,7 @@ class chamfer_3DFunction(Function):
             pcm_hip.chamfer_backward_strided(xyz1, xyz2, lay[0], lay[1], _graddist(graddist1, idx1),
                                              _graddist(graddist2, idx2), idx1, idx2, gradxyz1, gradxyz2)
             return gradxyz1, gradxyz2
-        # autograd hands None for an unused output
+        # an unused output's gradient arrives as None
         graddist1 = (torch.zeros_like(idx1, dtype=torch.float32) if graddist1 is None
                      else graddist1.contiguous().float())
         graddist2 = (torch.zeros_like(idx2, dtype=torch.float32) if graddist2 is None

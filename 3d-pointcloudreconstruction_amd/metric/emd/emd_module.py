@@ -59,11 +59,14 @@ class emdFunction(Function):
         pcm_hip.emd_forward(xyz1, xyz2, float(eps), int(iters), dist, assignment)
         ctx.save_for_backward(xyz1, xyz2, assignment)
         ctx.mark_non_differentiable(assignment)
+        ctx.set_materialize_grads(False)  # no zero-fill kernel for the int32 assignment's gradient
         return dist, assignment
 
     @staticmethod
     def backward(ctx, graddist, gradidx):
         xyz1, xyz2, assignment = ctx.saved_tensors
+        if graddist is None:  # dist unused by the loss
+            graddist = torch.zeros(assignment.shape, device=xyz1.device)
         graddist = graddist.contiguous().float().to(xyz1.device)
         gradxyz1 = torch.empty_like(xyz1)
         pcm_hip.emd_backward(xyz1, xyz2, graddist, assignment, gradxyz1)

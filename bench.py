@@ -437,7 +437,29 @@ def emd_leg(dev, reps=10, eps=EMD_EPS, iters=EMD_ITERS, clouds=None, label="unif
                          "achieved": lane_ops / 1e12, "peak": VALU_LANE_OPS_PEAK / 1e12,
                          "unit": "T lane-ops/s", "frac": lane_ops / VALU_LANE_OPS_PEAK,
                          "note": f"{EMD_LANE_OPS_PER_PAIR} lane-ops per (bidder, object) pair the reference "
-                                 "evaluates; the build evaluates fewer (caches), so this is the reference-work rate"}}
+                                 "evaluates; the build evaluates fewer (caches), so this is the reference-work rate"},
+            "roofline_executed": emd_executed_roofline(us) if clouds is None and eps == EMD_EPS else None}
+
+
+# the EMD kernels as profile_kernels.py runs them (BASELINE config 3) in the committed PMC summary
+EMD_KERNELS = ("emd_seed_kernel<true, true>", "emd_auction_kernel<false, true, true>")
+
+
+def emd_executed_roofline(us):
+    """The work the build actually executes at BASELINE config 3: VALU wave
+    instructions per forward (seed + auction, rocprofv3 SQ_INSTS_VALU from the
+    committed PMC summary) x 64 lanes / this forward's time, against the
+    78.6 T lane-instruction issue ceiling."""
+    try:
+        with open(PMC_SUMMARY) as fh:
+            cnt = json.load(fh)["counters"]
+        waves = sum(cnt[k]["SQ_INSTS_VALU"] for k in EMD_KERNELS)
+    except (OSError, KeyError, ValueError):
+        return None
+    rate = waves * 64 / (us * 1e-6)
+    return {"bound": "valu", "valu_wave_instructions": waves, "achieved": rate / 1e12,
+            "peak": VALU_LANE_OPS_PEAK / 1e12, "unit": "T lane-ops/s", "frac": rate / VALU_LANE_OPS_PEAK,
+            "source": os.path.relpath(PMC_SUMMARY, REPO)}
 
 
 def dense_f16_leg(dev, reps=10):

@@ -974,3 +974,25 @@ def test_reference_call_graddist_reaches_backward_in_place(cuda):
     os.makedirs(os.path.join(REPO, "gpurun_out", "test_records"), exist_ok=True)
     with open(os.path.join(REPO, "gpurun_out", "test_records", "mean_graddist_strides.json"), "w") as f:
         json.dump({"graddist_strides": seen[0], "torch": torch.__version__}, f)
+
+
+@pytest.mark.parametrize("lays", [(0, 0), (1, 0)])
+def test_backward_unused_output_gets_no_fill(cuda, oracle, lays):
+    # set_materialize_grads(False): an unused distance output's gradient arrives
+    # as None (an expanded zero here) and the index outputs' are never
+    # zero-filled; gradients equal the oracle's with graddist2 = 0
+    import dist_chamfer_3D
+    b, n, m = 2, 300, 260
+    a, c = _clouds(151, b, n, m)
+    leaf = (a.transpose(1, 2).contiguous() if lays[0] else a.clone()).to(cuda).requires_grad_(True)
+    x1 = leaf.transpose(1, 2) if lays[0] else leaf
+    x2 = c.to(cuda).requires_grad_(True)
+    d1, d2, i1, i2 = dist_chamfer_3D.chamfer_3DDist()(x1, x2)
+    (d1.sum() * 0.5).backward()
+    torch.cuda.synchronize()
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    gr1, gr2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), 0.5, np.float32),
+                                       np.zeros((b, m), np.float32), ref[2], ref[3])
+    got1 = (leaf.grad.transpose(1, 2) if lays[0] else leaf.grad).cpu().contiguous().numpy()
+    np.testing.assert_array_equal(got1.view(np.int32), gr1.view(np.int32))
+    np.testing.assert_array_equal(x2.grad.cpu().numpy().view(np.int32), gr2.view(np.int32))

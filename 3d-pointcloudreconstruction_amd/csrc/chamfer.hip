@@ -631,13 +631,6 @@ __device__ inline int block_exclusive_scan(int v, int *wave_tot) {
     return before + x - v;
 }
 
-// graddist element strides per direction (batch, point), read in place: an
-// expanded scalar (stride 0, what torch.mean's backward hands over) needs no
-// materialising copy.  bs < 0: contiguous [b, n].
-struct PcmGdStr {
-    int bs1 = -1, ps1 = 1, bs2 = -1, ps2 = 1;
-};
-
 // NT targets per workgroup (= threads): every workgroup reads the whole
 // other direction's argmins, so large clouds take NT = 1024 (4x less of that)
 template <typename TIn, int NT = kBwdT, int CAP = kBwdCap>
@@ -1275,14 +1268,17 @@ int launch_bwd(int variant, const float *xyz1, const float *xyz2, int b, int n, 
     const int nblk2 = (m + kBwdT - 1) / kBwdT;
     const long long blocks = (long long)b * (nblk1 + nblk2);
     if (blocks > 0x7fffffffLL) return PCM_ERR_UNSUPPORTED;
-    if (variant == 0 && n <= kBwdStageMax && m <= kBwdStageMax) {
+    if (variant == 0 && pcm_bwd_slots_fits(n, m))
+        return pcm_launch_bwd_slots(xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2, lay1,
+                                    lay2, GS, (hipStream_t)stream);
+    if (variant == 4 && n <= kBwdStageMax && m <= kBwdStageMax) {  // round 4's default (staged passes)
         hipLaunchKernelGGL(chamfer_bwd_staged_kernel, dim3((unsigned)blocks), dim3(kBwdT), 0,
                            (hipStream_t)stream, xyz1, xyz2, b, n, m, graddist1, graddist2, idx1,
                            idx2, gradxyz1, gradxyz2, nblk1, nblk2, lay1, lay2, GS);
         return pcm_launch_status();
     }
     const bool strided = GS.bs1 >= 0 || GS.bs2 >= 0 || GS.ps1 != 1 || GS.ps2 != 1;
-    if (lay1 != 0 || lay2 != 0 || (strided && !wide_bwd(n, m))) {
+    if (lay1 != 0 || lay2 != 0 || (strided && !wide_bwd(n, m)) || variant == 4) {
         // channel planes or strided graddists: the staged kernel's forms, else the global-memory kernel's
         hipLaunchKernelGGL(chamfer_bwd_kernel<float>, dim3((unsigned)blocks), dim3(kBwdT), 0, (hipStream_t)stream,
                            xyz1, xyz2, b, n, m, graddist1, graddist2, idx1, idx2, gradxyz1, gradxyz2, nblk1, nblk2,

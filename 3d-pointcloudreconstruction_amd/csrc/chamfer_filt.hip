@@ -1293,9 +1293,9 @@ __device__ __forceinline__ float ld_sc1(const float *p) {
 // rare rest one by one.  (Measured and rejected: both clouds' targets of a
 // round interleaved in straight-line code -- 2.6 -> 3.0 us per batch element.)
 // getA(i, x, y, z): the coordinates of source i of the other cloud
-template <typename GetA>
+template <typename GetA, typename GetH>
 __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, float sx, float sy, float sz,
-                                            float h, GetA getA, const uint16_t *tab, int cnt) {
+                                            GetH h, GetA getA, const uint16_t *tab, int cnt) {
     static_assert(kGradSlots == 8 && kGradSlotsMax == 16, "sorting networks for 8 and 16 ids");
     if (cnt > kGradSlots) {
         // rare: 9..16 sources.  Odd-even transposition sort of the two rows
@@ -1320,9 +1320,10 @@ __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, flo
         for (int u = 0; u < cnt; ++u) {
             float tx, ty, tz;
             getA(f[u], tx, ty, tz);
-            ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(tx, sx)));
-            ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(ty, sy)));
-            az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(tz, sz)));
+            const float hu = h(f[u]);
+            ax = __fadd_rn(ax, -__fmul_rn(hu, __fsub_rn(tx, sx)));
+            ay = __fadd_rn(ay, -__fmul_rn(hu, __fsub_rn(ty, sy)));
+            az = __fadd_rn(az, -__fmul_rn(hu, __fsub_rn(tz, sz)));
         }
         return;
     }
@@ -1343,20 +1344,24 @@ __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, flo
     cas(0, 1); cas(2, 3); cas(4, 5); cas(6, 7); cas(0, 2); cas(1, 3); cas(4, 6); cas(5, 7); cas(1, 2);
     cas(5, 6); cas(0, 4); cas(3, 7); cas(1, 5); cas(2, 6); cas(1, 4); cas(3, 6); cas(2, 4); cas(3, 5);
     cas(3, 4);
-    auto add = [&](float tx, float ty, float tz) {
-        ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(tx, sx)));
-        ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(ty, sy)));
-        az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(tz, sz)));
+    auto add = [&](float hu, float tx, float ty, float tz) {
+        ax = __fadd_rn(ax, -__fmul_rn(hu, __fsub_rn(tx, sx)));
+        ay = __fadd_rn(ay, -__fmul_rn(hu, __fsub_rn(ty, sy)));
+        az = __fadd_rn(az, -__fmul_rn(hu, __fsub_rn(tz, sz)));
     };
-    float gx[4], gy[4], gz[4];
+    float gx[4], gy[4], gz[4], gh[4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) getA(u < cnt ? e[u] : 0, gx[u], gy[u], gz[u]);
+    for (int u = 0; u < 4; ++u) {
+        const int su = u < cnt ? e[u] : 0;
+        getA(su, gx[u], gy[u], gz[u]);
+        gh[u] = h(su);
+    }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
         const bool on = u < cnt;
-        const float nx = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(gx[u], sx)));
-        const float ny = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(gy[u], sy)));
-        const float nz = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(gz[u], sz)));
+        const float nx = __fadd_rn(ax, -__fmul_rn(gh[u], __fsub_rn(gx[u], sx)));
+        const float ny = __fadd_rn(ay, -__fmul_rn(gh[u], __fsub_rn(gy[u], sy)));
+        const float nz = __fadd_rn(az, -__fmul_rn(gh[u], __fsub_rn(gz[u], sz)));
         ax = on ? nx : ax;
         ay = on ? ny : ay;
         az = on ? nz : az;
@@ -1364,8 +1369,129 @@ __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, flo
     for (int u = 4; u < cnt; ++u) {
         float tx, ty, tz;
         getA(e[u], tx, ty, tz);
-        add(tx, ty, tz);
+        add(h(e[u]), tx, ty, tz);
     }
+}
+
+// ---------------------------------------------------------------------------
+// Standalone backward with per-point graddists (pcm_chamfer_backward's default
+// for clouds of <= kBwdSlotsMax points): the 256-target workgroup layout of
+// chamfer.hip's staged kernel -- the other cloud's argmins, points and
+// graddists arrive by LDS-DMA -- but the sources are bucketed the fused step's
+// way (range_grad): one LDS atomic claims a slot of the target's 16-slot row,
+// and the target's thread sorts its row and sums in ascending source order
+// (scatter_sum), instead of a histogram, a scan, a fill and a rank pass with a
+// barrier each.  A target with more than 16 sources (a collapsed cloud) sums
+// by an ordered scan of the other cloud's argmins.  Same arithmetic and order
+// as the reference's kernels (chamfer3D.cu:155-195), bit-identical.
+// ---------------------------------------------------------------------------
+constexpr int kBwdSlotsT = 256;      // targets per workgroup = threads
+constexpr int kBwdSlotsMax = 2048;   // points of the other cloud staged in LDS
+
+__global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
+    const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
+    const int32_t *__restrict__ idx2, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
+    int lay1, int lay2, PcmGdStr GS) {
+    constexpr int NT = kBwdSlotsT;
+    __shared__ __attribute__((aligned(16))) float sO[3 * kBwdSlotsMax];  // other cloud, its layout
+    __shared__ __attribute__((aligned(16))) float sG[kBwdSlotsMax];      // other graddist
+    __shared__ __attribute__((aligned(16))) int sK[kBwdSlotsMax];        // other argmins
+    __shared__ int cnt[NT];
+    __shared__ __attribute__((aligned(16))) uint16_t tab[NT * kGradSlotsMax];
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6;
+    int batch, blk;
+    bool first;
+    pcm_split_bm(pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x), nblk1, nblk2, batch, first, blk);
+    const int ns = first ? n : m, no = first ? m : n;
+    const float *self = first ? xyz1 + (size_t)batch * n * 3 : xyz2 + (size_t)batch * m * 3;
+    const float *other = first ? xyz2 + (size_t)batch * m * 3 : xyz1 + (size_t)batch * n * 3;
+    const int gbs = first ? (GS.bs1 < 0 ? n : GS.bs1) : (GS.bs2 < 0 ? m : GS.bs2);
+    const int gbo = first ? (GS.bs2 < 0 ? m : GS.bs2) : (GS.bs1 < 0 ? n : GS.bs1);
+    const int gps = first ? GS.ps1 : GS.ps2, gpo = first ? GS.ps2 : GS.ps1;
+    const float *gds = (first ? gd1 : gd2) + (size_t)batch * gbs;
+    const float *gdo = (first ? gd2 : gd1) + (size_t)batch * gbo;
+    const int32_t *ids = (first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m);
+    const int32_t *ido = (first ? idx2 + (size_t)batch * m : idx1 + (size_t)batch * n);
+    float *grad = first ? grad1 + (size_t)batch * n * 3 : grad2 + (size_t)batch * m * 3;
+    const PcmLay LS = first ? pcm_lay(lay1, n) : pcm_lay(lay2, m);
+    const PcmLay LO = first ? pcm_lay(lay2, m) : pcm_lay(lay1, n);
+    const int t0 = blk * NT;
+    const int T = min(NT, ns - t0);
+
+    pcm_dma_to_lds(sK, ido, 4 * no, wave, NT / 64);
+    pcm_dma_to_lds(sO, other, 12 * no, wave, NT / 64);
+    // graddists of the other cloud: by LDS-DMA when contiguous, one register
+    // when an expanded scalar (stride 0), else strided loads
+    float hconst = 0.f;
+    if (gpo == 1)
+        pcm_dma_to_lds(sG, gdo, 4 * no, wave, NT / 64);
+    else if (gpo == 0)
+        hconst = __fmul_rn(gdo[0], 2.f);
+    else
+        for (int j = tid; j < no; j += NT) sG[j] = gdo[(size_t)j * gpo];
+    const int i = t0 + tid;
+    const bool own = tid < T;
+    float sx = 0.f, sy = 0.f, sz = 0.f, gself = 0.f;
+    int kself = 0;
+    if (own) {
+        sx = self[pcm_at(LS, i, 0)];
+        sy = self[pcm_at(LS, i, 1)];
+        sz = self[pcm_at(LS, i, 2)];
+        kself = ids[i];
+        gself = gds[(size_t)i * gps];
+    }
+    cnt[tid] = 0;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // every source whose argmin falls in [t0, t0 + T) claims a slot of its row
+    for (int j = tid; j < no; j += NT) {
+        const unsigned k = (unsigned)(sK[j] - t0);
+        if (k < (unsigned)T) {
+            const int slot = atomicAdd(&cnt[k], 1);
+            if (slot < kGradSlotsMax) tab[k * kGradSlotsMax + slot] = (uint16_t)j;
+        }
+    }
+    __syncthreads();
+    if (!own) return;
+    const float g = __fmul_rn(gself, 2.f);
+    const float d0 = __fmul_rn(g, __fsub_rn(sx, sO[pcm_at(LO, kself, 0)]));
+    const float d1 = __fmul_rn(g, __fsub_rn(sy, sO[pcm_at(LO, kself, 1)]));
+    const float d2 = __fmul_rn(g, __fsub_rn(sz, sO[pcm_at(LO, kself, 2)]));
+    float ax = 0.f, ay = 0.f, az = 0.f;
+    if (first) {  // cloud 1: direct term first (chamfer3D.cu:184), then the cloud-2 scatters
+        ax = __fadd_rn(ax, d0);
+        ay = __fadd_rn(ay, d1);
+        az = __fadd_rn(az, d2);
+    }
+    auto getA = [&](int j, float &x, float &y, float &z) {
+        x = sO[pcm_at(LO, j, 0)];
+        y = sO[pcm_at(LO, j, 1)];
+        z = sO[pcm_at(LO, j, 2)];
+    };
+    auto geth = [&](int j) { return gpo == 0 ? hconst : __fmul_rn(sG[j], 2.f); };
+    const int c = cnt[tid];
+    if (c <= kGradSlotsMax) {
+        scatter_sum(ax, ay, az, sx, sy, sz, geth, getA, tab + tid * kGradSlotsMax, c);
+    } else {
+        // a collapsed cloud: the other cloud's sources of this target in ascending order
+        for (int j = 0; j < no; ++j)
+            if (sK[j] == i) {
+                const float h = geth(j);
+                ax = __fadd_rn(ax, -__fmul_rn(h, __fsub_rn(sO[pcm_at(LO, j, 0)], sx)));
+                ay = __fadd_rn(ay, -__fmul_rn(h, __fsub_rn(sO[pcm_at(LO, j, 1)], sy)));
+                az = __fadd_rn(az, -__fmul_rn(h, __fsub_rn(sO[pcm_at(LO, j, 2)], sz)));
+            }
+    }
+    if (!first) {  // cloud 2: the cloud-1 scatters first (kernel 1 ran before kernel 2), then direct
+        ax = __fadd_rn(ax, d0);
+        ay = __fadd_rn(ay, d1);
+        az = __fadd_rn(az, d2);
+    }
+    grad[pcm_at(LS, i, 0)] = ax;
+    grad[pcm_at(LS, i, 1)] = ay;
+    grad[pcm_at(LS, i, 2)] = az;
 }
 
 // Gradients of L = w1 sum(dist1) + w2 sum(dist2) for the targets
@@ -1561,7 +1687,7 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                 ay = __fadd_rn(ay, dy);
                 az = __fadd_rn(az, dz);
             }
-            scatter_sum(ax, ay, az, sx, sy, sz, h, getA, tab + tid * kGradSlotsMax, c);
+            scatter_sum(ax, ay, az, sx, sy, sz, [h](int) { return h; }, getA, tab + tid * kGradSlotsMax, c);
             if (!dir1) {  // cloud 2: cloud-1 scatters first (kernel 1 ran before kernel 2), then direct
                 ax = __fadd_rn(ax, dx);
                 ay = __fadd_rn(ay, dy);
@@ -2008,6 +2134,20 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
 }
 
 }  // namespace
+
+// the slot-bucket backward (above); the caller (chamfer.hip launch_bwd) has
+// checked the shapes and pointers, n, m > 0
+bool pcm_bwd_slots_fits(int n, int m) { return n <= kBwdSlotsMax && m <= kBwdSlotsMax; }
+int pcm_launch_bwd_slots(const float *xyz1, const float *xyz2, int b, int n, int m, const float *gd1, const float *gd2,
+                         const int32_t *idx1, const int32_t *idx2, float *grad1, float *grad2, int lay1, int lay2,
+                         PcmGdStr GS, hipStream_t stream) {
+    const int nblk1 = (n + kBwdSlotsT - 1) / kBwdSlotsT, nblk2 = (m + kBwdSlotsT - 1) / kBwdSlotsT;
+    const long long blocks = (long long)b * (nblk1 + nblk2);
+    if (blocks > 0x7fffffffLL) return PCM_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(chamfer_bwd_slots_kernel, dim3((unsigned)blocks), dim3(kBwdSlotsT), 0, stream, xyz1, xyz2, b,
+                       n, m, gd1, gd2, idx1, idx2, grad1, grad2, nblk1, nblk2, lay1, lay2, GS);
+    return pcm_launch_status();
+}
 
 #define PCM_FWD_FILT(W, Q, C, TILE)                                                                   \
     PcmFwdVariant{chamfer_fwd_filt_kernel<float, W, Q, C, TILE, 0>, nullptr, nullptr,                \

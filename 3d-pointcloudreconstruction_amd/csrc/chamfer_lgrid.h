@@ -683,7 +683,7 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
                 ay = __fadd_rn(ay, dy);
                 az = __fadd_rn(az, dz);
             }
-            scatter_sum(ax, ay, az, sx, sy, sz, gh, getA, tab + tid * kGradSlotsMax, c);
+            scatter_sum(ax, ay, az, sx, sy, sz, [gh](int) { return gh; }, getA, tab + tid * kGradSlotsMax, c);
             if (!first) {  // cloud 2: cloud-1 scatters first (kernel 1 ran before kernel 2), then direct
                 ax = __fadd_rn(ax, dx);
                 ay = __fadd_rn(ay, dy);

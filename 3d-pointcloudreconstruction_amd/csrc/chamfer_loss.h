@@ -167,6 +167,11 @@ struct PcmFwdVariant {
 };
 // filtered-scan variants (chamfer_filt.hip), appended to chamfer.hip's table
 extern const PcmFwdVariant kPcmFiltVariants[];
+// chamfer_filt.hip: the slot-bucket backward (per-point graddists at strides GS)
+bool pcm_bwd_slots_fits(int n, int m);
+int pcm_launch_bwd_slots(const float *xyz1, const float *xyz2, int b, int n, int m, const float *gd1, const float *gd2,
+                         const int32_t *idx1, const int32_t *idx2, float *grad1, float *grad2, int lay1, int lay2,
+                         PcmGdStr GS, hipStream_t stream);
 extern const int kPcmNumFiltVariants;
 
 // fp16-cloud forward kernels (same signature on binary16 clouds)

@@ -203,6 +203,13 @@ __device__ __forceinline__ int pcm_xcd_remap(int i, int g) {
     return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + s;
 }
 
+// Chamfer backward graddist element strides per direction (batch, point),
+// read in place: an expanded scalar (stride 0, what torch.mean's backward can
+// hand over) needs no materialising copy.  bs < 0: contiguous [b, n].
+struct PcmGdStr {
+    int bs1 = -1, ps1 = 1, bs2 = -1, ps2 = 1;
+};
+
 // Batch-major split of a two-direction grid (b elements, nblk1 direction-1
 // and nblk2 direction-2 workgroups each): logical id -> (batch, direction,
 // block).  With pcm_xcd_remap's contiguous ranges, both directions of one

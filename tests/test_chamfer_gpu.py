@@ -258,7 +258,7 @@ def test_backward_paths_identical(cuda, oracle, b, n, m):
     g1 = torch.rand(b, n, generator=gen).to(cuda)
     g2 = torch.rand(b, m, generator=gen).to(cuda)
     outs = []
-    for v in (0, 1, 2, 3):  # 3: 1024-target workgroups (the default from 4096 points)
+    for v in (0, 1, 2, 3, 4):  # 0: slot buckets to 2048 points; 3: 1024-target workgroups; 4: staged passes
         gx1 = torch.full((b, n, 3), float("nan"), device=cuda)
         gx2 = torch.full((b, m, 3), float("nan"), device=cuda)
         pcm_hip.tune_chamfer_backward(v, x1, x2, g1, g2, i1, i2, gx1, gx2)
@@ -996,3 +996,38 @@ def test_backward_unused_output_gets_no_fill(cuda, oracle, lays):
     got1 = (leaf.grad.transpose(1, 2) if lays[0] else leaf.grad).cpu().contiguous().numpy()
     np.testing.assert_array_equal(got1.view(np.int32), gr1.view(np.int32))
     np.testing.assert_array_equal(x2.grad.cpu().numpy().view(np.int32), gr2.view(np.int32))
+
+
+@pytest.mark.parametrize("kind", ["crowded", "collapsed"])
+def test_backward_slot_buckets_crowded(cuda, oracle, kind):
+    # the default backward's 16-slot rows: targets drawing 1..20 sources (the
+    # 8-id network, the 16-id sort and the ordered scan past 16) and a collapsed
+    # cloud (every source on one target), per-point graddists, both layouts
+    import pcm_hip
+    b, n, m = 2, 1024, 1024
+    a, c = _clouds(161, b, n, m)
+    g = torch.Generator().manual_seed(162)
+    if kind == "collapsed":
+        c[:, :, :] = c[:, :1, :]
+    else:
+        for bb in range(b):
+            pos = 0
+            for size in range(1, 21):
+                for src, dst, t in ((c, a, 16 * size), (a, c, 16 * size + 8)):
+                    for r in range(size):
+                        src[bb, 400 + pos + r] = dst[bb, t] + 1e-3 * (torch.rand(3, generator=g) - 0.5)
+                pos += size
+    ref = oracle.chamfer_forward(a.numpy(), c.numpy())
+    g1 = torch.rand(b, n, generator=g)
+    g2 = torch.rand(b, m, generator=g)
+    r1, r2 = oracle.chamfer_backward(a.numpy(), c.numpy(), g1.numpy(), g2.numpy(), ref[2], ref[3])
+    i1 = torch.from_numpy(ref[2]).to(cuda)
+    i2 = torch.from_numpy(ref[3]).to(cuda)
+    for lay in (0, 1):
+        x1 = a.transpose(1, 2).contiguous().to(cuda).transpose(1, 2) if lay else a.to(cuda)
+        gx1 = torch.empty(b, 3, n, device=cuda).transpose(1, 2) if lay else torch.empty(b, n, 3, device=cuda)
+        gx2 = torch.empty(b, m, 3, device=cuda)
+        pcm_hip.chamfer_backward_strided(x1, c.to(cuda), lay, 0, g1.to(cuda), g2.to(cuda), i1, i2, gx1, gx2)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(gx1.cpu().contiguous().numpy().view(np.int32), r1.view(np.int32))
+        np.testing.assert_array_equal(gx2.cpu().numpy().view(np.int32), r2.view(np.int32))

@@ -74,11 +74,20 @@ def main():
         "bwd graddist expanded": lambda: pcm_hip.chamfer_backward_strided(
             fake, points, 1, 0, g1e, g2e, i1, i2, gx["e"][0].transpose(1, 2), gx["e"][1]),
     }
+    gr = {v: (torch.empty(b, n, 3, device=dev), torch.empty(b, m, 3, device=dev)) for v in (0, 4)}
+    bw["bwd rows slot buckets (default)"] = lambda: pcm_hip.tune_chamfer_backward(0, rows, points, g1c, g2c, i1, i2,
+                                                                                 *gr[0])
+    bw["bwd rows staged passes (r04)"] = lambda: pcm_hip.tune_chamfer_backward(4, rows, points, g1c, g2c, i1, i2,
+                                                                              *gr[4])
     for fn in bw.values():
         fn()
     torch.cuda.synchronize()
     same = all(torch.equal(x.view(torch.int32), y.view(torch.int32)) for x, y in zip(gx["c"], gx["e"]))
     print(f"backward expanded vs materialised bit-identical: {same}", flush=True)
+    assert same
+    same = all(torch.equal(x.view(torch.int32), y.view(torch.int32)) for x, y in zip(gr[0], gr[4]))
+    same &= torch.equal(gr[0][0].view(torch.int32), gx["c"][0].transpose(1, 2).contiguous().view(torch.int32))
+    print(f"backward slot buckets vs staged passes (and vs the planes form) bit-identical: {same}", flush=True)
     assert same
     forms = {k: v[1] for k, v in fw.items()}
     forms.update(bw)

@@ -32,6 +32,8 @@ def main():
     ws = pcm_hip.chamfer_workspace(dev, b, n, m)
     w1, w2 = 1.0 / (b * n), 1.0 / (b * m)
     vs = list(range(7, pcm_hip.tune_num_chamfer_loss_grad_variants()))
+    if os.environ.get("AB_VARIANTS"):  # e.g. AB_VARIANTS=11,15
+        vs = [int(v) for v in os.environ["AB_VARIANTS"].split(",")]
     out = {}
     # a zero-filled workspace per variant: variants of different granule formats
     # sharing one would make each switch's first call recompute every argmin
@@ -40,7 +42,7 @@ def main():
         pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, wss[v], variant=v)
         torch.cuda.synchronize()
         out[v] = [t.clone() for t in (d1, d2, i1, i2, gx1, gx2, mo)]
-    same = {v: all(torch.equal(a, r) for a, r in zip(out[v], out[7])) for v in vs}
+    same = {v: all(torch.equal(a, r) for a, r in zip(out[v], out[vs[0]])) for v in vs}
     graphs = {v: graph_of(lambda v=v: pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, wss[v],
                                                                 variant=v), reps) for v in vs}
     res = {v: [] for v in vs}

@@ -20,6 +20,7 @@
 #   probe      tools/probe_replay.py (timed-region overhead by launch form)
 #   benchab    the driver's bench command twice per side-leg order (same box)
 #   probeev    tools/probe_events.py (does recording the region's timing events cost wall time)
+#   abcl       tools/ab_chamfer.sh (the A/B across lib/libpcm_hip_{base,v*}.so builds, twice)
 #   abr        tools/ab_ref_call.py (the unchanged caller's pieces: forward geometries, strided backward)
 set -o pipefail
 TAG=$1
@@ -60,6 +61,7 @@ for S in "$@"; do
               timeout -k 10 300 python -u tools/stamp_lgrid.py 11 >> "$O/stamps_lgrid.txt" 2>&1 ;;
     probe) timeout -k 10 300 python -u tools/probe_replay.py > "$O/probe_replay.txt" 2>&1 &&
            timeout -k 10 300 python -u tools/probe_timed.py > "$O/probe_timed.txt" 2>&1 ;;
+    abcl) timeout -k 10 900 bash tools/ab_chamfer.sh > "$O/ab_chamfer_libs.txt" 2>&1 ;;
     abr) timeout -k 10 300 python -u tools/ab_ref_call.py > "$O/ab_ref_call.txt" 2>&1 ;;
     benchab) for i in 1 2; do for o in first last; do
                timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 --side-legs $o \

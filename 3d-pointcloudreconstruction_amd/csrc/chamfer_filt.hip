@@ -2207,6 +2207,9 @@ const GradVariant kGradVariants[] = {
     // 15: 14 with four granules per 16-byte write-through store (a quarter of the fabric writes)
     {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true>, 8, 4},
 };
+// (round 5, rejected: 15 with two queries per lane -- 128-query workgroups,
+// two per CU, four waves per SIMD -- 15.45 us against 13.39 us,
+// profiles/r05/ab_qpt2_r05t.txt)
 // (round 4, rejected: 7 and 11 with 16 waves -- four per SIMD, a 16-way
 // merge -- 15.9-16.2 us against 13.85 us, profiles/r04/chamfer_w16_r04n_ab.txt)
 // (round 4, rejected: 7 with the raw target rows parked in an LDS region of

@@ -1869,19 +1869,38 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
     const int total = b * per;
     float s1 = 0.f, s2 = 0.f;
     bool ok = true;
-    for (int base = 0; base < total && ok; base += 64) {
-        const int i = base + lane;
-        unsigned long long x = (unsigned long long)epoch << 32;
+    // kPollPer granules per lane in flight at once (one round trip per sweep,
+    // not one per 64 granules: the last producer's partial is then summed one
+    // load latency after it lands), summed per lane in ascending i -- the
+    // order of a 64-wide sweep, so the means keep their bits
+    constexpr int kPollPer = 8;
+    for (int base = 0; base < total && ok; base += 64 * kPollPer) {
+        unsigned long long x[kPollPer];
+#pragma unroll
+        for (int c = 0; c < kPollPer; ++c)  // past the end: ready; else not yet read
+            x[c] = (unsigned long long)(base + 64 * c + lane < total ? epoch - 1u : epoch) << 32;
         for (unsigned spins = 0;; ++spins) {
-            if (i < total) x = __hip_atomic_load(ws.wg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__all((unsigned)(x >> 32) == epoch)) break;
+            bool ready = true;
+#pragma unroll
+            for (int c = 0; c < kPollPer; ++c) {
+                const int i = base + 64 * c + lane;
+                if (i < total && (unsigned)(x[c] >> 32) != epoch)
+                    x[c] = __hip_atomic_load(ws.wg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+#pragma unroll
+            for (int c = 0; c < kPollPer; ++c) ready &= (unsigned)(x[c] >> 32) == epoch;
+            if (__all(ready)) break;
             if (spins >= max_spins) { ok = false; break; }
             __builtin_amdgcn_s_sleep(1);
         }
-        const float v = __uint_as_float((unsigned)x);
-        if (i < total) {
-            if (i % per < nblk1) s1 += v;
-            else s2 += v;
+#pragma unroll
+        for (int c = 0; c < kPollPer; ++c) {
+            const int i = base + 64 * c + lane;
+            const float v = __uint_as_float((unsigned)x[c]);
+            if (i < total) {
+                if (i % per < nblk1) s1 += v;
+                else s2 += v;
+            }
         }
     }
     s1 = wave_sum(s1);

@@ -21,6 +21,7 @@
 #   benchab    the driver's bench command twice per side-leg order (same box)
 #   probeev    tools/probe_events.py (does recording the region's timing events cost wall time)
 #   abcl       tools/ab_chamfer.sh (the A/B across lib/libpcm_hip_{base,v*}.so builds, twice)
+#   emddiag    tools/emd_diag.py: config 3 per iteration, the training call by bidder count
 #   abr        tools/ab_ref_call.py (the unchanged caller's pieces: forward geometries, strided backward)
 set -o pipefail
 TAG=$1
@@ -56,12 +57,14 @@ for S in "$@"; do
                -- python3 tools/grid_diag.py > "$O/gridkt.log" 2>&1 ;;
     pmc) timeout -k 10 900 bash tools/pmc_passes.sh "$O/pmc" > "$O/pmc_passes.log" 2>&1 ;;
     stamps) PCM_HIP_LIB=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_stamps.so timeout -k 10 300 \
-               python -u tools/stamp_filt.py fused 7 11 > "$O/stamps_fused.txt" 2>&1 ;;
+               python -u tools/stamp_filt.py fused 15 11 > "$O/stamps_fused.txt" 2>&1 ;;
     stampslg) timeout -k 10 300 python -u tools/stamp_lgrid.py 13 > "$O/stamps_lgrid.txt" 2>&1 &&
               timeout -k 10 300 python -u tools/stamp_lgrid.py 11 >> "$O/stamps_lgrid.txt" 2>&1 ;;
     probe) timeout -k 10 300 python -u tools/probe_replay.py > "$O/probe_replay.txt" 2>&1 &&
            timeout -k 10 300 python -u tools/probe_timed.py > "$O/probe_timed.txt" 2>&1 ;;
     abcl) timeout -k 10 900 bash tools/ab_chamfer.sh > "$O/ab_chamfer_libs.txt" 2>&1 ;;
+    emddiag) timeout -k 10 300 python -u tools/emd_diag.py --per-iter > "$O/emd_diag_c3.txt" 2>&1 &&
+             timeout -k 10 300 python -u tools/emd_diag.py --train --by-nu > "$O/emd_diag_train.txt" 2>&1 ;;
     abr) timeout -k 10 300 python -u tools/ab_ref_call.py > "$O/ab_ref_call.txt" 2>&1 ;;
     benchab) for i in 1 2; do for o in first last; do
                timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 --side-legs $o \

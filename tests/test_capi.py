@@ -62,3 +62,33 @@ def test_invalid_arguments_rejected_without_device(lib):
     assert L.pcm_chamfer_forward(null, null, 0, 4, 4, null, null, null, null, null) == 0
     assert L.pcm_emd_forward(null, null, 0, 1024, 0.005, 50, null, null, null, null, 0, null) == 0
     assert pcm_hip.emd_workspace_bytes(16, 1024) >= 0
+
+
+def test_layout_and_strided_entries_reject_bad_arguments(lib):
+    # pcm_chamfer_forward_layout / _backward_layout / _backward_strided check
+    # layouts, sizes, strides and pointers before any device call
+    L = lib
+    null = None
+    # layouts are 0 (rows) or 1 (channel planes)
+    assert L.pcm_chamfer_forward_layout(null, null, 2, 4, 4, 2, 0, null, null, null, null, null) == -1
+    assert L.pcm_chamfer_forward_layout(null, null, 2, 4, 4, 0, -1, null, null, null, null, null) == -1
+    assert L.pcm_chamfer_backward_layout(null, null, 2, 4, 4, 0, 3, null, null, null, null, null, null, null) == -1
+    assert L.pcm_chamfer_backward_strided(null, null, 2, 4, 4, 5, 0, null, 4, 1, null, 4, 1, null, null, null, null,
+                                          null) == -1
+    # negative sizes, null pointers with non-empty shapes
+    assert L.pcm_chamfer_forward_layout(null, null, -1, 4, 4, 1, 0, null, null, null, null, null) == -1
+    assert L.pcm_chamfer_forward_layout(null, null, 2, 4, 4, 1, 0, null, null, null, null, null) == -1
+    # graddist strides must be >= 0 and fit an int
+    assert L.pcm_chamfer_backward_strided(null, null, 2, 4, 4, 0, 0, null, -1, 1, null, 4, 1, null, null, null, null,
+                                          null) == -1
+    assert L.pcm_chamfer_backward_strided(null, null, 2, 4, 4, 0, 0, null, 4, 1 << 31, null, 4, 1, null, null, null,
+                                          null, null) == -1
+    # the backward needs both clouds non-empty, and its pointers
+    assert L.pcm_chamfer_backward_strided(null, null, 2, 0, 4, 0, 0, null, 0, 0, null, 0, 0, null, null, null, null,
+                                          null) == -1
+    assert L.pcm_chamfer_backward_strided(null, null, 2, 4, 4, 0, 0, null, 0, 0, null, 0, 0, null, null, null, null,
+                                          null) == -1
+    # empty problems are no-ops
+    assert L.pcm_chamfer_forward_layout(null, null, 0, 4, 4, 1, 1, null, null, null, null, null) == 0
+    assert L.pcm_chamfer_backward_strided(null, null, 0, 4, 4, 1, 0, null, 0, 0, null, 0, 0, null, null, null, null,
+                                          null) == 0

@@ -1245,17 +1245,19 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
 // (dist_chamfer_3D.py:79-80), this reads it in place.  Same results as
 // pcm_chamfer_forward on the rows, bit for bit (the same arithmetic on the
 // same values).
-template <int W, int QPT, int C, int TILE>
+// (the layouts are template arguments: a row stride known at compile time
+// lets the loads of a point's three coordinates merge)
+template <int W, int QPT, int C, int TILE, int LAY1, int LAY2>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_fwd_filt_lay_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1,
-    int32_t *__restrict__ idx2, int nblk1, int nblk2, int lay1, int lay2) {
+    int32_t *__restrict__ idx2, int nblk1, int nblk2) {
     constexpr int QW = 64 * QPT;
     int batch, blk;
     bool first;
     pcm_split_bm(pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x), nblk1, nblk2, batch, first, blk);
     const float *X1 = xyz1 + (size_t)batch * n * 3, *X2 = xyz2 + (size_t)batch * m * 3;
-    const PcmLay L1 = pcm_lay(lay1, n), L2 = pcm_lay(lay2, m);
+    const PcmLay L1 = LAY1 ? PcmLay{1, n} : PcmLay{3, 1}, L2 = LAY2 ? PcmLay{1, m} : PcmLay{3, 1};
     if (first)
         filt_forward<float, W, QPT, C, TILE, false>(X1, X2, n, m, blk * QW, dist1 + (size_t)batch * n,
                                                    idx1 + (size_t)batch * n, lds_arena<FiltLds<W, QPT, TILE>::kBytes>(),
@@ -2364,14 +2366,17 @@ int launch_fwd_layout(int variant, const float *xyz1, const float *xyz2, int b, 
     const long long blocks = (long long)b * (nblk1 + nblk2);
     if (blocks > 0x7ffffffeLL) return PCM_ERR_UNSUPPORTED;
     if (blocks == 0) return PCM_OK;
-    if (variant == 0)
-        hipLaunchKernelGGL((chamfer_fwd_filt_lay_kernel<W, QPT, 32, 2048>), dim3((unsigned)blocks), dim3(64 * W), 0,
-                           (hipStream_t)stream, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nblk1, nblk2, layout1,
-                           layout2);
-    else
-        hipLaunchKernelGGL((chamfer_fwd_filt_lay_kernel<W, QPT, 16, 1024>), dim3((unsigned)blocks), dim3(64 * W), 0,
-                           (hipStream_t)stream, xyz1, xyz2, b, n, m, dist1, dist2, idx1, idx2, nblk1, nblk2, layout1,
-                           layout2);
+    typedef void (*lay_kernel_t)(const float *, const float *, int, int, int, float *, float *, int32_t *, int32_t *,
+                                 int, int);
+    static const lay_kernel_t k32[4] = {
+        chamfer_fwd_filt_lay_kernel<W, QPT, 32, 2048, 0, 0>, chamfer_fwd_filt_lay_kernel<W, QPT, 32, 2048, 0, 1>,
+        chamfer_fwd_filt_lay_kernel<W, QPT, 32, 2048, 1, 0>, chamfer_fwd_filt_lay_kernel<W, QPT, 32, 2048, 1, 1>};
+    static const lay_kernel_t k16[4] = {
+        chamfer_fwd_filt_lay_kernel<W, QPT, 16, 1024, 0, 0>, chamfer_fwd_filt_lay_kernel<W, QPT, 16, 1024, 0, 1>,
+        chamfer_fwd_filt_lay_kernel<W, QPT, 16, 1024, 1, 0>, chamfer_fwd_filt_lay_kernel<W, QPT, 16, 1024, 1, 1>};
+    const lay_kernel_t k = (variant == 0 ? k32 : k16)[2 * layout1 + layout2];
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * W), 0, (hipStream_t)stream, xyz1, xyz2, b, n, m, dist1,
+                       dist2, idx1, idx2, nblk1, nblk2);
     return pcm_launch_status();
 }
 }  // namespace

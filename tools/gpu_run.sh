@@ -67,6 +67,11 @@ for S in "$@"; do
              timeout -k 10 300 python -u tools/emd_diag.py --train --by-nu > "$O/emd_diag_train.txt" 2>&1 ;;
     emdstamps) PCM_HIP_LIB=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_stamps.so timeout -k 10 300 \
                python -u tools/emd_diag.py > "$O/emd_stamps_c3.txt" 2>&1 ;;
+    abrl) for r in 1 2; do for lib in base default; do
+              if [ $lib = base ]; then L=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_base.so; else L=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip.so; fi
+              echo "== $lib" >> "$O/ab_ref_call_libs.txt"
+              PCM_HIP_LIB=$L timeout -k 10 300 python -u tools/ab_ref_call.py >> "$O/ab_ref_call_libs.txt" 2>&1 || exit 1
+          done; done ;;
     abr) timeout -k 10 300 python -u tools/ab_ref_call.py > "$O/ab_ref_call.txt" 2>&1 ;;
     benchab) for i in 1 2; do for o in first last; do
                timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 --side-legs $o \

@@ -375,18 +375,8 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
 #pragma unroll
                 for (int g = 0; g < G; ++g) {
                     const pcm_f4 X4 = X4n, Y4 = Y4n, Z4 = Z4n, W4 = W4n;
-#ifdef PCM_PROBE_HALF_LDS
-                    // timing probe only, wrong results (tools/stamp_filt.py on a variant build): every
-                    // other group reuses the previous candidates -- the same VALU work, half the LDS
-                    // broadcast reads (scan 6.0 -> 4.0 us: the reads, not the VALU, bind the scan)
-                    if (g & 1) {
-                        if (g + 1 < G) fetch(c, g + 1);
-                        else fetch(cn, 0);
-                    }
-#else
                     if (g + 1 < G) fetch(c, g + 1);
                     else fetch(cn, 0);
-#endif
                     // the next group's four reads stay ahead of this group's math
                     // (hipcc otherwise sinks them to their use and waits on each)
                     __builtin_amdgcn_sched_barrier(0);

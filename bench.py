@@ -466,6 +466,25 @@ def emd_executed_roofline(us):
             "source": os.path.relpath(PMC_SUMMARY, REPO)}
 
 
+def chamfer_executed_roofline(kernel, us):
+    """The one-launch kernel's executed VALU work: its counter VALU wave
+    instructions per launch (rocprofv3 SQ_INSTS_VALU, committed PMC summary)
+    x 64 lanes / this run's kernel time, against the 78.6 T lane-instruction
+    issue ceiling -- what the VALU actually issued, beside the algorithmic
+    8-FLOP-per-pair figure; with the counters' wait share."""
+    try:
+        with open(PMC_SUMMARY) as fh:
+            c = json.load(fh)["counters"][kernel]
+        waves = c["SQ_INSTS_VALU"]
+        wait = c["SQ_WAIT_ANY"] / c["SQ_WAVE_CYCLES"]
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None
+    rate = waves * 64 / (us * 1e-6)
+    return {"bound": "valu", "valu_wave_instructions": waves, "achieved": rate / 1e12,
+            "peak": VALU_LANE_OPS_PEAK / 1e12, "unit": "T lane-ops/s", "frac": rate / VALU_LANE_OPS_PEAK,
+            "wait_share": wait, "source": os.path.relpath(PMC_SUMMARY, REPO)}
+
+
 def dense_f16_leg(dev, reps=10):
     """BASELINE config 5: dense Chamfer fwd+bwd, B=8, N=M=16384, fp16 clouds
     (fp32 arithmetic on the exactly-widened coordinates), graph-timed."""
@@ -899,6 +918,7 @@ def main(argv=None):
         out["graph"] = graph_info
         out["warmup_steps_run"] = graph_info["warmup_steps_run"]
     out["roofline"]["step_minus_kernel_us"] = ms * 1000.0 - dom_us
+    out["roofline_executed"] = chamfer_executed_roofline(dom_kernel, dom_us)
     if capture_error is not None:
         out["config"]["allreduce_capture_error"] = capture_error
     if multi:

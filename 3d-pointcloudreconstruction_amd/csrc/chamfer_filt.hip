@@ -812,7 +812,7 @@ __device__ __forceinline__ unsigned bf_pair(unsigned lo, unsigned hi) {
 // Three-way bf16 split of (a, b): a = lo16 parts of H, M, L; b = the high parts.
 // Each level is the RNE bf16 of the remainder of the levels above; every
 // remainder is exact in fp32.
-__device__ __forceinline__ void split3x2(float a, float b, unsigned &H, unsigned &M, unsigned &L) {
+[[maybe_unused]] __device__ __forceinline__ void split3x2(float a, float b, unsigned &H, unsigned &M, unsigned &L) {
     H = cvt_bf16x2(a, b);
     const float ra = a - bf_lo(H), rb = b - bf_hi(H);
     M = cvt_bf16x2(ra, rb);
@@ -820,7 +820,7 @@ __device__ __forceinline__ void split3x2(float a, float b, unsigned &H, unsigned
 }
 // 64-target groups of the raw tile rotated by 4 (group mod 8): the rescan's
 // lanes -- one query each, chunks of stride-16 quads -- spread over the banks
-__device__ __forceinline__ int mslot(int p) { return (p & ~63) | ((p + 4 * ((p >> 6) & 7)) & 63); }
+[[maybe_unused]] __device__ __forceinline__ int mslot(int p) { return (p & ~63) | ((p + 4 * ((p >> 6) & 7)) & 63); }
 
 template <bool kSc1>
 __device__ __forceinline__ float filt_forward_mfma(const float *__restrict__ Q, const float *__restrict__ T, int nq,
@@ -1262,6 +1262,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
 // Fused loss + gradient
 // ---------------------------------------------------------------------------
 constexpr int kGradCap = 1024;   // points per cloud the per-element backward holds in LDS
+// 4-byte argmin granules (variants 14, 15, 13): {tag (21 bits) << 11 | idx}
+constexpr unsigned kG4TagBits = 21;
+constexpr unsigned kG4TagMask = (1u << kG4TagBits) - 1u;
+static_assert(kGradCap <= 2048, "a 4-byte granule holds an 11-bit index");
 // Bound of a gradient-phase wait on the other workgroups' argmins (polls of
 // about a microsecond each): past it the workgroup computes what is missing
 // itself.  The loss poll (pcm_loss::kPollMaxSpins) waits longer: its
@@ -1387,15 +1391,39 @@ __device__ __forceinline__ void scatter_sum(float &ax, float &ay, float &az, flo
 // by an ordered scan of the other cloud's argmins.  Same arithmetic and order
 // as the reference's kernels (chamfer3D.cu:155-195), bit-identical.
 // ---------------------------------------------------------------------------
+//
+// Rescale mode (RS.gl != nullptr; pcm_chamfer_loss_grad_rescale): the backward
+// of a one-launch step (pcm_chamfer_loss_grad_layout) whose gradient was
+// computed for an expected upstream scale *RS.used.  If the real upstream
+// gradient *RS.gl has the same bits, the step's gradient is already exact and
+// every workgroup returns at once; otherwise this recomputes it with the
+// scalar graddists fl(*RS.gl * inv) -- torch's mean backward -- in place.
+// Either way *RS.next = *RS.gl (the next step's expectation).
+// ---------------------------------------------------------------------------
 constexpr int kBwdSlotsT = 256;      // targets per workgroup = threads
 constexpr int kBwdSlotsMax = 2048;   // points of the other cloud staged in LDS
+
+struct PcmRescale {
+    const float *gl = nullptr;    // device: the upstream gradient of the loss
+    const float *used = nullptr;  // device: the scale the step used (nullptr: always recompute)
+    float *next = nullptr;        // device: receives *gl (nullable)
+    float inv1 = 0.f, inv2 = 0.f; // fl(1 / (b n)), fl(1 / (b m))
+};
 
 __global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
     const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
     const int32_t *__restrict__ idx2, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
-    int lay1, int lay2, PcmGdStr GS) {
+    int lay1, int lay2, PcmGdStr GS, PcmRescale RS) {
     constexpr int NT = kBwdSlotsT;
+    float rs1 = 0.f, rs2 = 0.f;  // rescale mode: the two scalar graddists
+    if (RS.gl) {
+        const float gl = *RS.gl;
+        if (RS.next && blockIdx.x == 0 && threadIdx.x == 0) *RS.next = gl;
+        if (RS.used && __float_as_uint(*RS.used) == __float_as_uint(gl)) return;  // the step's gradient stands
+        rs1 = __fmul_rn(gl, RS.inv1);
+        rs2 = __fmul_rn(gl, RS.inv2);
+    }
     __shared__ __attribute__((aligned(16))) float sO[3 * kBwdSlotsMax];  // other cloud, its layout
     __shared__ __attribute__((aligned(16))) float sG[kBwdSlotsMax];      // other graddist
     __shared__ __attribute__((aligned(16))) int sK[kBwdSlotsMax];        // other argmins
@@ -1407,12 +1435,13 @@ __global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
     bool first;
     pcm_split_bm(pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x), nblk1, nblk2, batch, first, blk);
     const int ns = first ? n : m, no = first ? m : n;
+    const float rs_self = first ? rs1 : rs2, rs_other = first ? rs2 : rs1;
     const float *self = first ? xyz1 + (size_t)batch * n * 3 : xyz2 + (size_t)batch * m * 3;
     const float *other = first ? xyz2 + (size_t)batch * m * 3 : xyz1 + (size_t)batch * n * 3;
     const int gbs = first ? (GS.bs1 < 0 ? n : GS.bs1) : (GS.bs2 < 0 ? m : GS.bs2);
     const int gbo = first ? (GS.bs2 < 0 ? m : GS.bs2) : (GS.bs1 < 0 ? n : GS.bs1);
-    const int gps = first ? GS.ps1 : GS.ps2, gpo = first ? GS.ps2 : GS.ps1;
-    const float *gds = (first ? gd1 : gd2) + (size_t)batch * gbs;
+    const int gps = RS.gl ? 0 : (first ? GS.ps1 : GS.ps2), gpo = RS.gl ? 0 : (first ? GS.ps2 : GS.ps1);
+    const float *gds = (first ? gd1 : gd2) + (size_t)batch * gbs;  // (not read in rescale mode)
     const float *gdo = (first ? gd2 : gd1) + (size_t)batch * gbo;
     const int32_t *ids = (first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m);
     const int32_t *ido = (first ? idx2 + (size_t)batch * m : idx1 + (size_t)batch * n);
@@ -1427,7 +1456,9 @@ __global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
     // graddists of the other cloud: by LDS-DMA when contiguous, one register
     // when an expanded scalar (stride 0), else strided loads
     float hconst = 0.f;
-    if (gpo == 1)
+    if (RS.gl)
+        hconst = __fmul_rn(rs_other, 2.f);
+    else if (gpo == 1)
         pcm_dma_to_lds(sG, gdo, 4 * no, wave, NT / 64);
     else if (gpo == 0)
         hconst = __fmul_rn(gdo[0], 2.f);
@@ -1442,7 +1473,7 @@ __global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
         sy = self[pcm_at(LS, i, 1)];
         sz = self[pcm_at(LS, i, 2)];
         kself = ids[i];
-        gself = gds[(size_t)i * gps];
+        gself = RS.gl ? rs_self : gds[(size_t)i * gps];
     }
     cnt[tid] = 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1529,7 +1560,9 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                                            const void *__restrict__ Goth_v = nullptr,
                                            unsigned long long tag = 0, unsigned max_spins = 0,
                                            unsigned *slow = nullptr, const pcm_f4 *TA = nullptr,
-                                           const pcm_f4 *SO = nullptr, int own_k = -1) {
+                                           const pcm_f4 *SO = nullptr, int own_k = -1,
+                                           PcmLay LS = PcmLay{3, 1}, PcmLay LA = PcmLay{3, 1},
+                                           PcmLay LG = PcmLay{3, 1}) {
     typedef typename std::conditional<kG4, unsigned, unsigned long long>::type gran_t;
     const gran_t *Gown = reinterpret_cast<const gran_t *>(Gown_v);
     const gran_t *Goth = reinterpret_cast<const gran_t *>(Goth_v);
@@ -1553,9 +1586,9 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
             y = t4.y;
             z = t4.z;
         } else {
-            x = A[3 * i];
-            y = A[3 * i + 1];
-            z = A[3 * i + 2];
+            x = A[pcm_at(LA, i, 0)];
+            y = A[pcm_at(LA, i, 1)];
+            z = A[pcm_at(LA, i, 2)];
         }
     };
     auto getS = [&](int t, float &x, float &y, float &z) {
@@ -1565,9 +1598,9 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
             y = s4.y;
             z = s4.z;
         } else {
-            x = S[3 * (q0 + t)];
-            y = S[3 * (q0 + t) + 1];
-            z = S[3 * (q0 + t) + 2];
+            x = S[pcm_at(LS, q0 + t, 0)];
+            y = S[pcm_at(LS, q0 + t, 1)];
+            z = S[pcm_at(LS, q0 + t, 2)];
         }
     };
     constexpr int NW = NT / 64;
@@ -1623,7 +1656,7 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                     float d, x, y, z;
                     int k;
                     getS(tid, x, y, z);
-                    pcm_ref_nn_scan(x, y, z, A, na, d, k);
+                    pcm_ref_nn_scan(x, y, z, A, na, d, k, LA);
                     go = tagv | (gran_t)k;
                 }
 #pragma unroll
@@ -1633,7 +1666,7 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                         float d, x, y, z;
                         int k;
                         getA(i, x, y, z);
-                        pcm_ref_nn_scan(x, y, z, S, nq, d, k);
+                        pcm_ref_nn_scan(x, y, z, S, nq, d, k, LS);
                         gr[r] = tagv | (gran_t)k;
                     }
                 }
@@ -1695,9 +1728,9 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                 ay = __fadd_rn(ay, dy);
                 az = __fadd_rn(az, dz);
             }
-            G[3 * jt] = ax;
-            G[3 * jt + 1] = ay;
-            G[3 * jt + 2] = az;
+            G[pcm_at(LG, jt, 0)] = ax;
+            G[pcm_at(LG, jt, 1)] = ay;
+            G[pcm_at(LG, jt, 2)] = az;
         } else {
             sOvf[atomicAdd(&sNOvf, 1)] = tid;
         }
@@ -1753,9 +1786,9 @@ __device__ __forceinline__ bool range_grad(bool dir1, int q0, int nq, int na, co
                 ay = __fadd_rn(ay, dy);
                 az = __fadd_rn(az, dz);
             }
-            G[3 * j] = ax;
-            G[3 * j + 1] = ay;
-            G[3 * j + 2] = az;
+            G[pcm_at(LG, j, 0)] = ax;
+            G[pcm_at(LG, j, 1)] = ay;
+            G[pcm_at(LG, j, 2)] = az;
         }
         __syncthreads();
     }
@@ -1786,6 +1819,7 @@ constexpr int kGradSlowWord = 5;  // diagnostics: gradient-phase waits that time
 // or granule format trusts no granule: its gradient phase computes every
 // argmin it needs itself (the timeout path: exact, slow, once).
 constexpr int kGradShapeWord = 6;
+static_assert(kGradCap <= 4096, "grad_shape_word packs n - 1 and m - 1 into 12 bits each");
 __host__ __device__ __forceinline__ unsigned grad_shape_word(int n, int m, unsigned fmt) {
     return (fmt << 24) | ((unsigned)(n - 1) << 12) | (unsigned)(m - 1);  // n, m <= 1024; fmt 1 or 2: never 0
 }
@@ -1819,7 +1853,7 @@ inline GradWs grad_ws(void *base, int b, long long blocks) {
 // the grid's last workgroup: sweep the 2b granules until all carry this
 // call's epoch (bounded: NaN means on timeout), fixed-order sums, advance the
 // epoch (chamfer_loss.h poll_loss, with the granules per batch element)
-__device__ __forceinline__ void poll_grad_loss(int b, int n, int m, const GradWs &ws, float *__restrict__ mean_out,
+[[maybe_unused]] __device__ __forceinline__ void poll_grad_loss(int b, int n, int m, const GradWs &ws, float *__restrict__ mean_out,
                                                unsigned max_spins) {
     if (threadIdx.x >= 64) return;
     const int lane = threadIdx.x;
@@ -1921,15 +1955,27 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
     }
 }
 
-#include "chamfer_lgrid.h"
+#ifdef PCM_TUNE
+#include "chamfer_lgrid.h"  // fused variant 13 (rejected, tuning build only)
+#endif
 
+// LAY1 / LAY2 (the default variant's layout instances): cloud 1 / 2 given as
+// channel planes [b, 3, n] (pcm_common.h PcmLay) -- train.py:163's
+// fake.transpose(2, 1) read in place -- and its gradient written in the same
+// layout.  gscale (nullable, device): the upstream gradient the step is
+// expected to receive; the gradients are then those of
+// gscale * (w1 sum(dist1) + w2 sum(dist2)) with graddist = fl(gscale * w) as
+// torch's mean backward forms it, and mean_out[3] records the scale used
+// (pcm_chamfer_loss_grad_rescale checks it against the real one).
 template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false,
-          bool kLocal = false, bool kSplit = false, bool kG4 = false, bool kG4x = false>
+          bool kLocal = false, bool kSplit = false, bool kG4 = false, bool kG4x = false, int LAY1 = 0, int LAY2 = 0>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
     float *__restrict__ mean_out, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
-    GradWs ws, unsigned max_spins, unsigned poll_spins) {
+    GradWs ws, unsigned max_spins, unsigned poll_spins, const float *__restrict__ gscale) {
+    static_assert((LAY1 == 0 && LAY2 == 0) || (kGran && kLocal && kG4 && !kEarly && !kMfma),
+                  "channel planes: the local-gradient 4-byte granule form");
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
     static_assert(!kMfma || (W == 8 && QPT == 4 && TILE == kMfmaTile), "the MFMA forward's fixed geometry");
@@ -1953,12 +1999,19 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     unsigned char *arena = lds_arena<kArena>();
     unsigned char *garena = kEarly ? lds_arena<kGradBytes, 1>() : arena;  // gradient phase
     const int nprod = (int)gridDim.x - 1;
+    float gsc = 1.f;
+    if (gscale) {  // graddist = fl(upstream * w), torch's mean backward (a scalar load, hidden by the forward)
+        gsc = *gscale;
+        w1 = __fmul_rn(gsc, w1);
+        w2 = __fmul_rn(gsc, w2);
+    }
     if ((int)blockIdx.x == nprod) {
         PCM_STAMP2(5);
         if constexpr (kGran)
             poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, poll_spins,
                               grad_shape_word(n, m, kG4 ? 2u : 1u));
         else poll_grad_loss(b, n, m, ws, mean_out, poll_spins);
+        if (gscale && threadIdx.x == 0) mean_out[3] = gsc;
         PCM_STAMP2(6);
         return;
     }
@@ -1973,6 +2026,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int q0 = (first ? r : r - nblk1) * QW;
     const float *X1 = xyz1 + (size_t)batch * n * 3;
     const float *X2 = xyz2 + (size_t)batch * m * 3;
+    const PcmLay L1 = LAY1 ? PcmLay{1, n} : PcmLay{3, 1}, L2 = LAY2 ? PcmLay{1, m} : PcmLay{3, 1};
     if constexpr (kGran) {
         // ---- granule hand-off (no counters): the forward publishes every
         // argmin as a {tag, idx} granule and the workgroup's partial as a
@@ -1982,20 +2036,34 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         // kG4: 4-byte argmin granules {tag (21 bits) << 11 | idx}, cloud 1 then
         // cloud 2 (chamfer_lgrid.h's layout); the range's own argmins come
         // from this workgroup's forward (no granule read)
-        const unsigned tag4 = ((ws.epoch[0] + 1u) & kLgTagMask) << 11;
+        const unsigned tag4 = ((ws.epoch[0] + 1u) & kG4TagMask) << 11;
         unsigned *H1 = reinterpret_cast<unsigned *>(ws.ig) + (size_t)batch * n;
         unsigned *H2 = reinterpret_cast<unsigned *>(ws.ig) + (size_t)b * n + (size_t)batch * m;
         int myk = -1;
         unsigned long long *G1 = ws.ig + (size_t)batch * n, *G2 = ws.ig + (size_t)b * n + (size_t)batch * m;
         const PreDma pre{garena, X1, 12 * n, garena + 12 * kGradCap, X2, 12 * m};
         __shared__ pcm_f4 sQown[kLocal ? QW : 1];  // kLocal: the range's points (the forward's queries)
-        const float my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
-            first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
-            first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
-            first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, kG4 ? nullptr : (first ? G1 : G2),
-            tag, kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, PcmLay{3, 1}, PcmLay{3, 1},
-            kG4 ? (first ? H1 : H2) : nullptr, tag4, kG4 ? &myk : nullptr,
-            kG4x && ((n | m) & 3) == 0);  // 16-byte granule stores when every row start is 16-byte aligned
+        // 16-byte granule stores when every row start is 16-byte aligned
+        const bool g4x = kG4x && ((n | m) & 3) == 0;
+        float my_d;
+        if constexpr (LAY1 == LAY2) {
+            const PcmLay LQ = LAY1 ? PcmLay{1, first ? n : m} : PcmLay{3, 1};
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
+                first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
+                first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
+                first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, kG4 ? nullptr : (first ? G1 : G2),
+                tag, kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, LQ,
+                LAY1 ? PcmLay{1, first ? m : n} : PcmLay{3, 1}, kG4 ? (first ? H1 : H2) : nullptr, tag4,
+                kG4 ? &myk : nullptr, g4x);
+        } else if (first) {  // mixed layouts: each direction's strides known at compile time
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
+                X1, X2, n, m, q0, dist1 + (size_t)batch * n, idx1 + (size_t)batch * n, arena, nullptr, tag, nullptr,
+                sQown, L1, L2, H1, tag4, &myk, g4x);
+        } else {
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
+                X2, X1, m, n, q0, dist2 + (size_t)batch * m, idx2 + (size_t)batch * m, arena, nullptr, tag, nullptr,
+                sQown, L2, L1, H2, tag4, &myk, g4x);
+        }
         PCM_STAMP2(1);
         const float s = wave_sum(my_d);
         if (lane == 0) sRed[wave] = s;
@@ -2022,10 +2090,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
             if constexpr (kG4)
                 ok = first ? range_grad<NT, QW, true, C, true>(true, q0, n, m, X1, X2, g1, g2, nullptr, nullptr, G,
                                                                arena + kTileBytes, H1, H2, tag4, max_spins,
-                                                               ws.epoch + kGradSlowWord, TA, sQown, myk)
+                                                               ws.epoch + kGradSlowWord, TA, sQown, myk, L1, L2, L1)
                            : range_grad<NT, QW, true, C, true>(false, q0, m, n, X2, X1, g2, g1, nullptr, nullptr, G,
                                                                arena + kTileBytes, H2, H1, tag4, max_spins,
-                                                               ws.epoch + kGradSlowWord, TA, sQown, myk);
+                                                               ws.epoch + kGradSlowWord, TA, sQown, myk, L2, L1, L2);
             else
                 ok = first ? range_grad<NT, QW, true, C>(true, q0, n, m, X1, X2, g1, g2, nullptr, nullptr, G,
                                                          arena + kTileBytes, G1, G2, tag, max_spins,
@@ -2046,8 +2114,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (!ok) {  // a workgroup of this element never published: sticky error, NaN gradients
             if (tid == 0) __hip_atomic_store(ws.epoch + kGradErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const int nq = first ? n : m;
+            const PcmLay LG = first ? L1 : L2;
             for (int t = tid; t < 3 * QW; t += NT)
-                if (q0 * 3 + t < 3 * nq) G[3 * q0 + t] = __builtin_nanf("");
+                if (q0 + t / 3 < nq) G[pcm_at(LG, q0 + t / 3, t % 3)] = __builtin_nanf("");
         }
         PCM_STAMP2(7);
         return;
@@ -2166,7 +2235,36 @@ int pcm_launch_bwd_slots(const float *xyz1, const float *xyz2, int b, int n, int
     const long long blocks = (long long)b * (nblk1 + nblk2);
     if (blocks > 0x7fffffffLL) return PCM_ERR_UNSUPPORTED;
     hipLaunchKernelGGL(chamfer_bwd_slots_kernel, dim3((unsigned)blocks), dim3(kBwdSlotsT), 0, stream, xyz1, xyz2, b,
-                       n, m, gd1, gd2, idx1, idx2, grad1, grad2, nblk1, nblk2, lay1, lay2, GS);
+                       n, m, gd1, gd2, idx1, idx2, grad1, grad2, nblk1, nblk2, lay1, lay2, GS, PcmRescale());
+    return pcm_launch_status();
+}
+
+// The backward of a one-launch step whose upstream gradient was not known when
+// it ran (chamfer_bwd_slots_kernel's rescale mode): a no-op launch when
+// *grad_loss equals *scale_used bit for bit, else the exact gradients of
+// *grad_loss * (w1 sum(dist1) + w2 sum(dist2)) into gradxyz1/2 (their clouds'
+// layouts); *scale_next = *grad_loss either way.  scale_used nullptr: always
+// recompute.
+extern "C" int pcm_chamfer_loss_grad_rescale(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1,
+                                             int layout2, float w1, float w2, const float *grad_loss,
+                                             const float *scale_used, float *scale_next, const int32_t *idx1,
+                                             const int32_t *idx2, float *gradxyz1, float *gradxyz2, void *stream) {
+    if (b <= 0 || n <= 0 || m <= 0 || (unsigned)layout1 > 1u || (unsigned)layout2 > 1u) return PCM_ERR_INVALID_ARG;
+    if (n > kBwdSlotsMax || m > kBwdSlotsMax) return PCM_ERR_UNSUPPORTED;
+    if (!xyz1 || !xyz2 || !grad_loss || !idx1 || !idx2 || !gradxyz1 || !gradxyz2) return PCM_ERR_INVALID_ARG;
+    if (scale_next && (scale_next == grad_loss || scale_next == scale_used)) return PCM_ERR_INVALID_ARG;
+    const int nblk1 = (n + kBwdSlotsT - 1) / kBwdSlotsT, nblk2 = (m + kBwdSlotsT - 1) / kBwdSlotsT;
+    const long long blocks = (long long)b * (nblk1 + nblk2);
+    if (blocks > 0x7fffffffLL) return PCM_ERR_UNSUPPORTED;
+    PcmRescale RS;
+    RS.gl = grad_loss;
+    RS.used = scale_used;
+    RS.next = scale_next;
+    RS.inv1 = w1;
+    RS.inv2 = w2;
+    hipLaunchKernelGGL(chamfer_bwd_slots_kernel, dim3((unsigned)blocks), dim3(kBwdSlotsT), 0, (hipStream_t)stream,
+                       xyz1, xyz2, b, n, m, nullptr, nullptr, idx1, idx2, gradxyz1, gradxyz2, nblk1, nblk2, layout1,
+                       layout2, PcmGdStr(), RS);
     return pcm_launch_status();
 }
 
@@ -2197,37 +2295,53 @@ const int kPcmNumFilt16Variants = sizeof(kPcmFilt16Variants) / sizeof(kPcmFilt16
 namespace {
 typedef void (*grad_kernel_t)(const float *, const float *, int, int, int, float, float, float *, float *,
                               int32_t *, int32_t *, float *, float *, float *, int, int, GradWs, unsigned,
-                              unsigned);
+                              unsigned, const float *);
 struct GradVariant {
+    int id;  // the variant number tools and tests name
     grad_kernel_t k;
     int waves, qpt;
 };
+// round 5: variant 15 (4-byte argmin granules, four per 16-byte write-through
+// store, the range's own argmins from the forward): the same time as 11
+// (13.56 vs 13.56 us same-box, profiles/r05/) with 3.03 MB of HBM-side traffic
+// per launch against 3.65 MB
+constexpr int kDefaultGradVariant = 15;
+#define PCM_GRAD_DEFAULT(L1, L2) chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true, L1, L2>
+// The product library holds the default only; the measured alternatives are
+// compiled into the tuning build (make tune: -DPCM_TUNE, libpcm_hip_tune.so),
+// which tools/ and the variant tests load.
 const GradVariant kGradVariants[] = {
-    {chamfer_loss_grad_kernel<8, 2, 16, 1024>, 8, 2},  // 0
-    {chamfer_loss_grad_kernel<8, 4, 16, 1024>, 8, 4},  // 1
-    {chamfer_loss_grad_kernel<4, 2, 16, 1024>, 4, 2},  // 2
-    {chamfer_loss_grad_kernel<16, 4, 16, 1024>, 16, 4},  // 3
-    {chamfer_loss_grad_kernel<8, 4, 32, 1024>, 8, 4},  // 4
-    {chamfer_loss_grad_kernel<16, 4, 32, 1024>, 16, 4},  // 5
-    {chamfer_loss_grad_kernel<8, 4, 16, 1024, true>, 8, 4},  // 6: screen on the matrix cores
-    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true>, 8, 4},  // 7: granule hand-off
-    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, true>, 8, 4},  // 8: 7 + the clouds copied during the scan
-    {chamfer_loss_grad_kernel<8, 4, 8, 1024, false, true>, 8, 4},   // 9: 7 with 8-candidate chunks
-    {chamfer_loss_grad_kernel<8, 4, 32, 1024, false, true>, 8, 4},  // 10: 7 with 32-candidate chunks
+#ifdef PCM_TUNE
+    {0, chamfer_loss_grad_kernel<8, 2, 16, 1024>, 8, 2},
+    {1, chamfer_loss_grad_kernel<8, 4, 16, 1024>, 8, 4},
+    {2, chamfer_loss_grad_kernel<4, 2, 16, 1024>, 4, 2},
+    {3, chamfer_loss_grad_kernel<16, 4, 16, 1024>, 16, 4},
+    {4, chamfer_loss_grad_kernel<8, 4, 32, 1024>, 8, 4},
+    {5, chamfer_loss_grad_kernel<16, 4, 32, 1024>, 16, 4},
+    {6, chamfer_loss_grad_kernel<8, 4, 16, 1024, true>, 8, 4},  // screen on the matrix cores
+    {7, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true>, 8, 4},  // granule hand-off
+    {8, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, true>, 8, 4},  // 7 + the clouds copied during the scan
+    {9, chamfer_loss_grad_kernel<8, 4, 8, 1024, false, true>, 8, 4},   // 7 with 8-candidate chunks
+    {10, chamfer_loss_grad_kernel<8, 4, 32, 1024, false, true>, 8, 4},  // 7 with 32-candidate chunks
     // 11: 7 whose gradient phase copies nothing in: the other cloud is the
     // forward's resident target tile, the range's points its queries
-    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true>, 8, 4},
+    {11, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true>, 8, 4},
     // 12: 11 with the target tile staged and scanned in two halves
-    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, true>, 8, 4},
+    {12, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, true>, 8, 4},
     // 13: LDS grid per workgroup (chamfer_lgrid.h): each group of 64 spatially
     // sorted queries screens only the target cells around it
-    {chamfer_loss_grad_lgrid_kernel, 8, 4},
+    {13, chamfer_loss_grad_lgrid_kernel, 8, 4},
     // 14: 11 with 4-byte argmin granules and the range's own argmins taken
     // from the forward (half the hand-off bytes, no own-range granule reads)
-    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true>, 8, 4},
+    {14, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true>, 8, 4},
+#endif
     // 15: 14 with four granules per 16-byte write-through store (a quarter of the fabric writes)
-    {chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true>, 8, 4},
+    {kDefaultGradVariant, PCM_GRAD_DEFAULT(0, 0), 8, 4},
 };
+// the default variant with cloud 1 / cloud 2 in channel planes (index 2 lay1 + lay2)
+const grad_kernel_t kGradDefaultLay[4] = {PCM_GRAD_DEFAULT(0, 0), PCM_GRAD_DEFAULT(0, 1), PCM_GRAD_DEFAULT(1, 0),
+                                          PCM_GRAD_DEFAULT(1, 1)};
+#undef PCM_GRAD_DEFAULT
 // (round 5, rejected: 15 with two queries per lane -- 128-query workgroups,
 // two per CU, four waves per SIMD -- 15.45 us against 13.39 us,
 // profiles/r05/ab_qpt2_r05t.txt)
@@ -2244,11 +2358,12 @@ constexpr int kNumGradVariants = sizeof(kGradVariants) / sizeof(kGradVariants[0]
 // forward with the gradient phase reading the forward's own LDS instead of
 // copying both clouds in, 0.07-0.12 us faster than 7 in each of 4 same-box
 // runs (profiles/r04/variant_7_11_r04ze_ab.txt)
-// round 5: variant 15 (4-byte argmin granules, four per 16-byte write-through
-// store, the range's own argmins from the forward): the same time as 11
-// (13.56 vs 13.56 us same-box, profiles/r05/) with 3.03 MB of HBM-side traffic
-// per launch against 3.65 MB
-constexpr int kDefaultGradVariant = 15;
+
+const GradVariant *find_grad_variant(int id) {
+    for (int i = 0; i < kNumGradVariants; ++i)
+        if (kGradVariants[i].id == id) return &kGradVariants[i];
+    return nullptr;
+}
 
 long long grad_blocks(const GradVariant &v, int b, int n, int m, int &nblk1, int &nblk2) {
     const int QW = 64 * v.qpt;
@@ -2257,6 +2372,8 @@ long long grad_blocks(const GradVariant &v, int b, int n, int m, int &nblk1, int
     return (long long)b * (nblk1 + nblk2);
 }
 
+// the workspace serves every variant this build holds (the product build: the
+// default alone)
 long long grad_blocks_max(int b, int n, int m) {
     long long most = 0;
     for (int i = 0; i < kNumGradVariants; ++i) {
@@ -2267,35 +2384,33 @@ long long grad_blocks_max(int b, int n, int m) {
     return most;
 }
 
-// variant 8 holds ~108 KB of LDS (one workgroup per CU): the default while
-// the grid is one residency wave of the device, variant 7 (64 KB, two per CU)
-// beyond
-// variant 8 (DMA issued before the scan) measured 0.4 us slower than 7 at the
-// benchmark size (r03h: 15.4 vs 15.0 us; the early copies slow the scan more
-// than they shorten the wait), so the default stays 7 at every size
 int default_grad_variant(int, int, int) { return kDefaultGradVariant; }
 
 int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, int n, int m, float w1, float w2,
                      float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out, float *grad1,
                      float *grad2, void *workspace, size_t workspace_bytes, void *stream,
-                     unsigned max_spins = kGradWaitSpins, unsigned poll_spins = pcm_loss::kPollMaxSpins) {
+                     unsigned max_spins = kGradWaitSpins, unsigned poll_spins = pcm_loss::kPollMaxSpins,
+                     int lay1 = 0, int lay2 = 0, const float *gscale = nullptr) {
     if (b <= 0 || n <= 0 || m <= 0) return PCM_ERR_INVALID_ARG;
     if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
-    if (variant < 0 || variant >= kNumGradVariants) return PCM_ERR_INVALID_ARG;
+    if ((unsigned)lay1 > 1u || (unsigned)lay2 > 1u) return PCM_ERR_INVALID_ARG;
+    const GradVariant *v = find_grad_variant(variant);
+    if (!v) return variant >= 0 && variant <= 15 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // 0-14: tuning build
+    if ((lay1 | lay2) && variant != kDefaultGradVariant) return PCM_ERR_UNSUPPORTED;
     if (!xyz1 || !xyz2 || !dist1 || !dist2 || !idx1 || !idx2 || !mean_out || !grad1 || !grad2 || !workspace)
         return PCM_ERR_INVALID_ARG;
-    const GradVariant &v = kGradVariants[variant];
     int nblk1, nblk2;
-    const long long blocks = grad_blocks(v, b, n, m, nblk1, nblk2);
+    const long long blocks = grad_blocks(*v, b, n, m, nblk1, nblk2);
     if (blocks > 0x7ffffffeLL) return PCM_ERR_UNSUPPORTED;
     const size_t off = pcm_chamfer_loss_ws_offset(b, n, m);
     if (workspace_bytes < off + grad_ws_bytes(b, grad_blocks_max(b, n, m), (long long)b * (n + m)))
         return PCM_ERR_WORKSPACE;
     const GradWs ws = grad_ws((char *)workspace + off, b, blocks);
+    const grad_kernel_t k = variant == kDefaultGradVariant ? kGradDefaultLay[2 * lay1 + lay2] : v->k;
     // + the polling workgroup (the grid's last)
-    hipLaunchKernelGGL(v.k, dim3((unsigned)blocks + 1), dim3(64 * v.waves), 0, (hipStream_t)stream, xyz1, xyz2, b,
+    hipLaunchKernelGGL(k, dim3((unsigned)blocks + 1), dim3(64 * v->waves), 0, (hipStream_t)stream, xyz1, xyz2, b,
                        n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out, grad1, grad2, nblk1, nblk2, ws, max_spins,
-                       poll_spins);
+                       poll_spins, gscale);
     return pcm_launch_status();
 }
 }  // namespace
@@ -2315,6 +2430,33 @@ extern "C" int pcm_chamfer_loss_grad(const float *xyz1, const float *xyz2, int b
                             gradxyz1, gradxyz2, workspace, workspace_bytes, stream);
 }
 
+extern "C" int pcm_chamfer_loss_grad_layout(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1,
+                                            int layout2, float w1, float w2, const float *grad_scale, float *dist1,
+                                            float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out,
+                                            float *gradxyz1, float *gradxyz2, void *workspace,
+                                            size_t workspace_bytes, void *stream) {
+    return launch_loss_grad(default_grad_variant(b, n, m), xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2,
+                            mean_out, gradxyz1, gradxyz2, workspace, workspace_bytes, stream, kGradWaitSpins,
+                            pcm_loss::kPollMaxSpins, layout1, layout2, grad_scale);
+}
+
+// `steps` back-to-back launches of the default step from one host call, its
+// arguments bound once: K steps of a native training loop on fixed buffers
+// (what bench.py's N=1 region times; a ctypes call per step from Python is
+// host-bound, ~17 us for 17 arguments against a ~14 us kernel)
+extern "C" int pcm_chamfer_loss_grad_steps(int steps, const float *xyz1, const float *xyz2, int b, int n, int m,
+                                           float w1, float w2, float *dist1, float *dist2, int32_t *idx1,
+                                           int32_t *idx2, float *mean_out, float *gradxyz1, float *gradxyz2,
+                                           void *workspace, size_t workspace_bytes, void *stream) {
+    if (steps < 0) return PCM_ERR_INVALID_ARG;
+    for (int r = 0; r < steps; ++r) {
+        const int st = launch_loss_grad(default_grad_variant(b, n, m), xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1,
+                                        idx2, mean_out, gradxyz1, gradxyz2, workspace, workspace_bytes, stream);
+        if (st != PCM_OK) return st;
+    }
+    return PCM_OK;
+}
+
 extern "C" int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, int n, int m,
                                           float w1, float w2, float *dist1, float *dist2, int32_t *idx1,
                                           int32_t *idx2, float *mean_out, float *gradxyz1, float *gradxyz2,
@@ -2323,21 +2465,8 @@ extern "C" int pcm_tune_chamfer_loss_grad(int variant, const float *xyz1, const 
                             gradxyz2, workspace, workspace_bytes, stream);
 }
 
+// variants this build holds (the product: the default alone)
 extern "C" int pcm_tune_num_chamfer_loss_grad_variants(void) { return kNumGradVariants; }
-
-// `reps` back-to-back launches of the default step from one host call (a C
-// caller's training loop, without Python's per-call cost): tools/probe_replay.py
-extern "C" int pcm_tune_chamfer_loss_grad_repeat(int reps, const float *xyz1, const float *xyz2, int b, int n, int m,
-                                                 float w1, float w2, float *dist1, float *dist2, int32_t *idx1,
-                                                 int32_t *idx2, float *mean_out, float *gradxyz1, float *gradxyz2,
-                                                 void *workspace, size_t workspace_bytes, void *stream) {
-    for (int r = 0; r < reps; ++r) {
-        const int st = launch_loss_grad(default_grad_variant(b, n, m), xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1,
-                                        idx2, mean_out, gradxyz1, gradxyz2, workspace, workspace_bytes, stream);
-        if (st != PCM_OK) return st;
-    }
-    return PCM_OK;
-}
 
 namespace {
 // variant 0: the filtered geometry of larger clouds (W 8, QPT 4, C 32, 2048-point tiles); 1: that of clouds of

@@ -67,8 +67,7 @@ constexpr int kLgCap = kGradCap;     // points per cloud (1024)
 constexpr int kLgCells = 512;        // G^3 cells at G = 8
 constexpr int kLgC = 8;              // screen chunk (candidates)
 constexpr int kLgGroupCap = 512;     // window entries a group's screen buffer holds (one piece)
-constexpr unsigned kLgTagBits = 21;  // granule: tag << 11 | idx (idx < 2048)
-constexpr unsigned kLgTagMask = (1u << kLgTagBits) - 1u;
+constexpr unsigned kLgTagMask = kG4TagMask;  // granule: tag << 11 | idx (idx < 2048), chamfer_filt.hip
 constexpr float kLgU16 = 9.5367431640625e-07f;  // 16 u = 2^-20 (chamfer_filt.hip's bound)
 constexpr int kLgArena = 4 * kLgGroupCap * 16;   // 32 KB: the groups' screen buffers, then gradient scratch
 static_assert(kLgArena >= 4 * kLgQW + 2 * kLgQW * kGradSlotsMax + 4 * kLgCap, "gradient scratch fits the arena");
@@ -112,7 +111,13 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
     float *__restrict__ mean_out, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
-    GradWs ws, unsigned max_spins, unsigned poll_spins) {
+    GradWs ws, unsigned max_spins, unsigned poll_spins, const float *__restrict__ gscale) {
+    float gsc = 1.f;
+    if (gscale) {  // as chamfer_loss_grad_kernel: graddist = fl(upstream * w)
+        gsc = *gscale;
+        w1 = __fmul_rn(gsc, w1);
+        w2 = __fmul_rn(gsc, w2);
+    }
     __shared__ pcm_f4 sTs[kLgCap];            // targets sorted by cell: (x, y, z, index bits)
     __shared__ uint16_t sInv[kLgCap];         // target index -> sorted position
     __shared__ int sTSt[kLgCells + 4];        // target cell counts, then starts (row-major cells)
@@ -145,6 +150,7 @@ __global__ __launch_bounds__(kLgNT) __attribute__((amdgpu_waves_per_eu(4))) void
     if ((int)blockIdx.x == nprod) {  // the grid's last workgroup: the loss means
         PCM_STAMP2(5);
         poll_grad_loss_wg(b, n, m, nblk1 + nblk2, nblk1, ws, mean_out, poll_spins, grad_shape_word(n, m, 2u));
+        if (gscale && threadIdx.x == 0) mean_out[3] = gsc;
         PCM_STAMP2(6);
         return;
     }

@@ -16,9 +16,12 @@ layout, so autograd's transpose backward needs no copy either.
 
 Extension: ``chamfer_3DLossFunction`` / ``chamfer_3DLoss`` return the training
 loss mean(dist1) + mean(dist2) of loss/loss.py:36 directly and compute its
-gradient in the SAME launch as the forward (pcm_chamfer_loss_grad, float32
-clouds of <= 1024 points); backward only scales the saved gradient by the
-upstream scalar.  Other clouds take the forward + torch means + backward path.
+gradient in the SAME launch as the forward (pcm_chamfer_loss_grad_layout,
+float32 clouds of <= 1024 points, rows or channel planes read in place), for
+the upstream gradient (train.py:169's lambda_cd) the previous step saw; the
+backward confirms it or recomputes the exact gradient in place
+(pcm_chamfer_loss_grad_rescale).  Other clouds take the forward + torch means
++ backward path.
 
 Differences, all on the "stricter" side:
   * outputs are allocated directly on the device (the reference built them on
@@ -137,7 +140,23 @@ def _empty_like_layout(t, lay):
 
 
 class chamfer_3DLossFunction(Function):
-    """mean(dist1) + mean(dist2) and its gradient from one kernel launch."""
+    """mean(dist1) + mean(dist2) and its gradient from one kernel launch.
+
+    train.py:163-176 hands the loss fake.transpose(2, 1) -- a [B, N, 3] view
+    of the generator's [B, 3, N] output -- and scales it by lambda_cd before
+    .backward().  Both are taken as they come:
+      * a channel-plane view is read in place and its gradient written in the
+        same layout (pcm_chamfer_loss_grad_layout), so neither the forward nor
+        autograd's transpose backward copies anything;
+      * the gradient is computed, in the same launch as the forward, for the
+        upstream gradient this (device, stream) saw last (pcm_hip.grad_scale_hint,
+        1.0 at first), as the reference's backward computes it:
+        graddist = fl(upstream * fl(1/(B N))) (torch's mean backward), then
+        g = 2 graddist (chamfer3D.cu:160-171).  backward() launches
+        pcm_chamfer_loss_grad_rescale with the real upstream gradient: nothing
+        to do when it has the expected bits (every step of a loop with a
+        constant lambda but the first), else the exact gradient recomputed
+        in place.  No torch multiply, no copy: two launches of ours per step."""
 
     @staticmethod
     def forward(ctx, xyz1, xyz2):
@@ -146,29 +165,53 @@ class chamfer_3DLossFunction(Function):
         _, m, dim = xyz2.size()
         assert dim == 3, "Wrong last dimension for the chamfer distance 's input! Check with .size()"
         assert xyz2.size(0) == batchsize, "batch sizes of the two clouds differ"
-        xyz1 = xyz1.contiguous()
-        xyz2 = xyz2.contiguous()
         if not pcm_hip.loss_grad_supported(xyz1, xyz2):
             raise ValueError("chamfer_3DLossFunction takes float32 clouds of 1..%d points; use "
                              "chamfer_3DDist + torch.mean" % pcm_hip.LOSS_GRAD_MAX_POINTS)
+        lay = _fused_layouts(xyz1, xyz2)
+        if lay is None:
+            xyz1, xyz2, lay = xyz1.contiguous(), xyz2.contiguous(), (0, 0)
         device = xyz1.device
         dist1 = torch.empty(batchsize, n, device=device)
         dist2 = torch.empty(batchsize, m, device=device)
         idx1 = torch.empty(batchsize, n, dtype=torch.int32, device=device)
         idx2 = torch.empty(batchsize, m, dtype=torch.int32, device=device)
-        means = torch.empty(3, device=device)
-        gradxyz1 = torch.empty_like(xyz1)
-        gradxyz2 = torch.empty_like(xyz2)
-        # gradient of torch.mean: 1/numel per element (the weight torch's mean backward feeds)
-        pcm_hip.chamfer_loss_grad(xyz1, xyz2, 1.0 / (batchsize * n), 1.0 / (batchsize * m), dist1, dist2,
-                                  idx1, idx2, means, gradxyz1, gradxyz2)
-        ctx.save_for_backward(gradxyz1, gradxyz2)
+        means = torch.empty(4, device=device)  # mean1, mean2, loss, the gradient scale used
+        gradxyz1 = _empty_like_layout(xyz1, lay[0])
+        gradxyz2 = _empty_like_layout(xyz2, lay[1])
+        # torch's mean backward multiplies the upstream gradient by fl32(1/numel)
+        w1, w2 = pcm_hip.mean_weight(batchsize * n), pcm_hip.mean_weight(batchsize * m)
+        pcm_hip.chamfer_loss_grad(xyz1, xyz2, w1, w2, dist1, dist2, idx1, idx2, means, gradxyz1, gradxyz2,
+                                  layouts=lay, grad_scale=pcm_hip.grad_scale_hint(device))
+        ctx.save_for_backward(xyz1, xyz2, idx1, idx2, means, gradxyz1, gradxyz2)
+        ctx.lay, ctx.w, ctx.done = lay, (w1, w2), False
         return means[2]
 
     @staticmethod
     def backward(ctx, grad_loss):
-        gradxyz1, gradxyz2 = ctx.saved_tensors
-        return gradxyz1 * grad_loss, gradxyz2 * grad_loss
+        xyz1, xyz2, idx1, idx2, means, gradxyz1, gradxyz2 = ctx.saved_tensors
+        dev = xyz1.device
+        gl = grad_loss.detach().to(device=dev, dtype=torch.float32).reshape(1)
+        used = means[3:4]
+        if ctx.done:  # a second backward through this graph: fresh buffers, always recomputed
+            gradxyz1 = _empty_like_layout(xyz1, ctx.lay[0])
+            gradxyz2 = _empty_like_layout(xyz2, ctx.lay[1])
+            used = None
+        ctx.done = True
+        pcm_hip.chamfer_loss_grad_rescale(xyz1, xyz2, ctx.lay, ctx.w[0], ctx.w[1], gl, used,
+                                          pcm_hip.grad_scale_hint(dev), idx1, idx2, gradxyz1, gradxyz2)
+        return gradxyz1, gradxyz2
+
+
+def _fused_layouts(xyz1, xyz2):
+    """(layout1, layout2) of float32 device clouds the one-launch step reads
+    in place (rows 0 or channel planes 1, pcm_hip.cloud_layout), else None."""
+    if not xyz1.is_cuda:
+        return None
+    l1, l2 = pcm_hip.cloud_layout(xyz1), pcm_hip.cloud_layout(xyz2)
+    if l1 is None or l2 is None:
+        return None
+    return (l1, l2)
 
 
 def _chamfer_loss_value(xyz1, xyz2):

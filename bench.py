@@ -219,10 +219,10 @@ class ChamferStep:
         ci, cf, cs = ctypes.c_int, ctypes.c_float, ctypes.c_size_t
         if self.fused:
             # K steps = K calls of pcm_chamfer_loss_grad from one host call
-            # (csrc/chamfer_filt.hip pcm_tune_chamfer_loss_grad_repeat: a C
-            # loop over the public entry; ctypes costs ~17 us per call of 17
-            # arguments from Python, more than the kernel, r05e)
-            f = L.pcm_tune_chamfer_loss_grad_repeat
+            # (include/pcm.h pcm_chamfer_loss_grad_steps: a C loop over the
+            # public entry; ctypes costs ~17 us per call of 17 arguments from
+            # Python, more than the kernel, r05e)
+            f = L.pcm_chamfer_loss_grad_steps
             f.restype = ctypes.c_int
             args = (P(self.xyz1), P(self.xyz2), ci(B), ci(N), ci(M), cf(self.w1), cf(self.w2), P(self.d1), P(self.d2),
                     P(self.i1), P(self.i2), P(self.loss[0]), P(self.gx1), P(self.gx2), P(self.ws),
@@ -376,6 +376,113 @@ def reference_call_leg(dev, reps=50):
                         ".backward() (loss/loss.py:34-36, train.py:163,174-175)",
             "eager_us_per_step": eager_us, "graph_us_per_step": graph_us,
             "graph_pairs_per_s": pairs / (graph_us * 1e-6)}
+
+
+LAMBDA_CD = 100  # train.py:43 --lambda_cd default
+
+
+def training_call_leg(dev, reps=50):
+    """The call train.py makes through THIS build's loss (loss/loss.py
+    counterpart): gen.zero_grad(), chamfer_loss =
+    Loss().get_chamfer_loss(fake.transpose(2, 1), points), total_loss =
+    chamfer_loss * lambda_cd (100), total_loss.backward() (train.py:163,169,
+    174-176; the EMD term has its own legs), at BASELINE config 2 on the
+    generator's [B, 3, N] output layout.  The one-launch step reads the
+    transposed view in place and computes the lambda-weighted gradient (the
+    scale learned from the previous step), the backward's rescale launch finds
+    nothing to do.  Timed eagerly and as a captured 20-step graph."""
+    sys.path.insert(0, os.path.join(PKG, "loss"))
+    import loss as loss_mod
+    g = torch.Generator(device="cpu").manual_seed(11)  # reference_call_leg's clouds
+    fake = torch.rand(B, 3, N, generator=g).to(dev).requires_grad_(True)
+    points = torch.rand(B, M, 3, generator=g).to(dev)
+    loss_fn = loss_mod.Loss()
+
+    def call():
+        fake.grad = None  # gen.zero_grad()
+        chamfer_loss = loss_fn.get_chamfer_loss(fake.transpose(2, 1), points)
+        total_loss = chamfer_loss * LAMBDA_CD
+        total_loss.backward()
+        return total_loss
+
+    out = _time_call(call, dev, reps)
+    out["before"] = _time_call(lambda: _round5_training_call(fake, points), dev, reps)
+    out["before"]["form"] = ("round 5's chamfer_3DLossFunction: .contiguous() copy of the transposed view, the "
+                             "one-launch step at weight 1/(B N), the saved gradients multiplied by the upstream "
+                             "gradient in backward (two torch multiplies)")
+    out.update(sequence="gen.zero_grad(); Loss().get_chamfer_loss(fake.transpose(2,1), points) * lambda_cd(100); "
+                        ".backward() (train.py:163,169,174-176, this build's loss/loss.py)",
+               graph_pairs_per_s=2 * B * N * M / (out["graph_us_per_step"] * 1e-6),
+               kernels_per_step="profiles/r06/training_call_kernels.txt (rocprofv3 kernel trace of "
+                                "tools/training_call_trace.py)")
+    return out
+
+
+class _Round5LossFunction(torch.autograd.Function):
+    """Round 5's form of the fused loss (for the training_call leg's 'before'
+    figure only): rows copied, gradient at weight 1/(B N), scaled afterwards."""
+
+    @staticmethod
+    def forward(ctx, xyz1, xyz2):
+        xyz1, xyz2 = xyz1.contiguous(), xyz2.contiguous()
+        b, n, _ = xyz1.shape
+        m = xyz2.shape[1]
+        dev = xyz1.device
+        d1, d2 = torch.empty(b, n, device=dev), torch.empty(b, m, device=dev)
+        i1 = torch.empty(b, n, dtype=torch.int32, device=dev)
+        i2 = torch.empty(b, m, dtype=torch.int32, device=dev)
+        means = torch.empty(3, device=dev)
+        g1, g2 = torch.empty_like(xyz1), torch.empty_like(xyz2)
+        pcm_hip.chamfer_loss_grad(xyz1, xyz2, 1.0 / (b * n), 1.0 / (b * m), d1, d2, i1, i2, means, g1, g2)
+        ctx.save_for_backward(g1, g2)
+        return means[2]
+
+    @staticmethod
+    def backward(ctx, grad_loss):
+        g1, g2 = ctx.saved_tensors
+        return g1 * grad_loss, g2 * grad_loss
+
+
+def _round5_training_call(fake, points):
+    fake.grad = None
+    total_loss = _Round5LossFunction.apply(fake.transpose(2, 1), points) * LAMBDA_CD
+    total_loss.backward()
+    return total_loss
+
+
+def _time_call(call, dev, reps):
+    """A python-level call sequence timed eagerly (host launch cost included)
+    and as a captured GRAPH_STEPS-step graph (device time per step)."""
+    s = torch.cuda.current_stream(dev)
+    side = torch.cuda.Stream(dev)
+    side.wait_stream(s)
+    with torch.cuda.stream(side):
+        for _ in range(3):
+            call()
+    s.wait_stream(side)
+    for _ in range(3):
+        call()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        call()
+    torch.cuda.synchronize(dev)
+    eager_us = (time.perf_counter() - t0) * 1e6 / reps
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        for _ in range(GRAPH_STEPS):
+            call()
+    graph.replay()
+    graph.replay()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    k = max(1, reps // GRAPH_STEPS)
+    e0.record(s)
+    for _ in range(k):
+        graph.replay()
+    e1.record(s)
+    e1.synchronize()
+    graph_us = e0.elapsed_time(e1) * 1000.0 / (k * GRAPH_STEPS)
+    return {"eager_us_per_step": eager_us, "graph_us_per_step": graph_us}
 
 
 EMD_TRAIN_CLOUDS = os.path.join(REPO, "bench_data", "emd_training_call.npz")
@@ -703,6 +810,7 @@ def side_legs(args, dev, rank, world):
         side["icp"] = icp_leg(dev, with_cpu=rank == 0 and world == 1 and not args.no_cpu)
     if not args.no_ref_call:
         side["reference_call"] = reference_call_leg(dev)
+        side["training_call"] = training_call_leg(dev)
     if not args.no_dense:
         side["dense_fp16"] = dense_f16_leg(dev)
     if not args.no_emd:
@@ -957,6 +1065,8 @@ def main(argv=None):
     out.update(side)
     if "reference_call" in out:
         out["reference_call"]["graph_vs_fused_step"] = out["reference_call"]["graph_us_per_step"] / (ms * 1000.0)
+    if "training_call" in out:
+        out["training_call"]["graph_vs_fused_step"] = out["training_call"]["graph_us_per_step"] / (ms * 1000.0)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline()
     if rank == 0:

@@ -112,6 +112,51 @@ int pcm_chamfer_loss_grad(const float *xyz1, const float *xyz2, int b, int n, in
                           void *stream);
 
 /*
+ * The fused loss + gradient as train.py:163-176 drives it (extension):
+ *   chamfer_loss = mean(dist1) + mean(dist2) on fake.transpose(2, 1), then
+ *   total_loss = chamfer_loss * lambda_cd + ..., total_loss.backward().
+ * pcm_chamfer_loss_grad_layout is pcm_chamfer_loss_grad with
+ *   - either cloud in channel planes (layout 1, as pcm_chamfer_forward_layout),
+ *     read in place, its gradient written in the same layout;
+ *   - grad_scale (nullable, device float): the upstream gradient the loss is
+ *     expected to receive.  The gradients are those of
+ *     grad_scale * (w1 sum(dist1) + w2 sum(dist2)) computed as the reference's
+ *     backward does it: graddist = fl(grad_scale * w) (torch's mean backward,
+ *     w = fl(1/(b n)) as torch forms it), g = 2 graddist
+ *     (chamfer3D.cu:160-171).  mean_out then needs 4 floats: mean_out[3]
+ *     receives the scale used.  NULL: scale 1 (pcm_chamfer_loss_grad).
+ * pcm_chamfer_loss_grad_rescale is its backward once the real upstream
+ * gradient *grad_loss is known (device floats; none of them may alias):
+ *   - *grad_loss == *scale_used bit for bit (pass mean_out + 3): the step's
+ *     gradients are already exact and the launch does nothing;
+ *   - otherwise gradxyz1/2 are recomputed in place from idx1/idx2 with
+ *     graddist = fl(*grad_loss * w) -- bit-identical to pcm_chamfer_backward
+ *     fed that constant -- and scale_used NULL always recomputes;
+ *   - *scale_next = *grad_loss (nullable): the expectation for the next step.
+ * A training loop with a constant loss weight therefore recomputes once, on
+ * its first step, and from then on runs the forward, the loss and the exact
+ * weighted gradient in one launch plus one empty launch.  Needs 0 < n, m <=
+ * 1024 and the workspace of pcm_chamfer_loss_grad.
+ */
+int pcm_chamfer_loss_grad_layout(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1, int layout2,
+                                 float w1, float w2, const float *grad_scale, float *dist1, float *dist2,
+                                 int32_t *idx1, int32_t *idx2, float *mean_out, float *gradxyz1, float *gradxyz2,
+                                 void *workspace, size_t workspace_bytes, void *stream);
+int pcm_chamfer_loss_grad_rescale(const float *xyz1, const float *xyz2, int b, int n, int m, int layout1,
+                                  int layout2, float w1, float w2, const float *grad_loss, const float *scale_used,
+                                  float *scale_next, const int32_t *idx1, const int32_t *idx2, float *gradxyz1,
+                                  float *gradxyz2, void *stream);
+/*
+ * `steps` back-to-back pcm_chamfer_loss_grad launches from one host call with
+ * the arguments bound once: K steps of a native training loop on fixed
+ * buffers (bench.py's N=1 region).  steps >= 0.
+ */
+int pcm_chamfer_loss_grad_steps(int steps, const float *xyz1, const float *xyz2, int b, int n, int m, float w1,
+                                float w2, float *dist1, float *dist2, int32_t *idx1, int32_t *idx2,
+                                float *mean_out, float *gradxyz1, float *gradxyz2, void *workspace,
+                                size_t workspace_bytes, void *stream);
+
+/*
  * Device-side failure of the fused-loss kernels on `workspace`: PCM_OK or
  * PCM_ERR_LAUNCH.  A gradient-phase wait of pcm_chamfer_loss_grad that times
  * out (workgroups that are not resident) is NOT a failure: the waiting
@@ -190,6 +235,11 @@ int pcm_chamfer_backward_f16(const uint16_t *xyz1, const uint16_t *xyz2, int b, 
  * which is what large clouds (BASELINE config 5, N=M=16384) need; smaller
  * problems take the dense kernels and ignore the workspace.  The workspace
  * needs no initialisation and holds no state between calls.
+ * pcm_chamfer_forward_ws_bytes returns 0 for a problem that takes the dense
+ * kernels, so the size does not grow with the shape: a buffer shared by
+ * several shapes must be sized by querying each of them (the largest answer
+ * serves all); a buffer sized for a dense-path shape is too small for a grid
+ * one (PCM_ERR_WORKSPACE).
  */
 size_t pcm_chamfer_forward_ws_bytes(int b, int n, int m);
 int pcm_chamfer_forward_ws(const float *xyz1, const float *xyz2, int b, int n, int m,

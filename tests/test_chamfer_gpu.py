@@ -802,20 +802,126 @@ def test_wrapper_reports_and_resets_sticky_error(cuda, oracle):
     pcm_hip.chamfer_workspace_status(ws, b, n, m)
 
 
-def test_loss_function_scales_upstream_gradient(cuda):
+def _reference_training_call(cuda, oracle, planes, gt, lam):
+    """train.py:163,169,176 through the REFERENCE's own sequence
+    (loss/loss.py:34-36: chamfer_3DDist, torch.mean(dist1) + torch.mean(dist2))
+    on a channel-plane generator output, scaled by lambda_cd = lam: the
+    graddists torch's mean backward hands chamfer_3DFunction.backward are
+    captured, and the oracle's restatement of the reference backward
+    (chamfer3D.cu:155-195) fed exactly those gives the expected gradients."""
     import dist_chamfer_3D
-    a, c = _clouds(122, 4, 512, 512)
+    fake = planes.to(cuda).requires_grad_(True)
+    pts = gt.to(cuda).requires_grad_(True)
+    d1, d2, _, _ = dist_chamfer_3D.chamfer_3DDist()(fake.transpose(2, 1), pts)
+    gd = {}
+    d1.register_hook(lambda g: gd.__setitem__(1, g.detach().clone()))
+    d2.register_hook(lambda g: gd.__setitem__(2, g.detach().clone()))
+    cd = torch.mean(d1) + torch.mean(d2)
+    (cd * lam).backward()
+    torch.cuda.synchronize()
+    rows = planes.transpose(1, 2).contiguous().numpy()
+    r1, r2, j1, j2 = oracle.chamfer_forward(rows, gt.numpy())
+    g1, g2 = gd[1].cpu().numpy(), gd[2].cpu().numpy()
+    rg1, rg2 = oracle.chamfer_backward(rows, gt.numpy(), np.ascontiguousarray(g1), np.ascontiguousarray(g2), j1, j2)
+    return cd.item(), g1, g2, rg1, rg2, (r1, r2)
+
+
+@pytest.mark.parametrize("b", [32, 24])  # 1/(B N) is exact at 32, inexact at 24
+def test_training_call_matches_oracle(cuda, oracle, b):
+    # the call train.py makes, through the builder's Loss (loss/loss.py
+    # counterpart): Loss().get_chamfer_loss(fake.transpose(2, 1), gt), then
+    # (cd * lambda_cd).backward() with lambda_cd = 100 (train.py:43,169,176).
+    # The gradients must equal the oracle's reference backward fed the
+    # graddists torch's mean backward produces, bit for bit, on the first step
+    # (scale expected 1.0: recomputed in the backward) and on later steps (the
+    # scale learned: the one-launch step's own gradient stands), and after
+    # lambda changes (recomputed again).
+    import loss as loss_mod
+    import pcm_hip
+    n = m = 1024
+    g = torch.Generator().manual_seed(140 + b)
+    planes = torch.rand(b, 3, n, generator=g)  # the generator's [B, 3, N] output
+    gt = torch.rand(b, m, 3, generator=g)
+    refs = {lam: _reference_training_call(cuda, oracle, planes, gt, lam) for lam in (100.0, 1.0)}
+    # torch's mean backward: graddist = fl(lambda * fl(1/(B N))), the kernels' formula
+    for lam, (_, g1, g2, _, _, _) in refs.items():
+        w = np.float32(pcm_hip.mean_weight(b * n))
+        assert np.all(g1 == np.float32(np.float32(lam) * w)) and np.all(g2 == np.float32(np.float32(lam) * w))
+    hint = pcm_hip.grad_scale_hint(cuda)
+    hint.fill_(1.0)
+    pts = gt.to(cuda).requires_grad_(True)
+    for step, lam in enumerate((100.0, 100.0, 100.0, 1.0, 100.0)):
+        fake = planes.to(cuda).requires_grad_(True)
+        pts.grad = None
+        cd = loss_mod.Loss().get_chamfer_loss(fake.transpose(2, 1), pts)
+        (cd * lam).backward()
+        torch.cuda.synchronize()
+        ref_cd, _, _, rg1, rg2, (r1, r2) = refs[lam]
+        np.testing.assert_allclose(cd.item(), ref_cd, rtol=2e-6)
+        assert fake.grad.is_contiguous()  # written as channel planes: no transpose copy
+        got1 = fake.grad.transpose(1, 2).contiguous().cpu().numpy()
+        np.testing.assert_array_equal(got1.view(np.int32), rg1.view(np.int32), err_msg=f"step {step}")
+        np.testing.assert_array_equal(pts.grad.cpu().numpy().view(np.int32), rg2.view(np.int32),
+                                      err_msg=f"step {step}")
+        assert hint.item() == lam
+
+
+def test_training_call_double_backward_and_rows(cuda, oracle):
+    # retain_graph: a second backward through the same loss gets fresh,
+    # recomputed gradients (autograd may have kept the first ones as .grad);
+    # row clouds take the same one-launch path
+    import dist_chamfer_3D
+    import pcm_hip
+    b, n, m = 4, 700, 900
+    a, c = _clouds(141, b, n, m)
     x1 = a.to(cuda).requires_grad_(True)
     x2 = c.to(cuda).requires_grad_(True)
-    L = dist_chamfer_3D.chamfer_3DLossFunction.apply(x1, x2)
-    (3.0 * L).backward()
-    y1 = a.to(cuda).requires_grad_(True)
-    y2 = c.to(cuda).requires_grad_(True)
-    d1, d2, _, _ = dist_chamfer_3D.chamfer_3DDist()(y1, y2)
-    (3.0 * (torch.mean(d1) + torch.mean(d2))).backward()
+    pcm_hip.grad_scale_hint(cuda).fill_(2.0)
+    L = dist_chamfer_3D.chamfer_3DLoss()(x1, x2)
+    (L * 3.0).backward(retain_graph=True)
+    first1, first2 = x1.grad.clone(), x2.grad.clone()
+    (L * 3.0).backward()
     torch.cuda.synchronize()
-    np.testing.assert_allclose(x1.grad.cpu().numpy(), y1.grad.cpu().numpy(), rtol=1e-6, atol=1e-9)
-    np.testing.assert_allclose(x2.grad.cpu().numpy(), y2.grad.cpu().numpy(), rtol=1e-6, atol=1e-9)
+    r1, r2, j1, j2 = oracle.chamfer_forward(a.numpy(), c.numpy())
+    w1, w2 = np.float32(pcm_hip.mean_weight(b * n)), np.float32(pcm_hip.mean_weight(b * m))
+    rg1, rg2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), np.float32(3.0) * w1, np.float32),
+                                       np.full((b, m), np.float32(3.0) * w2, np.float32), j1, j2)
+    np.testing.assert_array_equal(first1.cpu().numpy().view(np.int32), rg1.view(np.int32))
+    np.testing.assert_array_equal(first2.cpu().numpy().view(np.int32), rg2.view(np.int32))
+    # accumulated twice: first + second, torch's own add
+    np.testing.assert_array_equal(x1.grad.cpu().numpy(), (first1 + first1).cpu().numpy())
+    np.testing.assert_array_equal(x2.grad.cpu().numpy(), (first2 + first2).cpu().numpy())
+
+
+def test_training_call_graph_capture(cuda, oracle):
+    # the whole training call captured into one graph (as bench.py's
+    # training_call leg runs it) and replayed: the learned scale is read and
+    # written by the replay itself, the gradients stay exact
+    import loss as loss_mod
+    import pcm_hip
+    b, n, m = 8, 1024, 1024
+    g = torch.Generator().manual_seed(142)
+    planes = torch.rand(b, 3, n, generator=g)
+    gt = torch.rand(b, m, 3, generator=g)
+    _, _, _, rg1, _, _ = _reference_training_call(cuda, oracle, planes, gt, 100.0)
+    fake = planes.to(cuda).requires_grad_(True)
+    pts = gt.to(cuda)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            fake.grad = None
+            (loss_mod.Loss().get_chamfer_loss(fake.transpose(2, 1), pts) * 100).backward()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    fake.grad = None
+    with torch.cuda.graph(graph):
+        (loss_mod.Loss().get_chamfer_loss(fake.transpose(2, 1), pts) * 100).backward()
+    for _ in range(3):
+        graph.replay()
+    torch.cuda.synchronize()
+    got = fake.grad.transpose(1, 2).contiguous().cpu().numpy()
+    np.testing.assert_array_equal(got.view(np.int32), rg1.view(np.int32))
 
 
 @pytest.mark.parametrize("b,n,m,lays", [

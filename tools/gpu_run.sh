@@ -23,6 +23,7 @@
 #   abcl       tools/ab_chamfer.sh (the A/B across lib/libpcm_hip_{base,v*}.so builds, twice)
 #   emddiag    tools/emd_diag.py: config 3 per iteration, the training call by bidder count
 #   abr        tools/ab_ref_call.py (the unchanged caller's pieces: forward geometries, strided backward)
+#   tct        rocprofv3 kernel traces of tools/training_call_trace.py {after,before,reference}
 set -o pipefail
 TAG=$1
 shift
@@ -73,6 +74,11 @@ for S in "$@"; do
               PCM_HIP_LIB=$L timeout -k 10 300 python -u tools/ab_ref_call.py >> "$O/ab_ref_call_libs.txt" 2>&1 || exit 1
           done; done ;;
     abr) timeout -k 10 300 python -u tools/ab_ref_call.py > "$O/ab_ref_call.txt" 2>&1 ;;
+    tct) for f in after before reference; do
+             (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/tct_$f" -o run \
+                 --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/training_call_trace.py" $f 20 \
+                 > "$GRAFT_REPO_ROOT/$O/tct_$f.log" 2>&1) || exit 1
+         done ;;
     benchab) for i in 1 2; do for o in first last; do
                timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 --side-legs $o \
                    > "$O/bench_${o}_$i.json" 2> "$O/bench_${o}_$i.err" || exit 1; done; done ;;

@@ -9,18 +9,35 @@ extern "C" int pcm_version(void) { return 100; /* 0.1.0 */ }
 // microseconds while issuing nothing but s_sleep -- a stand-in for another
 // kernel sharing the CUs (an RCCL all-reduce beside the one-launch Chamfer
 // step at N > 1).  Every wave leaves once the real-time clock (100 MHz) has
-// advanced `usec`; nothing is stored.
+// advanced `usec`.  stamps (nullable, device, 3 words, caller-initialised to
+// {~0, 0, 0}): the earliest workgroup start, the latest workgroup end (both
+// s_memrealtime ticks) and the number of workgroups that started -- the
+// evidence that the occupier was resident while another kernel ran.
+// pcm_tune_clock_stamp writes s_memrealtime to *out from a one-thread kernel:
+// on the step's stream just before and after the step it brackets the step's
+// whole run (a stream runs its kernels one after the other).
 // ---------------------------------------------------------------------------
 namespace {
-__global__ void pcm_occupy_kernel(unsigned long long ticks) {
+__global__ void pcm_occupy_kernel(unsigned long long ticks, unsigned long long *stamps) {
     extern __shared__ int occupy_lds[];
     (void)occupy_lds;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+    if (stamps && threadIdx.x == 0) {
+        atomicMin(stamps, t0);
+        atomicAdd(stamps + 2, 1ull);
+    }
+    unsigned long long t = t0;
+    while ((t = __builtin_amdgcn_s_memrealtime()) - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+    if (stamps && threadIdx.x == 0) atomicMax(stamps + 1, t);
+}
+
+__global__ void pcm_clock_stamp_kernel(unsigned long long *out) {
+    if (threadIdx.x == 0) *out = __builtin_amdgcn_s_memrealtime();
 }
 }  // namespace
 
-extern "C" int pcm_tune_occupy(int blocks, int threads, int lds_bytes, unsigned usec, void *stream) {
+extern "C" int pcm_tune_occupy_stamped(int blocks, int threads, int lds_bytes, unsigned usec,
+                                       unsigned long long *stamps, void *stream) {
     if (blocks <= 0 || threads <= 0 || threads > 1024 || lds_bytes < 0 || lds_bytes > 160 * 1024 || usec > 1000000u)
         return PCM_ERR_INVALID_ARG;
     if (lds_bytes > 64 * 1024 &&
@@ -28,7 +45,17 @@ extern "C" int pcm_tune_occupy(int blocks, int threads, int lds_bytes, unsigned 
                             lds_bytes) != hipSuccess)
         return PCM_ERR_LAUNCH;
     hipLaunchKernelGGL(pcm_occupy_kernel, dim3((unsigned)blocks), dim3((unsigned)threads), (size_t)lds_bytes,
-                       (hipStream_t)stream, 100ull * usec);
+                       (hipStream_t)stream, 100ull * usec, stamps);
+    return pcm_launch_status();
+}
+
+extern "C" int pcm_tune_occupy(int blocks, int threads, int lds_bytes, unsigned usec, void *stream) {
+    return pcm_tune_occupy_stamped(blocks, threads, lds_bytes, usec, nullptr, stream);
+}
+
+extern "C" int pcm_tune_clock_stamp(unsigned long long *out, void *stream) {
+    if (!out) return PCM_ERR_INVALID_ARG;
+    hipLaunchKernelGGL(pcm_clock_stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out);
     return pcm_launch_status();
 }
 

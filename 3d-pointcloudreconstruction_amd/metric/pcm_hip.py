@@ -172,6 +172,11 @@ def _open(path):
     if hasattr(L, "pcm_tune_occupy"):  # absent from A/B builds of older sources
         L.pcm_tune_occupy.restype = ci
         L.pcm_tune_occupy.argtypes = [ci, ci, ci, ctypes.c_uint, vp]
+    if hasattr(L, "pcm_tune_occupy_stamped"):
+        L.pcm_tune_occupy_stamped.restype = ci
+        L.pcm_tune_occupy_stamped.argtypes = [ci, ci, ci, ctypes.c_uint, vp, vp]
+        L.pcm_tune_clock_stamp.restype = ci
+        L.pcm_tune_clock_stamp.argtypes = [vp, vp]
     cd = ctypes.c_double
     L.pcm_icp.restype = ci
     L.pcm_icp.argtypes = [vp, vp, ci, ci, vp, ci, cd, vp, vp, vp, vp, cs, vp]
@@ -613,13 +618,25 @@ def chamfer_slow_paths(workspace, b: int, n: int, m: int) -> int:
     return r
 
 
-def tune_occupy(dev: torch.device, blocks: int, threads: int, lds_bytes: int, usec: int) -> None:
+def tune_occupy(dev: torch.device, blocks: int, threads: int, lds_bytes: int, usec: int, stamps=None) -> None:
     """Internal (tests): hold `blocks` workgroups of `threads` threads and
     `lds_bytes` of LDS resident for `usec` microseconds on the current stream,
-    issuing only s_sleep -- another kernel sharing the CUs."""
+    issuing only s_sleep -- another kernel sharing the CUs.  stamps: an int64
+    device tensor of 3, initialised to (-1, 0, 0): the earliest workgroup
+    start, the latest end (s_memrealtime ticks, 100 MHz) and the count of
+    workgroups that started."""
     with torch.cuda.device(dev):
-        _check(load_library().pcm_tune_occupy(int(blocks), int(threads), int(lds_bytes), int(usec), _stream(dev)),
-               "pcm_tune_occupy")
+        _check(load_library().pcm_tune_occupy_stamped(int(blocks), int(threads), int(lds_bytes), int(usec),
+                                                      _ptr(stamps), _stream(dev)), "pcm_tune_occupy_stamped")
+
+
+def tune_clock_stamp(out) -> None:
+    """Internal (tests): a one-thread kernel on the current stream writes the
+    GPU real-time clock (s_memrealtime, 100 MHz ticks) to the int64 device
+    scalar `out`."""
+    dev = out.device
+    with torch.cuda.device(dev):
+        _check(load_library().pcm_tune_clock_stamp(_ptr(out), _stream(dev)), "pcm_tune_clock_stamp")
 
 
 def tune_num_chamfer_loss_grad_variants() -> int:

@@ -10,10 +10,14 @@ check, at BASELINE config 2 (B=32, N=M=1024):
   * outputs bit-identical to the step run alone, and to the oracle;
   * no gradient-phase wait timed out (slow-path count unchanged);
   * the step's time, recorded (gpurun_out/test_records/coresidency.json).
-Case "block_half" takes every CU of half the chip (LDS) for 1 ms: one of the
-step's 257 workgroups cannot be resident until the occupier leaves, so its
-batch element's other workgroups wait that long -- the step takes about the
-occupier's remaining time, and is still exact without a timeout.
+Every case proves the overlap it claims: the occupier's workgroups stamp
+their first start and last end (s_memrealtime) and count themselves in; the
+host launches the step only once all of them have started (read on a stream
+of its own while they run), and one-thread clock-stamp kernels before and
+after the step on its stream bracket its run.  The step must start inside the
+occupier's interval, and where it fits beside the occupier, end there too.
+Case "block_half" takes every CU of half the chip's LDS for 1 ms; whether the
+step also ends inside it is recorded, not asserted.
 """
 import json
 import os
@@ -82,21 +86,42 @@ def _alone_us(step, dev, reps=20):
     return e0.elapsed_time(e1) * 1000.0 / reps
 
 
-def _beside(step, dev, start_other):
-    """start the other kernel on a side stream, give it time to become
-    resident, then the step on the current stream; the step's event time"""
-    side = torch.cuda.Stream(dev)
-    side.wait_stream(torch.cuda.current_stream(dev))
-    with torch.cuda.stream(side):
-        start_other()
-    time.sleep(2e-4)
+def _read_now(t, dev):
+    """t's current content, copied on a stream of its own (so the copy does not
+    wait for the other streams' kernels, which may still be running)."""
+    poll = torch.cuda.Stream(dev)
+    host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
+    with torch.cuda.stream(poll):
+        host.copy_(t, non_blocking=True)
+    poll.synchronize()
+    return host.clone()
+
+
+def _wait_for(t, dev, ready, what, limit_s=0.5):
+    t0 = time.perf_counter()
+    while True:
+        v = _read_now(t, dev)
+        if ready(v):
+            return v
+        assert time.perf_counter() - t0 < limit_s, f"{what} not reached within {limit_s} s: {v.tolist()}"
+        time.sleep(2e-5)
+
+
+def _step_bracketed(step, dev):
+    """The step on the current stream between two one-thread clock-stamp
+    kernels: [m0, m1] (s_memrealtime ticks, 100 MHz) contains its whole run."""
+    import pcm_hip
+    marks = torch.zeros(2, dtype=torch.int64, device=dev)
     s = torch.cuda.current_stream(dev)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    pcm_hip.tune_clock_stamp(marks[0])
     e0.record(s)
     step["run"]()
     e1.record(s)
+    pcm_hip.tune_clock_stamp(marks[1])
     torch.cuda.synchronize(dev)
-    return e0.elapsed_time(e1) * 1000.0
+    m0, m1 = (int(x) for x in marks.cpu())
+    return e0.elapsed_time(e1) * 1000.0, m0, m1
 
 
 # (blocks, threads, LDS bytes, microseconds) of the occupier
@@ -105,44 +130,81 @@ OCCUPIERS = {
     "light": (256, 256, 0, 1000),
     # 16 waves and 32 KB LDS on every CU: the step's 8-wave workgroups still fit beside it
     "heavy_waves": (256, 1024, 32 * 1024, 1000),
-    # 128 KB LDS on 128 CUs (half of every XCD): the step's ~55 KB workgroups fit only
-    # on the other half, two per CU -- 256 slots for 257 workgroups
+    # 128 KB LDS on 128 CUs (half of every XCD): the step's workgroups fit only
+    # on the other half
     "block_half": (128, 1024, 128 * 1024, 1000),
 }
 
 
 @pytest.mark.parametrize("case", sorted(OCCUPIERS))
 def test_loss_grad_beside_occupier(cuda, oracle, step, case):
+    # the occupier is RESIDENT (every workgroup started: its own count, read
+    # while it runs) before the step is launched, and the step's bracketing
+    # clock stamps prove it started inside the occupier's [first start, last
+    # end]; where the step fits beside the occupier it must also END inside it
     import pcm_hip
     blocks, threads, lds, usec = OCCUPIERS[case]
     slow0 = pcm_hip.chamfer_slow_paths(step["ws"], B, N, M)
     alone = _alone_us(step, cuda)
     for k in ("d1", "d2", "i1", "i2", "mo", "gx1", "gx2"):  # poison: the step must rewrite them
         step["bufs"][k].fill_(-7)
-    us = _beside(step, cuda, lambda: pcm_hip.tune_occupy(cuda, blocks, threads, lds, usec))
+    stamps = torch.tensor([-1, 0, 0], dtype=torch.int64, device=cuda)  # (-1: the largest unsigned start)
+    side = torch.cuda.Stream(cuda)
+    side.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(side):
+        pcm_hip.tune_occupy(cuda, blocks, threads, lds, usec, stamps)
+    _wait_for(stamps, cuda, lambda v: int(v[2]) == blocks, f"{case}: all {blocks} occupier workgroups resident")
+    us, m0, m1 = _step_bracketed(step, cuda)
+    torch.cuda.synchronize(cuda)
+    o0, o1, started = (int(x) for x in stamps.cpu())
     got = step["outputs"]()
     for g, r in zip(got, step["ref"]):
         assert torch.equal(g, r), case
     pcm_hip.chamfer_workspace_status(step["ws"], B, N, M)
     slow = pcm_hip.chamfer_slow_paths(step["ws"], B, N, M) - slow0
     assert slow == 0, f"{case}: {slow} gradient-phase waits timed out"
+    assert started == blocks
+    assert o0 < m0 < o1, f"{case}: the step did not start while the occupier ran ({o0}, {m0}, {o1})"
+    fits = case != "block_half"
+    if fits:
+        assert m1 < o1, f"{case}: the step did not finish beside the occupier ({m1} >= {o1})"
     _record(case, {"occupier": {"blocks": blocks, "threads": threads, "lds_bytes": lds, "usec": usec},
-                   "step_us_beside": us, "step_us_alone": alone, "slow_paths": slow})
+                   "step_us_beside": us, "step_us_alone": alone, "slow_paths": slow,
+                   "ticks_100mhz": {"occupier_first_start": 0, "step_start_mark": m0 - o0,
+                                    "step_end_mark": m1 - o0, "occupier_last_end": o1 - o0},
+                   "step_inside_occupier": m1 < o1})
 
 
 def test_loss_grad_beside_gemm(cuda, oracle, step):
-    # a real library kernel on a side stream (hipBLASLt GEMM, ~1 ms, every CU)
+    # a real library kernel on a side stream (a 4096^3 fp32 GEMM on every CU,
+    # ~1 ms) bracketed by clock stamps; the step is launched only once the
+    # GEMM's leading stamp has landed (the GEMM is then executing), and must
+    # start before its trailing stamp: launched while the GEMM held the CUs
     import pcm_hip
     a = torch.rand(4096, 4096, device=cuda)
     bm = torch.rand(4096, 4096, device=cuda)
     torch.mm(a, bm)
     torch.cuda.synchronize()
     slow0 = pcm_hip.chamfer_slow_paths(step["ws"], B, N, M)
-    us = _beside(step, cuda, lambda: torch.mm(a, bm))
+    gm = torch.zeros(2, dtype=torch.int64, device=cuda)
+    side = torch.cuda.Stream(cuda)
+    side.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(side):
+        pcm_hip.tune_clock_stamp(gm[0])
+        torch.mm(a, bm)
+        pcm_hip.tune_clock_stamp(gm[1])
+    _wait_for(gm, cuda, lambda v: int(v[0]) != 0, "the GEMM's leading stamp")
+    us, m0, m1 = _step_bracketed(step, cuda)
+    torch.cuda.synchronize(cuda)
+    g0, g1 = (int(x) for x in gm.cpu())
     for g, r in zip(step["outputs"](), step["ref"]):
         assert torch.equal(g, r)
     assert pcm_hip.chamfer_slow_paths(step["ws"], B, N, M) - slow0 == 0
-    _record("gemm_4096", {"step_us_beside": us})
+    assert g0 < m0 < g1, f"the step did not start while the GEMM ran ({g0}, {m0}, {g1})"
+    _record("gemm_4096", {"step_us_beside": us,
+                          "ticks_100mhz": {"gemm_start_mark": 0, "step_start_mark": m0 - g0,
+                                           "step_end_mark": m1 - g0, "gemm_end_mark": g1 - g0},
+                          "step_inside_gemm": m1 < g1})
 
 
 def test_reference_outputs_match_oracle(cuda, oracle, step):

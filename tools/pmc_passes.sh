@@ -24,4 +24,9 @@ timeout -s KILL 90 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum -d "$OUT/l2" -o l2 -
 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES \
     SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sq" -o sq --output-format csv \
     -- python3 "$PROG" > "$OUT/sq.log" 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES \
+    SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY -d "$OUT/sq_emdtrain" -o sq --output-format csv \
+    -- python3 "$PROG" emdtrain > "$OUT/sq_emdtrain.log" 2>&1
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$OUT/kt_emdtrain" -o kt --output-format csv \
+    -- python3 "$PROG" emdtrain > "$OUT/kt_emdtrain.log" 2>&1
 echo "pmc passes done"

@@ -64,6 +64,16 @@ def main(src, dst):
             for c, v in cs.items():
                 ent[c] = sum(v) / len(v)
                 ent[c + "_dispatches"] = len(v)
+    # the EMD training call's own pass (tools/profile_kernels.py emdtrain)
+    emdt = {}
+    for k, cs in read_counters(os.path.join(src, "sq_emdtrain")).items():
+        ent = emdt.setdefault(k, {})
+        for c, v in cs.items():
+            ent[c] = sum(v) / len(v)
+            ent[c + "_dispatches"] = len(v)
+    if emdt:
+        summary["counters_emd_training_call"] = emdt
+        summary["kernel_trace_emd_training_call"] = read_stats(os.path.join(src, "kt_emdtrain"))
     for k, ent in summary["counters"].items():
         if "FETCH_SIZE" in ent:  # KB per dispatch -> bytes, corrected
             ent["hbm_read_bytes"] = ent["FETCH_SIZE"] * 1024.0 * 2.0

@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
 """Fixed kernel sequence for rocprofv3 counter passes (BASELINE configs 2 and 3):
 20x Chamfer fused-loss forward, 20x Chamfer backward, 20x one-launch loss +
-gradient and 20x each of its variants 14 and 15, 20x the channel-plane forward and 20x the
-strided backward (B=32, N=M=1024), 3x EMD forward (B=16, N=1024, 50 iters, eps 0.005),
+gradient, 20x the training call's form of it (channel planes, lambda 100) with its
+rescale launch, 20x the channel-plane forward and 20x the strided backward
+(B=32, N=M=1024), 3x EMD forward (B=16, N=1024, 50 iters, eps 0.005),
 then BASELINE config 5 (B=8, N=M=16384): 2x the fp32 forward and 2x the fp16
 forward (both the grid path from 4096 points), 1x the dense fp16 forward,
-2x the fp16 backward.  Inputs resident before the loop."""
+2x the fp16 backward.  Inputs resident before the loop.
+`profile_kernels.py emdtrain`: the EMD training call alone (emd_training_call)."""
 import os
 import sys
 
@@ -16,7 +18,26 @@ sys.path.insert(0, os.path.join(REPO, "3d-pointcloudreconstruction_amd", "metric
 import pcm_hip  # noqa: E402
 
 
+def emd_training_call():
+    """The EMD training call alone (loss/loss.py:23: eps 0.05, 3000 iterations)
+    on bench.py's committed generator predictions, 3 forwards: its counters
+    in a pass of their own (the kernels share names with config 3's)."""
+    sys.path.insert(0, REPO)
+    import bench
+    dev = torch.device("cuda:0")
+    pred, points = bench.generator_predictions(dev)
+    b, n, _ = pred.shape
+    ed = torch.empty(b, n, device=dev)
+    ea = torch.empty(b, n, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        pcm_hip.emd_forward(pred, points, 0.05, 3000, ed, ea)
+    torch.cuda.synchronize()
+    print("done")
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "emdtrain":
+        return emd_training_call()
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(0)
     B, N = 32, 1024
@@ -42,17 +63,20 @@ def main():
     mo3 = torch.empty(3, device=dev)
     for _ in range(20):
         pcm_hip.chamfer_loss_grad(x1, x2, 1.0 / (B * N), 1.0 / (B * N), d1, d2, i1, i2, mo3, gx1, gx2, ws)
-    # fused variants 14 (4-byte argmin granules, own argmins from the forward) and 15 (14 with 16-byte
-    # granule stores), each on a fresh zero-filled workspace of its own (a granule-format switch on one
-    # workspace makes its first call recompute every argmin)
-    for v in (14, 15):
-        wsv = torch.zeros_like(ws)
-        for _ in range(20):
-            pcm_hip.chamfer_loss_grad(x1, x2, 1.0 / (B * N), 1.0 / (B * N), d1, d2, i1, i2, mo3, gx1, gx2, wsv,
-                                      variant=v)
     # the unchanged caller's kernels: channel planes read in place, the graddist torch's mean hands over
     xp = x1.transpose(1, 2).contiguous()
     gp = torch.empty_like(xp)
+    # the training call's one-launch step (train.py:163,169: planes, lambda_cd = 100 learned) and its
+    # backward's rescale launch (nothing to do once the scale is learned)
+    mo4 = torch.empty(4, device=dev)
+    lam = torch.full((1,), 100.0, device=dev)
+    nxt = torch.empty(1, device=dev)
+    w = pcm_hip.mean_weight(B * N)
+    for _ in range(20):
+        pcm_hip.chamfer_loss_grad(xp.transpose(1, 2), x2, w, w, d1, d2, i1, i2, mo4, gp.transpose(1, 2), gx2, ws,
+                                  layouts=(1, 0), grad_scale=lam)
+        pcm_hip.chamfer_loss_grad_rescale(xp.transpose(1, 2), x2, (1, 0), w, w, lam, mo4[3:4], nxt, i1, i2,
+                                          gp.transpose(1, 2), gx2)
     for _ in range(20):
         pcm_hip.chamfer_forward_layout(xp.transpose(1, 2), x2, 1, 0, d1, d2, i1, i2)
     for _ in range(20):

@@ -16,7 +16,7 @@ host launches the step only once all of them have started (read on a stream
 of its own while they run), and one-thread clock-stamp kernels before and
 after the step on its stream bracket its run.  The step must start inside the
 occupier's interval, and where it fits beside the occupier, end there too.
-Case "block_half" takes every CU of half the chip's LDS for 1 ms; whether the
+Case "block_half" takes every CU of half the chip's LDS for 4 ms; whether the
 step also ends inside it is recorded, not asserted.
 """
 import json
@@ -86,25 +86,29 @@ def _alone_us(step, dev, reps=20):
     return e0.elapsed_time(e1) * 1000.0 / reps
 
 
-def _read_now(t, dev):
-    """t's current content, copied on a stream of its own (so the copy does not
-    wait for the other streams' kernels, which may still be running)."""
-    poll = torch.cuda.Stream(dev)
-    host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-    with torch.cuda.stream(poll):
-        host.copy_(t, non_blocking=True)
-    poll.synchronize()
-    return host.clone()
+class _Poller:
+    """Reads a device tensor's current content while other streams' kernels
+    still run: a copy on a stream of its own into pinned memory, both made
+    before the kernels start (allocating pinned memory takes milliseconds)."""
 
+    def __init__(self, t, dev):
+        self.t = t
+        self.stream = torch.cuda.Stream(dev)
+        self.host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
 
-def _wait_for(t, dev, ready, what, limit_s=0.5):
-    t0 = time.perf_counter()
-    while True:
-        v = _read_now(t, dev)
-        if ready(v):
-            return v
-        assert time.perf_counter() - t0 < limit_s, f"{what} not reached within {limit_s} s: {v.tolist()}"
-        time.sleep(2e-5)
+    def read(self):
+        with torch.cuda.stream(self.stream):
+            self.host.copy_(self.t, non_blocking=True)
+        self.stream.synchronize()
+        return self.host.clone()
+
+    def wait_for(self, ready, what, limit_s=0.5):
+        t0 = time.perf_counter()
+        while True:
+            v = self.read()
+            if ready(v):
+                return v
+            assert time.perf_counter() - t0 < limit_s, f"{what} not reached within {limit_s} s: {v.tolist()}"
 
 
 def _step_bracketed(step, dev):
@@ -127,12 +131,12 @@ def _step_bracketed(step, dev):
 # (blocks, threads, LDS bytes, microseconds) of the occupier
 OCCUPIERS = {
     # a few waves on every CU, no LDS: an RCCL-like share that leaves room
-    "light": (256, 256, 0, 1000),
+    "light": (256, 256, 0, 4000),
     # 16 waves and 32 KB LDS on every CU: the step's 8-wave workgroups still fit beside it
-    "heavy_waves": (256, 1024, 32 * 1024, 1000),
+    "heavy_waves": (256, 1024, 32 * 1024, 4000),
     # 128 KB LDS on 128 CUs (half of every XCD): the step's workgroups fit only
     # on the other half
-    "block_half": (128, 1024, 128 * 1024, 1000),
+    "block_half": (128, 1024, 128 * 1024, 4000),
 }
 
 
@@ -149,11 +153,13 @@ def test_loss_grad_beside_occupier(cuda, oracle, step, case):
     for k in ("d1", "d2", "i1", "i2", "mo", "gx1", "gx2"):  # poison: the step must rewrite them
         step["bufs"][k].fill_(-7)
     stamps = torch.tensor([-1, 0, 0], dtype=torch.int64, device=cuda)  # (-1: the largest unsigned start)
+    poller = _Poller(stamps, cuda)
     side = torch.cuda.Stream(cuda)
     side.wait_stream(torch.cuda.current_stream(cuda))
+    torch.cuda.synchronize(cuda)
     with torch.cuda.stream(side):
         pcm_hip.tune_occupy(cuda, blocks, threads, lds, usec, stamps)
-    _wait_for(stamps, cuda, lambda v: int(v[2]) == blocks, f"{case}: all {blocks} occupier workgroups resident")
+    poller.wait_for(lambda v: int(v[2]) == blocks, f"{case}: all {blocks} occupier workgroups resident")
     us, m0, m1 = _step_bracketed(step, cuda)
     torch.cuda.synchronize(cuda)
     o0, o1, started = (int(x) for x in stamps.cpu())
@@ -176,8 +182,8 @@ def test_loss_grad_beside_occupier(cuda, oracle, step, case):
 
 
 def test_loss_grad_beside_gemm(cuda, oracle, step):
-    # a real library kernel on a side stream (a 4096^3 fp32 GEMM on every CU,
-    # ~1 ms) bracketed by clock stamps; the step is launched only once the
+    # real library kernels on a side stream (four 4096^3 fp32 GEMMs on every
+    # CU, ~1 ms each) bracketed by clock stamps; the step is launched only once the
     # GEMM's leading stamp has landed (the GEMM is then executing), and must
     # start before its trailing stamp: launched while the GEMM held the CUs
     import pcm_hip
@@ -187,13 +193,16 @@ def test_loss_grad_beside_gemm(cuda, oracle, step):
     torch.cuda.synchronize()
     slow0 = pcm_hip.chamfer_slow_paths(step["ws"], B, N, M)
     gm = torch.zeros(2, dtype=torch.int64, device=cuda)
+    poller = _Poller(gm, cuda)
     side = torch.cuda.Stream(cuda)
     side.wait_stream(torch.cuda.current_stream(cuda))
+    torch.cuda.synchronize(cuda)
     with torch.cuda.stream(side):
         pcm_hip.tune_clock_stamp(gm[0])
-        torch.mm(a, bm)
+        for _ in range(4):  # ~4 ms of GEMMs on every CU
+            torch.mm(a, bm)
         pcm_hip.tune_clock_stamp(gm[1])
-    _wait_for(gm, cuda, lambda v: int(v[0]) != 0, "the GEMM's leading stamp")
+    poller.wait_for(lambda v: int(v[0]) != 0, "the GEMM's leading stamp")
     us, m0, m1 = _step_bracketed(step, cuda)
     torch.cuda.synchronize(cuda)
     g0, g1 = (int(x) for x in gm.cpu())

@@ -24,6 +24,7 @@
 #   emddiag    tools/emd_diag.py: config 3 per iteration, the training call by bidder count
 #   abr        tools/ab_ref_call.py (the unchanged caller's pieces: forward geometries, strided backward)
 #   abl        tools/ab_launch_form.py (N=1 region: direct C loop against the warmed 20-step graph)
+#   gfc        tools/grid_first_call.py in fresh processes (+ a per-call kernel trace)
 #   tct        rocprofv3 kernel traces of tools/training_call_trace.py {after,before,reference}
 set -o pipefail
 TAG=$1
@@ -75,6 +76,12 @@ for S in "$@"; do
               PCM_HIP_LIB=$L timeout -k 10 300 python -u tools/ab_ref_call.py >> "$O/ab_ref_call_libs.txt" 2>&1 || exit 1
           done; done ;;
     abr) timeout -k 10 300 python -u tools/ab_ref_call.py > "$O/ab_ref_call.txt" 2>&1 ;;
+    gfc) for o in f32,f32,f32,f16,f16 f16,f16,f32,f32 dense,tiny,f32,f32 ; do
+             timeout -k 10 120 python -u tools/grid_first_call.py $o >> "$O/grid_first_call.txt" 2>&1 || exit 1
+         done
+         (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$O/gfc_kt" -o run \
+             --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/grid_first_call.py" f32,f32,f32,f16,f16 \
+             > "$GRAFT_REPO_ROOT/$O/gfc_kt.log" 2>&1) ;;
     abl) timeout -k 10 300 python -u tools/ab_launch_form.py 10 > "$O/ab_launch_form.txt" 2>&1 ;;
     tct) for f in after before reference; do
              (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/tct_$f" -o run \

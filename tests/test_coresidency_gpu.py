@@ -99,7 +99,10 @@ class _Poller:
 
     def __init__(self, t, dev):
         self.t = t
-        self.stream = torch.cuda.Stream(dev)
+        # from the high-priority pool: never the same HIP stream as a side
+        # stream of the default pool (torch hands those out round-robin), or
+        # the copy would queue behind the kernel it is meant to watch
+        self.stream = torch.cuda.Stream(dev, priority=-1)
         self.host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
 
     def read(self):

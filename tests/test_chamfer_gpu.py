@@ -1137,3 +1137,70 @@ def test_backward_slot_buckets_crowded(cuda, oracle, kind):
         torch.cuda.synchronize()
         np.testing.assert_array_equal(gx1.cpu().contiguous().numpy().view(np.int32), r1.view(np.int32))
         np.testing.assert_array_equal(gx2.cpu().numpy().view(np.int32), r2.view(np.int32))
+
+
+def test_captured_workspaces_survive_eviction_and_growth(cuda, oracle):
+    # a graph keeps the raw pointers of the cached workspaces
+    # it was captured with.  After capture, the fused-loss workspace is evicted
+    # from the LRU (17 other shapes) and the grid forward's per-stream
+    # workspace is replaced by a larger one; freed memory is then reused and
+    # scribbled over.  Replays must still be exact (pcm_hip pins every
+    # workspace handed out under capture).
+    import pcm_hip
+    b, n, m = 4, 512, 300
+    a, c = _clouds(150, b, n, m)
+    x1, x2 = a.to(cuda), c.to(cuda)
+    d1, d2 = torch.empty(b, n, device=cuda), torch.empty(b, m, device=cuda)
+    i1 = torch.empty(b, n, dtype=torch.int32, device=cuda)
+    i2 = torch.empty(b, m, dtype=torch.int32, device=cuda)
+    mo = torch.empty(3, device=cuda)
+    gx1, gx2 = torch.empty_like(x1), torch.empty_like(x2)
+    w1, w2 = pcm_hip.mean_weight(b * n), pcm_hip.mean_weight(b * m)
+    gb, gn = 16, 4096  # the grid forward (B N M >= 2^28)
+    g = torch.Generator().manual_seed(151)
+    y1, y2 = torch.rand(gb, gn, 3, generator=g), torch.rand(gb, gn, 3, generator=g)
+    z1, z2 = y1.to(cuda), y2.to(cuda)
+    f1, f2 = torch.empty(gb, gn, device=cuda), torch.empty(gb, gn, device=cuda)
+    k1 = torch.empty(gb, gn, dtype=torch.int32, device=cuda)
+    k2 = torch.empty(gb, gn, dtype=torch.int32, device=cuda)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2)
+            pcm_hip.chamfer_forward(z1, z2, f1, f2, k1, k2)
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=s):
+        pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2)
+        pcm_hip.chamfer_forward(z1, z2, f1, f2, k1, k2)
+    with torch.cuda.stream(s):
+        for bb in range(1, 18):  # evict the captured fused-loss workspace from the LRU
+            pcm_hip.chamfer_workspace(cuda, bb, 8, 8)
+        big = torch.rand(gb, 2 * gn, 3, device=cuda)  # grows (replaces) this stream's grid workspace
+        pcm_hip.chamfer_forward(big, big, torch.empty(gb, 2 * gn, device=cuda),
+                                torch.empty(gb, 2 * gn, device=cuda),
+                                torch.empty(gb, 2 * gn, dtype=torch.int32, device=cuda),
+                                torch.empty(gb, 2 * gn, dtype=torch.int32, device=cuda))
+    torch.cuda.synchronize()
+    junk = [torch.full((1 << 22,), -1, dtype=torch.int32, device=cuda) for _ in range(16)]  # reuse freed memory
+    for t in (d1, d2, i1, i2, mo, gx1, gx2, f1, f2, k1, k2):
+        t.fill_(-5)
+    graph.replay()
+    graph.replay()
+    torch.cuda.synchronize()
+    del junk
+    r1, r2, j1, j2 = oracle.chamfer_forward(a.numpy(), c.numpy())
+    np.testing.assert_array_equal(i1.cpu().numpy(), j1)
+    np.testing.assert_array_equal(i2.cpu().numpy(), j2)
+    rg1, rg2 = oracle.chamfer_backward(a.numpy(), c.numpy(), np.full((b, n), w1, np.float32),
+                                       np.full((b, m), w2, np.float32), j1, j2)
+    np.testing.assert_array_equal(gx1.cpu().numpy().view(np.int32), rg1.view(np.int32))
+    np.testing.assert_array_equal(gx2.cpu().numpy().view(np.int32), rg2.view(np.int32))
+    ref = float(r1.astype(np.float64).mean()) + float(r2.astype(np.float64).mean())
+    np.testing.assert_allclose(mo[2].item(), ref, rtol=2e-6)
+    q1, q2, p1, p2 = oracle.chamfer_forward(y1.numpy(), y2.numpy())
+    np.testing.assert_array_equal(k1.cpu().numpy(), p1)
+    np.testing.assert_array_equal(k2.cpu().numpy(), p2)
+    np.testing.assert_array_equal(f1.cpu().numpy().view(np.int32), q1.view(np.int32))

@@ -29,9 +29,9 @@ def main():
     i2 = torch.empty(b, m, dtype=torch.int32, device=dev)
     gx1, gx2 = torch.empty(b, n, 3, device=dev), torch.empty(b, m, 3, device=dev)
     mo = torch.empty(3, device=dev)
-    ws = pcm_hip.chamfer_workspace(dev, b, n, m)
     w1, w2 = 1.0 / (b * n), 1.0 / (b * m)
-    vs = list(range(7, pcm_hip.tune_num_chamfer_loss_grad_variants()))
+    vs = list(range(7, pcm_hip.tune_num_chamfer_loss_grad_variants()))  # (loads the tuning build first)
+    ws = pcm_hip.chamfer_workspace(dev, b, n, m)  # sized for every variant of the tuning build
     if os.environ.get("AB_VARIANTS"):  # e.g. AB_VARIANTS=11,15
         vs = [int(v) for v in os.environ["AB_VARIANTS"].split(",")]
     out = {}

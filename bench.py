@@ -72,7 +72,9 @@ BENCH_SEED = 1234                  # rank r's clouds: torch.Generator seed BENCH
 FWD_KERNEL = "chamfer_fwd_filt_kernel<float, 8, 4, 16, 1024, 3>"  # default fused-loss forward (clouds <= 1024)
 BWD_KERNEL = "chamfer_bwd_slots_kernel"
 FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true>"  # default variant 15 (4-byte granules in 16-byte stores, local gradient data)
-PMC_SUMMARY = os.path.join(REPO, "profiles", "r05", "pmc_summary.json")
+# the newest committed counter summary (profiles/rNN/pmc_summary.json)
+PMC_SUMMARY = next((p for p in (os.path.join(REPO, "profiles", r, "pmc_summary.json") for r in ("r06", "r05"))
+                    if os.path.exists(p)), os.path.join(REPO, "profiles", "r05", "pmc_summary.json"))
 
 # MI355X peaks (/opt/skills/guides/MI355X_MICROARCH.md, chip-level parameters)
 HBM_PEAK_GBS = 8000.0
@@ -549,28 +551,34 @@ def emd_leg(dev, reps=10, eps=EMD_EPS, iters=EMD_ITERS, clouds=None, label="unif
                          "unit": "T lane-ops/s", "frac": lane_ops / VALU_LANE_OPS_PEAK,
                          "note": f"{EMD_LANE_OPS_PER_PAIR} lane-ops per (bidder, object) pair the reference "
                                  "evaluates; the build evaluates fewer (caches), so this is the reference-work rate"},
-            "roofline_executed": emd_executed_roofline(us) if clouds is None and eps == EMD_EPS else None}
+            "roofline_executed": (emd_executed_roofline(us) if clouds is None and eps == EMD_EPS else
+                                  emd_executed_roofline(us, "counters_emd_training_call")
+                                  if clouds is not None and eps == 0.05 and iters == 3000 else None)}
 
 
 # the EMD kernels as profile_kernels.py runs them (BASELINE config 3) in the committed PMC summary
 EMD_KERNELS = ("emd_seed_kernel<true, true>", "emd_auction_kernel<false, true, true>")
 
 
-def emd_executed_roofline(us):
-    """The work the build actually executes at BASELINE config 3: VALU wave
-    instructions per forward (seed + auction, rocprofv3 SQ_INSTS_VALU from the
-    committed PMC summary) x 64 lanes / this forward's time, against the
-    78.6 T lane-instruction issue ceiling."""
+def emd_executed_roofline(us, which="counters"):
+    """The work the build actually executes: VALU wave instructions per
+    forward (seed + auction, rocprofv3 SQ_INSTS_VALU from the committed PMC
+    summary: "counters" = BASELINE config 3, "counters_emd_training_call" =
+    the training call's own pass) x 64 lanes / this forward's time, against
+    the 78.6 T lane-instruction issue ceiling; with the auction's wait share
+    (SQ_WAIT_ANY / SQ_WAVE_CYCLES) and its busiest-wave view."""
     try:
         with open(PMC_SUMMARY) as fh:
-            cnt = json.load(fh)["counters"]
+            cnt = json.load(fh)[which]
         waves = sum(cnt[k]["SQ_INSTS_VALU"] for k in EMD_KERNELS)
-    except (OSError, KeyError, ValueError):
+        auc = cnt[EMD_KERNELS[1]]
+        wait = auc["SQ_WAIT_ANY"] / auc["SQ_WAVE_CYCLES"] if "SQ_WAIT_ANY" in auc else None
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
         return None
     rate = waves * 64 / (us * 1e-6)
     return {"bound": "valu", "valu_wave_instructions": waves, "achieved": rate / 1e12,
             "peak": VALU_LANE_OPS_PEAK / 1e12, "unit": "T lane-ops/s", "frac": rate / VALU_LANE_OPS_PEAK,
-            "source": os.path.relpath(PMC_SUMMARY, REPO)}
+            "auction_wait_share": wait, "source": os.path.relpath(PMC_SUMMARY, REPO) + ":" + which}
 
 
 def chamfer_executed_roofline(kernel, us):

@@ -12,19 +12,27 @@ extern "C" int pcm_version(void) { return 100; /* 0.1.0 */ }
 // advanced `usec`.  stamps (nullable, device, 3 words, caller-initialised to
 // {~0, 0, 0}): the earliest workgroup start, the latest workgroup end (both
 // s_memrealtime ticks) and the number of workgroups that started -- the
-// evidence that the occupier was resident while another kernel ran.
+// evidence that the occupier was resident while another kernel ran;
+// host_flag (nullable, pinned host memory): set to 1 once every workgroup
+// has started.
 // pcm_tune_clock_stamp writes s_memrealtime to *out from a one-thread kernel:
 // on the step's stream just before and after the step it brackets the step's
 // whole run (a stream runs its kernels one after the other).
 // ---------------------------------------------------------------------------
 namespace {
-__global__ void pcm_occupy_kernel(unsigned long long ticks, unsigned long long *stamps) {
+__global__ void pcm_occupy_kernel(unsigned long long ticks, unsigned long long *stamps, unsigned *host_flag) {
     extern __shared__ int occupy_lds[];
     (void)occupy_lds;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     if (stamps && threadIdx.x == 0) {
         atomicMin(stamps, t0);
-        atomicAdd(stamps + 2, 1ull);
+        const unsigned long long old = atomicAdd(stamps + 2, 1ull);
+        // the last workgroup to start tells the host, through pinned host
+        // memory (no copy on another stream, which could share a hardware
+        // queue with this kernel and wait for it)
+        if (host_flag && old + 1 == (unsigned long long)gridDim.x) {
+            __hip_atomic_store(host_flag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
     unsigned long long t = t0;
     while ((t = __builtin_amdgcn_s_memrealtime()) - t0 < ticks) __builtin_amdgcn_s_sleep(16);
@@ -32,12 +40,14 @@ __global__ void pcm_occupy_kernel(unsigned long long ticks, unsigned long long *
 }
 
 __global__ void pcm_clock_stamp_kernel(unsigned long long *out) {
-    if (threadIdx.x == 0) *out = __builtin_amdgcn_s_memrealtime();
+    // (out may be pinned host memory: a system-scope store the host can poll)
+    if (threadIdx.x == 0)
+        __hip_atomic_store(out, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 }  // namespace
 
-extern "C" int pcm_tune_occupy_stamped(int blocks, int threads, int lds_bytes, unsigned usec,
-                                       unsigned long long *stamps, void *stream) {
+extern "C" int pcm_tune_occupy_flagged(int blocks, int threads, int lds_bytes, unsigned usec,
+                                       unsigned long long *stamps, unsigned *host_flag, void *stream) {
     if (blocks <= 0 || threads <= 0 || threads > 1024 || lds_bytes < 0 || lds_bytes > 160 * 1024 || usec > 1000000u)
         return PCM_ERR_INVALID_ARG;
     if (lds_bytes > 64 * 1024 &&
@@ -45,12 +55,17 @@ extern "C" int pcm_tune_occupy_stamped(int blocks, int threads, int lds_bytes, u
                             lds_bytes) != hipSuccess)
         return PCM_ERR_LAUNCH;
     hipLaunchKernelGGL(pcm_occupy_kernel, dim3((unsigned)blocks), dim3((unsigned)threads), (size_t)lds_bytes,
-                       (hipStream_t)stream, 100ull * usec, stamps);
+                       (hipStream_t)stream, 100ull * usec, stamps, host_flag);
     return pcm_launch_status();
 }
 
+extern "C" int pcm_tune_occupy_stamped(int blocks, int threads, int lds_bytes, unsigned usec,
+                                       unsigned long long *stamps, void *stream) {
+    return pcm_tune_occupy_flagged(blocks, threads, lds_bytes, usec, stamps, nullptr, stream);
+}
+
 extern "C" int pcm_tune_occupy(int blocks, int threads, int lds_bytes, unsigned usec, void *stream) {
-    return pcm_tune_occupy_stamped(blocks, threads, lds_bytes, usec, nullptr, stream);
+    return pcm_tune_occupy_flagged(blocks, threads, lds_bytes, usec, nullptr, nullptr, stream);
 }
 
 extern "C" int pcm_tune_clock_stamp(unsigned long long *out, void *stream) {

@@ -177,6 +177,9 @@ def _open(path):
         L.pcm_tune_occupy_stamped.argtypes = [ci, ci, ci, ctypes.c_uint, vp, vp]
         L.pcm_tune_clock_stamp.restype = ci
         L.pcm_tune_clock_stamp.argtypes = [vp, vp]
+    if hasattr(L, "pcm_tune_occupy_flagged"):
+        L.pcm_tune_occupy_flagged.restype = ci
+        L.pcm_tune_occupy_flagged.argtypes = [ci, ci, ci, ctypes.c_uint, vp, vp, vp]
     cd = ctypes.c_double
     L.pcm_icp.restype = ci
     L.pcm_icp.argtypes = [vp, vp, ci, ci, vp, ci, cd, vp, vp, vp, vp, cs, vp]
@@ -618,16 +621,19 @@ def chamfer_slow_paths(workspace, b: int, n: int, m: int) -> int:
     return r
 
 
-def tune_occupy(dev: torch.device, blocks: int, threads: int, lds_bytes: int, usec: int, stamps=None) -> None:
+def tune_occupy(dev: torch.device, blocks: int, threads: int, lds_bytes: int, usec: int, stamps=None,
+                host_flag=None) -> None:
     """Internal (tests): hold `blocks` workgroups of `threads` threads and
     `lds_bytes` of LDS resident for `usec` microseconds on the current stream,
     issuing only s_sleep -- another kernel sharing the CUs.  stamps: an int64
     device tensor of 3, initialised to (-1, 0, 0): the earliest workgroup
     start, the latest end (s_memrealtime ticks, 100 MHz) and the count of
-    workgroups that started."""
+    workgroups that started.  host_flag: a pinned host int32 tensor the last
+    workgroup to start sets to 1 (the host sees residency without a copy)."""
     with torch.cuda.device(dev):
-        _check(load_library().pcm_tune_occupy_stamped(int(blocks), int(threads), int(lds_bytes), int(usec),
-                                                      _ptr(stamps), _stream(dev)), "pcm_tune_occupy_stamped")
+        _check(load_library().pcm_tune_occupy_flagged(int(blocks), int(threads), int(lds_bytes), int(usec),
+                                                      _ptr(stamps), _ptr(host_flag), _stream(dev)),
+               "pcm_tune_occupy_flagged")
 
 
 def tune_clock_stamp(out) -> None:

@@ -5,23 +5,21 @@ that overlaps the next step's pcm_chamfer_loss_grad (bench.py capture_steps),
 and that kernel's workgroups wait on each other's argmin granules (bounded:
 2^16 polls, then the missing argmins are computed locally -- DESIGN.md 6).
 These tests stand a kernel in for RCCL's share of the CUs (pcm_tune_occupy:
-resident workgroups that only s_sleep; and a real GEMM on a side stream) and
-check, at BASELINE config 2 (B=32, N=M=1024):
-  * outputs bit-identical to the step run alone, and to the oracle;
+resident workgroups that only s_sleep; and real GEMMs on a side stream) and
+check, at BASELINE config 2 (B=32, N=M=1024), through tools/coresidency_probe.py
+(one process per case, see there):
+  * outputs bit-identical to the step run alone (which is the oracle's,
+    test_reference_outputs_match_oracle);
   * no gradient-phase wait timed out (slow-path count unchanged);
-  * the step's time, recorded (gpurun_out/test_records/coresidency.json).
-Every case proves the overlap it claims: the occupier's workgroups stamp
-their first start and last end (s_memrealtime) and count themselves in; the
-host launches the step only once all of them have started (read on a stream
-of its own while they run), and one-thread clock-stamp kernels before and
-after the step on its stream bracket its run.  The step must start inside the
-occupier's interval, and where it fits beside the occupier, end there too.
-Case "block_half" takes every CU of half the chip's LDS for 4 ms; whether the
-step also ends inside it is recorded, not asserted.
+  * OVERLAP, proven with the GPU's real-time clock: the other kernel tells the
+    host through pinned memory that it is running, the step is launched only
+    then, and one-thread clock-stamp kernels before and after the step must
+    fall inside the other kernel's [first start, last end] -- the step's start
+    always, its end where its workgroups fit beside the occupier;
+  * the times and clock stamps, recorded (gpurun_out/test_records/coresidency.json).
 """
 import json
 import os
-import time
 
 import numpy as np
 import pytest
@@ -81,148 +79,34 @@ def step(cuda):
     return dict(a=a, c=c, run=run, outputs=outputs, ref=outputs(), ws=ws, w=(w1, w2), bufs=bufs)
 
 
-def _alone_us(step, dev, reps=20):
-    s = torch.cuda.current_stream(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(s)
-    for _ in range(reps):
-        step["run"]()
-    e1.record(s)
-    e1.synchronize()
-    return e0.elapsed_time(e1) * 1000.0 / reps
+CASES = ("block_half", "gemm", "heavy_waves", "light")
 
 
-class _Poller:
-    """Reads a device tensor's current content while other streams' kernels
-    still run: a copy on a stream of its own into pinned memory, both made
-    before the kernels start (allocating pinned memory takes milliseconds)."""
-
-    def __init__(self, t, dev):
-        self.t = t
-        # from the high-priority pool: never the same HIP stream as a side
-        # stream of the default pool (torch hands those out round-robin), or
-        # the copy would queue behind the kernel it is meant to watch
-        self.stream = torch.cuda.Stream(dev, priority=-1)
-        self.host = torch.empty(t.shape, dtype=t.dtype, pin_memory=True)
-
-    def read(self):
-        with torch.cuda.stream(self.stream):
-            self.host.copy_(self.t, non_blocking=True)
-        self.stream.synchronize()
-        return self.host.clone()
-
-    def wait_for(self, ready, what, limit_s=0.5):
-        t0 = time.perf_counter()
-        while True:
-            v = self.read()
-            if ready(v):
-                return v
-            assert time.perf_counter() - t0 < limit_s, f"{what} not reached within {limit_s} s: {v.tolist()}"
-
-
-def _step_bracketed(step, dev):
-    """The step on the current stream between two one-thread clock-stamp
-    kernels: [m0, m1] (s_memrealtime ticks, 100 MHz) contains its whole run."""
-    import pcm_hip
-    marks = torch.zeros(2, dtype=torch.int64, device=dev)
-    s = torch.cuda.current_stream(dev)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    pcm_hip.tune_clock_stamp(marks[0])
-    e0.record(s)
-    step["run"]()
-    e1.record(s)
-    pcm_hip.tune_clock_stamp(marks[1])
-    torch.cuda.synchronize(dev)
-    m0, m1 = (int(x) for x in marks.cpu())
-    return e0.elapsed_time(e1) * 1000.0, m0, m1
-
-
-# (blocks, threads, LDS bytes, microseconds) of the occupier
-OCCUPIERS = {
-    # a few waves on every CU, no LDS: an RCCL-like share that leaves room
-    "light": (256, 256, 0, 4000),
-    # 16 waves and 32 KB LDS on every CU: the step's 8-wave workgroups still fit beside it
-    "heavy_waves": (256, 1024, 32 * 1024, 4000),
-    # 128 KB LDS on 128 CUs (half of every XCD): the step's workgroups fit only
-    # on the other half
-    "block_half": (128, 1024, 128 * 1024, 4000),
-}
-
-
-@pytest.mark.parametrize("case", sorted(OCCUPIERS))
-def test_loss_grad_beside_occupier(cuda, oracle, step, case):
-    # the occupier is RESIDENT (every workgroup started: its own count, read
-    # while it runs) before the step is launched, and the step's bracketing
-    # clock stamps prove it started inside the occupier's [first start, last
-    # end]; where the step fits beside the occupier it must also END inside it
-    import pcm_hip
-    blocks, threads, lds, usec = OCCUPIERS[case]
-    slow0 = pcm_hip.chamfer_slow_paths(step["ws"], B, N, M)
-    alone = _alone_us(step, cuda)
-    for k in ("d1", "d2", "i1", "i2", "mo", "gx1", "gx2"):  # poison: the step must rewrite them
-        step["bufs"][k].fill_(-7)
-    stamps = torch.tensor([-1, 0, 0], dtype=torch.int64, device=cuda)  # (-1: the largest unsigned start)
-    poller = _Poller(stamps, cuda)
-    side = torch.cuda.Stream(cuda)
-    side.wait_stream(torch.cuda.current_stream(cuda))
-    torch.cuda.synchronize(cuda)
-    with torch.cuda.stream(side):
-        pcm_hip.tune_occupy(cuda, blocks, threads, lds, usec, stamps)
-    poller.wait_for(lambda v: int(v[2]) == blocks, f"{case}: all {blocks} occupier workgroups resident")
-    us, m0, m1 = _step_bracketed(step, cuda)
-    torch.cuda.synchronize(cuda)
-    o0, o1, started = (int(x) for x in stamps.cpu())
-    got = step["outputs"]()
-    for g, r in zip(got, step["ref"]):
-        assert torch.equal(g, r), case
-    pcm_hip.chamfer_workspace_status(step["ws"], B, N, M)
-    slow = pcm_hip.chamfer_slow_paths(step["ws"], B, N, M) - slow0
-    assert slow == 0, f"{case}: {slow} gradient-phase waits timed out"
-    assert started == blocks
-    assert o0 < m0 < o1, f"{case}: the step did not start while the occupier ran ({o0}, {m0}, {o1})"
-    fits = case != "block_half"
-    if fits:
-        assert m1 < o1, f"{case}: the step did not finish beside the occupier ({m1} >= {o1})"
-    _record(case, {"occupier": {"blocks": blocks, "threads": threads, "lds_bytes": lds, "usec": usec},
-                   "step_us_beside": us, "step_us_alone": alone, "slow_paths": slow,
-                   "ticks_100mhz": {"occupier_first_start": 0, "step_start_mark": m0 - o0,
-                                    "step_end_mark": m1 - o0, "occupier_last_end": o1 - o0},
-                   "step_inside_occupier": m1 < o1})
-
-
-def test_loss_grad_beside_gemm(cuda, oracle, step):
-    # real library kernels on a side stream (four 4096^3 fp32 GEMMs on every
-    # CU, ~1 ms each) bracketed by clock stamps; the step is launched only once the
-    # GEMM's leading stamp has landed (the GEMM is then executing), and must
-    # start before its trailing stamp: launched while the GEMM held the CUs
-    import pcm_hip
-    a = torch.rand(4096, 4096, device=cuda)
-    bm = torch.rand(4096, 4096, device=cuda)
-    torch.mm(a, bm)
-    torch.cuda.synchronize()
-    slow0 = pcm_hip.chamfer_slow_paths(step["ws"], B, N, M)
-    gm = torch.zeros(2, dtype=torch.int64, device=cuda)
-    poller = _Poller(gm, cuda)
-    side = torch.cuda.Stream(cuda)
-    side.wait_stream(torch.cuda.current_stream(cuda))
-    torch.cuda.synchronize(cuda)
-    with torch.cuda.stream(side):
-        pcm_hip.tune_clock_stamp(gm[0])
-        for _ in range(4):  # ~4 ms of GEMMs on every CU
-            torch.mm(a, bm)
-        pcm_hip.tune_clock_stamp(gm[1])
-    poller.wait_for(lambda v: int(v[0]) != 0, "the GEMM's leading stamp")
-    us, m0, m1 = _step_bracketed(step, cuda)
-    torch.cuda.synchronize(cuda)
-    g0, g1 = (int(x) for x in gm.cpu())
-    for g, r in zip(step["outputs"](), step["ref"]):
-        assert torch.equal(g, r)
-    assert pcm_hip.chamfer_slow_paths(step["ws"], B, N, M) - slow0 == 0
-    assert g0 < m0 < g1, f"the step did not start while the GEMM ran ({g0}, {m0}, {g1})"
-    _record("gemm_4096", {"step_us_beside": us,
-                          "ticks_100mhz": {"gemm_start_mark": 0, "step_start_mark": m0 - g0,
-                                           "step_end_mark": m1 - g0, "gemm_end_mark": g1 - g0},
-                          "step_inside_gemm": m1 < g1})
+@pytest.mark.parametrize("case", CASES)
+def test_loss_grad_beside_other_kernel(cuda, case):
+    # tools/coresidency_probe.py in a process of its own (two fresh streams:
+    # in this long-lived process torch's stream pool may hand out two streams
+    # that share a hardware queue, which would run them one after the other).
+    # The other kernel signals through pinned host memory that it is running
+    # (every occupier workgroup started; the GEMMs' leading clock stamp); the
+    # step is launched only then, and its bracketing clock stamps must fall
+    # inside the other kernel's run: started inside always; ended inside where
+    # the step fits beside it.  Outputs bit-identical to the step alone, and no
+    # gradient-phase wait timed out.
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "tools", "coresidency_probe.py"), case],
+                       capture_output=True, text=True, timeout=110)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and lines, f"{case}: rc {r.returncode}\n{r.stdout}\n{r.stderr[-2000:]}"
+    out = json.loads(lines[-1])
+    _record(case, out)
+    assert out["outputs_bit_identical"], case
+    assert out["slow_paths"] == 0, f"{case}: {out['slow_paths']} gradient-phase waits timed out"
+    assert out["step_started_inside"], f"{case}: the step did not start while the other kernel ran: {out}"
+    if case in ("light", "heavy_waves"):  # the step's workgroups fit beside the occupier
+        assert out["step_ended_inside"], f"{case}: the step did not finish beside the occupier: {out}"
 
 
 def test_reference_outputs_match_oracle(cuda, oracle, step):

@@ -639,8 +639,9 @@ def tune_occupy(dev: torch.device, blocks: int, threads: int, lds_bytes: int, us
 def tune_clock_stamp(out) -> None:
     """Internal (tests): a one-thread kernel on the current stream writes the
     GPU real-time clock (s_memrealtime, 100 MHz ticks) to the int64 device
-    scalar `out`."""
-    dev = out.device
+    scalar `out`, or to pinned host memory (a store the host can poll; the
+    current device's kernel)."""
+    dev = out.device if out.is_cuda else torch.device("cuda", torch.cuda.current_device())
     with torch.cuda.device(dev):
         _check(load_library().pcm_tune_clock_stamp(_ptr(out), _stream(dev)), "pcm_tune_clock_stamp")
 

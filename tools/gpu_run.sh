@@ -25,6 +25,7 @@
 #   abr        tools/ab_ref_call.py (the unchanged caller's pieces: forward geometries, strided backward)
 #   abl        tools/ab_launch_form.py (N=1 region: direct C loop against the warmed 20-step graph)
 #   gfc        tools/grid_first_call.py in fresh processes (+ a per-call kernel trace)
+#   gfc2       12 fresh processes under rocprofv3 --kernel-trace, fp32-first and fp16-first orders
 #   tct        rocprofv3 kernel traces of tools/training_call_trace.py {after,before,reference}
 set -o pipefail
 TAG=$1
@@ -83,6 +84,11 @@ for S in "$@"; do
          (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$O/gfc_kt" -o run \
              --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/grid_first_call.py" f32,f32,f32,f16,f16 \
              > "$GRAFT_REPO_ROOT/$O/gfc_kt.log" 2>&1) ;;
+    gfc2) for r in 1 2 3 4 5 6; do for o in f32,f32,f16,f16 f16,f16,f32,f32; do
+             (cd /tmp && timeout -k 10 120 rocprofv3 --kernel-trace -d "$GRAFT_REPO_ROOT/$O/gfc2/${o}_$r" -o run \
+                 --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/grid_first_call.py" $o \
+                 > "$GRAFT_REPO_ROOT/$O/gfc2_${o}_$r.log" 2>&1) || exit 1
+         done; done ;;
     abl) timeout -k 10 300 python -u tools/ab_launch_form.py 10 > "$O/ab_launch_form.txt" 2>&1 ;;
     tct) for f in after before reference; do
              (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/tct_$f" -o run \

@@ -1423,20 +1423,15 @@ struct PcmRescale {
     float inv1 = 0.f, inv2 = 0.f; // fl(1 / (b n)), fl(1 / (b m))
 };
 
-__global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
-    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
-    const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
-    const int32_t *__restrict__ idx2, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
-    int lay1, int lay2, PcmGdStr GS, PcmRescale RS) {
+// One 256-target block (task) of the slot backward; every thread of the
+// workgroup takes part (the caller's loop may run several tasks in a row).
+__device__ __forceinline__ void slots_task(int task, int ntasks, const float *__restrict__ xyz1,
+                                           const float *__restrict__ xyz2, int n, int m,
+                                           const float *__restrict__ gd1, const float *__restrict__ gd2,
+                                           const int32_t *__restrict__ idx1, const int32_t *__restrict__ idx2,
+                                           float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
+                                           int lay1, int lay2, PcmGdStr GS, bool rescale, float rs1, float rs2) {
     constexpr int NT = kBwdSlotsT;
-    float rs1 = 0.f, rs2 = 0.f;  // rescale mode: the two scalar graddists
-    if (RS.gl) {
-        const float gl = *RS.gl;
-        if (RS.next && blockIdx.x == 0 && threadIdx.x == 0) *RS.next = gl;
-        if (RS.used && __float_as_uint(*RS.used) == __float_as_uint(gl)) return;  // the step's gradient stands
-        rs1 = __fmul_rn(gl, RS.inv1);
-        rs2 = __fmul_rn(gl, RS.inv2);
-    }
     __shared__ __attribute__((aligned(16))) float sO[3 * kBwdSlotsMax];  // other cloud, its layout
     __shared__ __attribute__((aligned(16))) float sG[kBwdSlotsMax];      // other graddist
     __shared__ __attribute__((aligned(16))) int sK[kBwdSlotsMax];        // other argmins
@@ -1446,14 +1441,14 @@ __global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
     const int wave = tid >> 6;
     int batch, blk;
     bool first;
-    pcm_split_bm(pcm_xcd_remap((int)blockIdx.x, (int)gridDim.x), nblk1, nblk2, batch, first, blk);
+    pcm_split_bm(pcm_xcd_remap(task, ntasks), nblk1, nblk2, batch, first, blk);
     const int ns = first ? n : m, no = first ? m : n;
     const float rs_self = first ? rs1 : rs2, rs_other = first ? rs2 : rs1;
     const float *self = first ? xyz1 + (size_t)batch * n * 3 : xyz2 + (size_t)batch * m * 3;
     const float *other = first ? xyz2 + (size_t)batch * m * 3 : xyz1 + (size_t)batch * n * 3;
     const int gbs = first ? (GS.bs1 < 0 ? n : GS.bs1) : (GS.bs2 < 0 ? m : GS.bs2);
     const int gbo = first ? (GS.bs2 < 0 ? m : GS.bs2) : (GS.bs1 < 0 ? n : GS.bs1);
-    const int gps = RS.gl ? 0 : (first ? GS.ps1 : GS.ps2), gpo = RS.gl ? 0 : (first ? GS.ps2 : GS.ps1);
+    const int gps = rescale ? 0 : (first ? GS.ps1 : GS.ps2), gpo = rescale ? 0 : (first ? GS.ps2 : GS.ps1);
     const float *gds = (first ? gd1 : gd2) + (size_t)batch * gbs;  // (not read in rescale mode)
     const float *gdo = (first ? gd2 : gd1) + (size_t)batch * gbo;
     const int32_t *ids = (first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m);
@@ -1469,7 +1464,7 @@ __global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
     // graddists of the other cloud: by LDS-DMA when contiguous, one register
     // when an expanded scalar (stride 0), else strided loads
     float hconst = 0.f;
-    if (RS.gl)
+    if (rescale)
         hconst = __fmul_rn(rs_other, 2.f);
     else if (gpo == 1)
         pcm_dma_to_lds(sG, gdo, 4 * no, wave, NT / 64);
@@ -1486,7 +1481,7 @@ __global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
         sy = self[pcm_at(LS, i, 1)];
         sz = self[pcm_at(LS, i, 2)];
         kself = ids[i];
-        gself = RS.gl ? rs_self : gds[(size_t)i * gps];
+        gself = rescale ? rs_self : gds[(size_t)i * gps];
     }
     cnt[tid] = 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1500,7 +1495,7 @@ __global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
         }
     }
     __syncthreads();
-    if (!own) return;
+    if (!own) return;  // (no barrier follows inside the task)
     const float g = __fmul_rn(gself, 2.f);
     const float d0 = __fmul_rn(g, __fsub_rn(sx, sO[pcm_at(LO, kself, 0)]));
     const float d1 = __fmul_rn(g, __fsub_rn(sy, sO[pcm_at(LO, kself, 1)]));
@@ -1538,6 +1533,33 @@ __global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
     grad[pcm_at(LS, i, 0)] = ax;
     grad[pcm_at(LS, i, 1)] = ay;
     grad[pcm_at(LS, i, 2)] = az;
+}
+
+// Rescale mode (RS.gl): a small grid whose workgroups loop over the tasks --
+// almost always it only confirms the scale and leaves, and the rare recompute
+// (a loop's first step, a changed weight) can afford fewer workgroups.
+constexpr int kRescaleGrid = 32;
+
+__global__ __launch_bounds__(kBwdSlotsT) void chamfer_bwd_slots_kernel(
+    const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m,
+    const float *__restrict__ gd1, const float *__restrict__ gd2, const int32_t *__restrict__ idx1,
+    const int32_t *__restrict__ idx2, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
+    int lay1, int lay2, PcmGdStr GS, PcmRescale RS) {
+    const int ntasks = b * (nblk1 + nblk2);
+    if (RS.gl) {
+        const float gl = *RS.gl;
+        if (RS.next && blockIdx.x == 0 && threadIdx.x == 0) *RS.next = gl;
+        if (RS.used && __float_as_uint(*RS.used) == __float_as_uint(gl)) return;  // the step's gradient stands
+        const float rs1 = __fmul_rn(gl, RS.inv1), rs2 = __fmul_rn(gl, RS.inv2);
+        for (int t = (int)blockIdx.x; t < ntasks; t += (int)gridDim.x) {
+            slots_task(t, ntasks, xyz1, xyz2, n, m, gd1, gd2, idx1, idx2, grad1, grad2, nblk1, nblk2, lay1, lay2, GS,
+                       true, rs1, rs2);
+            __syncthreads();  // the next task reuses the LDS
+        }
+        return;
+    }
+    slots_task((int)blockIdx.x, ntasks, xyz1, xyz2, n, m, gd1, gd2, idx1, idx2, grad1, grad2, nblk1, nblk2, lay1,
+               lay2, GS, false, 0.f, 0.f);
 }
 
 // Gradients of L = w1 sum(dist1) + w2 sum(dist2) for the targets
@@ -2276,7 +2298,8 @@ extern "C" int pcm_chamfer_loss_grad_rescale(const float *xyz1, const float *xyz
     RS.next = scale_next;
     RS.inv1 = w1;
     RS.inv2 = w2;
-    hipLaunchKernelGGL(chamfer_bwd_slots_kernel, dim3((unsigned)blocks), dim3(kBwdSlotsT), 0, (hipStream_t)stream,
+    const unsigned grid = (unsigned)(blocks < kRescaleGrid ? blocks : kRescaleGrid);
+    hipLaunchKernelGGL(chamfer_bwd_slots_kernel, dim3(grid), dim3(kBwdSlotsT), 0, (hipStream_t)stream,
                        xyz1, xyz2, b, n, m, nullptr, nullptr, idx1, idx2, gradxyz1, gradxyz2, nblk1, nblk2, layout1,
                        layout2, PcmGdStr(), RS);
     return pcm_launch_status();

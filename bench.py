@@ -12,13 +12,13 @@ gradient torch's mean feeds it).  Inputs are resident in HBM before timing.
 The step runs as ONE launch of pcm_chamfer_loss_grad (forward, loss and both
 clouds' gradients; csrc/chamfer_filt.hip); --two-launch runs it as the fused-
 loss forward + the backward kernel instead (both are reported).
-At N=1 the timed region launches the step directly through the C ABI, once
-per step, from a C loop with the arguments bound once (a native training
-loop's calls; the host stays ahead of the ~14 us kernel, so the GPU runs the
-steps back to back).  tools/probe_replay.py measured the alternatives on MI355X: a replay of
-a 20-step hipGraph adds ~0.8 us per kernel node and ~16 us of replay floor,
-the Python wrapper per step ~0.5 us (r05c).  --graph times the 20-step graph
-instead (its first replay paid in warmup); --eager the Python wrapper.  The
+The timed region replays a captured 20-step hipGraph of the step (the first
+replay paid in warmup), at N=1 and at N>1 alike: N>1 only adds each step's
+loss all-reduce to the same graph, so a 1->N curve isolates the collective.
+Round 6's matched A/B against K direct launches from one C call
+(pcm_chamfer_loss_grad_steps, --c-loop) gave 15.71 against 15.82 us per step
+at the driver's K = 20 (tools/ab_launch_form.py,
+profiles/r06/ab_launch_form_r06c.txt); --eager times the Python wrapper.  The
 GPU-side time of the timed region (HIP events at its edges, on the kernel's
 stream) is the dominant kernel's duration in `roofline`.
 Order: the headline's W warmup steps and K timed steps first, then the legs
@@ -105,7 +105,10 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--eager", action="store_true", help="no hipGraph capture (Python wrapper per step)")
     p.add_argument("--graph", action="store_true",
-                   help="N=1: time replays of the captured 20-step hipGraph instead of direct C-ABI launches")
+                   help="(the default form; kept for old command lines)")
+    p.add_argument("--c-loop", action="store_true",
+                   help="N=1: time K direct launches from one C call (pcm_chamfer_loss_grad_steps) instead of "
+                        "replays of the captured 20-step hipGraph (matched A/B: profiles/r06/ab_launch_form_r06c.txt)")
     p.add_argument("--two-launch", action="store_true",
                    help="step = fused-loss forward + backward kernel (not the one-launch loss+gradient)")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
@@ -879,24 +882,25 @@ def main(argv=None):
         g_one = capture_steps(step, 1, dev, world, False)
         g_many = None
         if not multi:
-            # `per` consecutive steps per hipGraph replay (reported beside the
-            # headline; the default N=1 timed region launches directly)
+            # `per` consecutive steps per hipGraph replay: the same form as at
+            # N > 1 minus the per-step collective (round 6: the matched A/B of
+            # this against K direct launches from a C loop gave 15.71 against
+            # 15.82 us per step at K = 20, profiles/r06/ab_launch_form_r06c.txt)
             g_many = capture_steps(step, per, dev, world, False)
-            if args.graph:
+            if not args.c_loop:
                 def run_steps(k):
                     for _ in range(k // per):
                         g_many.replay()
                     for _ in range(k % per):
                         g_one.replay()
-                mode = f"hipgraph ({per} steps per graph)"
+                mode = f"hipgraph ({per} steps per graph; N>1 adds each step's all-reduce to the same graph)"
             else:
                 go = step.launcher()
 
                 def run_steps(k):
                     go(k)
                 mode = ("direct launches, one per step: a C loop over pcm_chamfer_loss_grad with its arguments "
-                        "bound once (tools/probe_replay.py: a hipGraph replay adds ~0.8 us per kernel node and a "
-                        "~16 us floor on ROCm 7; a ctypes call per step from Python is host-bound)")
+                        "bound once (pcm_chamfer_loss_grad_steps)")
         else:
             g_ar_many = g_ar_one = None
             if args.dist_backend == "nccl" and not args.eager_allreduce:
@@ -940,7 +944,7 @@ def main(argv=None):
                         step.reduce_losses(1)
                 mode = "one-step hipgraph replay + eager all-reduce of the step's loss, every step"
         side = side_legs(args, dev, rank, world) if args.side_legs == "first" else {}
-        if multi or args.graph:
+        if multi or not args.c_loop:
             g_tail = g_one if not multi else (g_ar_one if g_ar_many is not None else None)
             graph_info = warm_graphs(g_many, g_tail, per, args.warmup, args.steps, run_steps, dev, world)
         else:
@@ -981,7 +985,7 @@ def main(argv=None):
     if step.fused:
         dom_kernel, dom_bytes = FUSED_KERNEL, FUSED_BYTES
         graph_kernel_us = kernel_avg_us(lambda: step(0), 200, dev)
-        dom_us = region_us if not (args.eager or args.graph or multi) else graph_kernel_us
+        dom_us = region_us if not (args.eager or multi) else graph_kernel_us
     else:
         dom_kernel, dom_bytes, dom_us = FWD_KERNEL, FWD_BYTES, fwd_us
         graph_kernel_us = fwd_us

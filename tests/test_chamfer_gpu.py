@@ -792,8 +792,12 @@ def test_wrapper_reports_and_resets_sticky_error(cuda, oracle):
     pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2)  # sticky: NaN
     torch.cuda.synchronize()
     assert torch.isnan(means).all()
+    # the watch copies the words after every `every`-th call: reported within every * (depth + 1) calls
+    bound = pcm_hip._StickyWatch.every * (pcm_hip._StickyWatch.depth + 1) + 1
     with pytest.raises(pcm_hip.PcmError):
-        pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2)
+        for _ in range(bound):
+            pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2)
+            torch.cuda.synchronize()
     pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, means, gx1, gx2)
     torch.cuda.synchronize()
     ref = oracle.chamfer_forward(a.numpy(), c.numpy())

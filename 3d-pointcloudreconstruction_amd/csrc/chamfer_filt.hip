@@ -201,10 +201,7 @@ __device__ __forceinline__ void filt_group4(float (&mn)[4], const pcm_f2 (&px)[4
 // first part overlaps the rest of the prologue's load burst.  Chunks are
 // visited in the same order (c = wave, wave + W, ...), so results are
 // identical.
-// kTieB: near-tie rescans of a resident cloud take up to kTieB steps of 64
-// candidates per batch, every batch's LDS reads issued before its distances
-// (1: one step at a time, each read waited before the next is issued)
-template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1, bool kSplit = false, int kTieB = 1>
+template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1, bool kSplit = false>
 __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const TIn *__restrict__ T, int nq, int nt, int qbase,
                               float *__restrict__ D, int32_t *__restrict__ I, unsigned char *arena,
                               unsigned long long *__restrict__ Gr = nullptr, unsigned long long tag = 0,
@@ -593,31 +590,21 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                     }
                     if (nch - c0 < 64) M &= (1ull << (nch - c0)) - 1ull;
                     while (M) {
-                        // kTieB steps of kCps chunks: the chunk ids (wave-uniform
-                        // bit scans), then every step's read, then the distances
-                        int cs[kTieB], ks[kTieB];
-                        pcm_f4 t4[kTieB];
+                        int ch[kCps];
 #pragma unroll
-                        for (int t = 0; t < kTieB; ++t) {
-                            int ch[kCps];
-#pragma unroll
-                            for (int j = 0; j < kCps; ++j) {
-                                ch[j] = M ? c0 + __builtin_ctzll(M) : -1;
-                                M &= M - 1ull;
-                            }
-                            int c = ch[0];
-#pragma unroll
-                            for (int j = 1; j < kCps; ++j)
-                                if (lane / C == j) c = ch[j];
-                            cs[t] = c;
-                            ks[t] = c * C + (lane & (C - 1));
-                            t4[t] = sT[slot(min(max(ks[t], 0), nt - 1))];
+                        for (int j = 0; j < kCps; ++j) {
+                            ch[j] = M ? c0 + __builtin_ctzll(M) : -1;
+                            M &= M - 1ull;
                         }
+                        int c = ch[0];
 #pragma unroll
-                        for (int t = 0; t < kTieB; ++t) {  // ascending k within a lane: strict lexmin keeps the lowest
-                            const float d = pcm_sqd(t4[t].x - x, t4[t].y - y, t4[t].z - z);
-                            if (cs[t] >= 0 && ks[t] < nt) pcm_lexmin(bd, bk, d, ks[t]);
-                        }
+                        for (int j = 1; j < kCps; ++j)
+                            if (lane / C == j) c = ch[j];
+                        const int k = c * C + (lane & (C - 1));
+                        const int sk = slot(min(max(k, 0), nt - 1));
+                        const pcm_f4 t4 = sT[sk];
+                        const float d = pcm_sqd(t4.x - x, t4.y - y, t4.z - z);
+                        if (c >= 0 && k < nt) pcm_lexmin(bd, bk, d, k);
                     }
                 }
                 pcm_wave_lexmin(bd, bk);
@@ -2003,8 +1990,7 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
 // torch's mean backward forms it, and mean_out[3] records the scale used
 // (pcm_chamfer_loss_grad_rescale checks it against the real one).
 template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false,
-          bool kLocal = false, bool kSplit = false, bool kG4 = false, bool kG4x = false, int LAY1 = 0, int LAY2 = 0,
-          int kTieB = 1>
+          bool kLocal = false, bool kSplit = false, bool kG4 = false, bool kG4x = false, int LAY1 = 0, int LAY2 = 0>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -2084,7 +2070,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         float my_d;
         if constexpr (LAY1 == LAY2) {
             const PcmLay LQ = LAY1 ? PcmLay{1, first ? n : m} : PcmLay{3, 1};
-            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit, kTieB>(
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
                 first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
                 first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, kG4 ? nullptr : (first ? G1 : G2),
@@ -2092,11 +2078,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
                 LAY1 ? PcmLay{1, first ? m : n} : PcmLay{3, 1}, kG4 ? (first ? H1 : H2) : nullptr, tag4,
                 kG4 ? &myk : nullptr, g4x);
         } else if (first) {  // mixed layouts: each direction's strides known at compile time
-            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit, kTieB>(
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 X1, X2, n, m, q0, dist1 + (size_t)batch * n, idx1 + (size_t)batch * n, arena, nullptr, tag, nullptr,
                 sQown, L1, L2, H1, tag4, &myk, g4x);
         } else {
-            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit, kTieB>(
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 X2, X1, m, n, q0, dist2 + (size_t)batch * m, idx2 + (size_t)batch * m, arena, nullptr, tag, nullptr,
                 sQown, L2, L1, H2, tag4, &myk, g4x);
         }
@@ -2344,7 +2330,6 @@ struct GradVariant {
 // per launch against 3.65 MB
 constexpr int kDefaultGradVariant = 15;
 #define PCM_GRAD_DEFAULT(L1, L2) chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true, L1, L2>
-#define PCM_GRAD_V16 chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true, 0, 0, 4>
 // The product library holds the default only; the measured alternatives are
 // compiled into the tuning build (make tune: -DPCM_TUNE, libpcm_hip_tune.so),
 // which tools/ and the variant tests load.
@@ -2375,16 +2360,11 @@ const GradVariant kGradVariants[] = {
 #endif
     // 15: 14 with four granules per 16-byte write-through store (a quarter of the fabric writes)
     {kDefaultGradVariant, PCM_GRAD_DEFAULT(0, 0), 8, 4},
-#ifdef PCM_TUNE
-    // 16: 15 with the near-tie rescans' LDS reads issued four steps at a time
-    {16, PCM_GRAD_V16, 8, 4},
-#endif
 };
 // the default variant with cloud 1 / cloud 2 in channel planes (index 2 lay1 + lay2)
 const grad_kernel_t kGradDefaultLay[4] = {PCM_GRAD_DEFAULT(0, 0), PCM_GRAD_DEFAULT(0, 1), PCM_GRAD_DEFAULT(1, 0),
                                           PCM_GRAD_DEFAULT(1, 1)};
 #undef PCM_GRAD_DEFAULT
-#undef PCM_GRAD_V16
 // (round 5, rejected: 15 with two queries per lane -- 128-query workgroups,
 // two per CU, four waves per SIMD -- 15.45 us against 13.39 us,
 // profiles/r05/ab_qpt2_r05t.txt)
@@ -2438,7 +2418,7 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
     if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
     if ((unsigned)lay1 > 1u || (unsigned)lay2 > 1u) return PCM_ERR_INVALID_ARG;
     const GradVariant *v = find_grad_variant(variant);
-    if (!v) return variant >= 0 && variant <= 16 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // tuning build
+    if (!v) return variant >= 0 && variant <= 15 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // 0-14: tuning build
     if ((lay1 | lay2) && variant != kDefaultGradVariant) return PCM_ERR_UNSUPPORTED;
     if (!xyz1 || !xyz2 || !dist1 || !dist2 || !idx1 || !idx2 || !mean_out || !grad1 || !grad2 || !workspace)
         return PCM_ERR_INVALID_ARG;

@@ -51,8 +51,8 @@ for S in "$@"; do
     rocprof) (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" \
                -o run --output-format csv -- python3 "$GRAFT_REPO_ROOT/bench.py" --gpus 1 --steps 20 --warmup 5 --no-cpu > "$GRAFT_REPO_ROOT/$O/rocprof_bench.json" \
                2> "$GRAFT_REPO_ROOT/$O/rocprof.err") ;;
-    abc) AB_VARIANTS=${AB_VARIANTS:-15,16} timeout -k 10 600 python -u tools/ab_chamfer.py > "$O/ab_chamfer.txt" 2>&1 &&
-         AB_VARIANTS=${AB_VARIANTS:-15,16} timeout -k 10 600 python -u tools/ab_chamfer.py >> "$O/ab_chamfer.txt" 2>&1 ;;
+    abc) AB_VARIANTS=${AB_VARIANTS:-11,15} timeout -k 10 600 python -u tools/ab_chamfer.py > "$O/ab_chamfer.txt" 2>&1 &&
+         AB_VARIANTS=${AB_VARIANTS:-11,15} timeout -k 10 600 python -u tools/ab_chamfer.py >> "$O/ab_chamfer.txt" 2>&1 ;;
     abe) timeout -k 10 600 python -u tools/ab_emd.py > "$O/ab_emd.txt" 2>&1 ;;
     grid) timeout -k 10 600 python -u -m pytest tests/test_chamfer_grid_gpu.py -m gpu -x -q --timeout 120 \
                --timeout-method thread > "$O/pytest_grid.txt" 2>&1 &&

@@ -447,13 +447,13 @@ class _StickyWatch:
     instead of silently persisting.  No copy is ever dropped: a host that
     runs ahead of the GPU fills the ring, and a full ring waits for its
     oldest copy, which bounds the calls between a timeout and its report.
-    The words are copied after every `every`-th call only (each copy is a
+    The words are copied after the first and then every `every`-th call (a copy is a
     kernel on the stream: two per call had cost ~9 us of GPU time per step
     of a ~17 us training call), so a timeout is reported within
     every * (depth + 1) calls; its NaN means are visible at once anyway."""
 
     depth = 4
-    every = 16
+    every = 32
 
     def __init__(self, ws, b, n, m):
         L = load_library()

@@ -1990,7 +1990,8 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
 // torch's mean backward forms it, and mean_out[3] records the scale used
 // (pcm_chamfer_loss_grad_rescale checks it against the real one).
 template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false,
-          bool kLocal = false, bool kSplit = false, bool kG4 = false, bool kG4x = false, int LAY1 = 0, int LAY2 = 0>
+          bool kLocal = false, bool kSplit = false, bool kG4 = false, bool kG4x = false, int LAY1 = 0, int LAY2 = 0,
+          bool kLayOne = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -2077,6 +2078,12 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
                 tag, kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, LQ,
                 LAY1 ? PcmLay{1, first ? m : n} : PcmLay{3, 1}, kG4 ? (first ? H1 : H2) : nullptr, tag4,
                 kG4 ? &myk : nullptr, g4x);
+        } else if (kLayOne) {  // mixed layouts, one inlined forward with the strides in registers (tuning A/B)
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
+                first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
+                first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
+                first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, nullptr, tag, nullptr, sQown,
+                first ? L1 : L2, first ? L2 : L1, first ? H1 : H2, tag4, &myk, g4x);
         } else if (first) {  // mixed layouts: each direction's strides known at compile time
             my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 X1, X2, n, m, q0, dist1 + (size_t)batch * n, idx1 + (size_t)batch * n, arena, nullptr, tag, nullptr,
@@ -2364,6 +2371,14 @@ const GradVariant kGradVariants[] = {
 // the default variant with cloud 1 / cloud 2 in channel planes (index 2 lay1 + lay2)
 const grad_kernel_t kGradDefaultLay[4] = {PCM_GRAD_DEFAULT(0, 0), PCM_GRAD_DEFAULT(0, 1), PCM_GRAD_DEFAULT(1, 0),
                                           PCM_GRAD_DEFAULT(1, 1)};
+#ifdef PCM_TUNE
+// the mixed-layout instances with one inlined forward (strides in registers)
+const grad_kernel_t kGradLayOne[4] = {
+    PCM_GRAD_DEFAULT(0, 0),
+    chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true, 0, 1, true>,
+    chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true, 1, 0, true>,
+    PCM_GRAD_DEFAULT(1, 1)};
+#endif
 #undef PCM_GRAD_DEFAULT
 // (round 5, rejected: 15 with two queries per lane -- 128-query workgroups,
 // two per CU, four waves per SIMD -- 15.45 us against 13.39 us,
@@ -2413,7 +2428,7 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
                      float *dist1, float *dist2, int32_t *idx1, int32_t *idx2, float *mean_out, float *grad1,
                      float *grad2, void *workspace, size_t workspace_bytes, void *stream,
                      unsigned max_spins = kGradWaitSpins, unsigned poll_spins = pcm_loss::kPollMaxSpins,
-                     int lay1 = 0, int lay2 = 0, const float *gscale = nullptr) {
+                     int lay1 = 0, int lay2 = 0, const float *gscale = nullptr, int lay_form = 0) {
     if (b <= 0 || n <= 0 || m <= 0) return PCM_ERR_INVALID_ARG;
     if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
     if ((unsigned)lay1 > 1u || (unsigned)lay2 > 1u) return PCM_ERR_INVALID_ARG;
@@ -2429,7 +2444,12 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
     if (workspace_bytes < off + grad_ws_bytes(b, grad_blocks_max(b, n, m), (long long)b * (n + m)))
         return PCM_ERR_WORKSPACE;
     const GradWs ws = grad_ws((char *)workspace + off, b, blocks);
-    const grad_kernel_t k = variant == kDefaultGradVariant ? kGradDefaultLay[2 * lay1 + lay2] : v->k;
+    grad_kernel_t k = variant == kDefaultGradVariant ? kGradDefaultLay[2 * lay1 + lay2] : v->k;
+#ifdef PCM_TUNE
+    if (lay_form == 1 && variant == kDefaultGradVariant) k = kGradLayOne[2 * lay1 + lay2];
+#else
+    if (lay_form != 0) return PCM_ERR_UNSUPPORTED;
+#endif
     // + the polling workgroup (the grid's last)
     hipLaunchKernelGGL(k, dim3((unsigned)blocks + 1), dim3(64 * v->waves), 0, (hipStream_t)stream, xyz1, xyz2, b,
                        n, m, w1, w2, dist1, dist2, idx1, idx2, mean_out, grad1, grad2, nblk1, nblk2, ws, max_spins,
@@ -2461,6 +2481,19 @@ extern "C" int pcm_chamfer_loss_grad_layout(const float *xyz1, const float *xyz2
     return launch_loss_grad(default_grad_variant(b, n, m), xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2,
                             mean_out, gradxyz1, gradxyz2, workspace, workspace_bytes, stream, kGradWaitSpins,
                             pcm_loss::kPollMaxSpins, layout1, layout2, grad_scale);
+}
+
+// the layout entry with a chosen form of the mixed-layout instances (0: the
+// product's two inlined forwards, 1: one forward with runtime strides; the
+// tuning build only): tools/ab_layout_forms.py
+extern "C" int pcm_tune_chamfer_loss_grad_layout(int form, const float *xyz1, const float *xyz2, int b, int n, int m,
+                                                 int layout1, int layout2, float w1, float w2,
+                                                 const float *grad_scale, float *dist1, float *dist2, int32_t *idx1,
+                                                 int32_t *idx2, float *mean_out, float *gradxyz1, float *gradxyz2,
+                                                 void *workspace, size_t workspace_bytes, void *stream) {
+    return launch_loss_grad(default_grad_variant(b, n, m), xyz1, xyz2, b, n, m, w1, w2, dist1, dist2, idx1, idx2,
+                            mean_out, gradxyz1, gradxyz2, workspace, workspace_bytes, stream, kGradWaitSpins,
+                            pcm_loss::kPollMaxSpins, layout1, layout2, grad_scale, form);
 }
 
 // `steps` back-to-back launches of the default step from one host call, its

@@ -23,6 +23,7 @@
 #   abcl       tools/ab_chamfer.sh (the A/B across lib/libpcm_hip_{base,v*}.so builds, twice)
 #   emddiag    tools/emd_diag.py: config 3 per iteration, the training call by bidder count
 #   abr        tools/ab_ref_call.py (the unchanged caller's pieces: forward geometries, strided backward)
+#   abf        tools/ab_layout_forms.py (the training call's mixed-layout step: two forwards vs one), twice
 #   abl        tools/ab_launch_form.py (N=1 region: direct C loop against the warmed 20-step graph)
 #   gfc        tools/grid_first_call.py in fresh processes (+ a per-call kernel trace)
 #   gfc2       12 fresh processes under rocprofv3 --kernel-trace, fp32-first and fp16-first orders
@@ -89,6 +90,8 @@ for S in "$@"; do
                  --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/grid_first_call.py" $o \
                  > "$GRAFT_REPO_ROOT/$O/gfc2_${o}_$r.log" 2>&1) || exit 1
          done; done ;;
+    abf) timeout -k 10 300 python -u tools/ab_layout_forms.py > "$O/ab_layout_forms.txt" 2>&1 &&
+         timeout -k 10 300 python -u tools/ab_layout_forms.py >> "$O/ab_layout_forms.txt" 2>&1 ;;
     abl) timeout -k 10 300 python -u tools/ab_launch_form.py 10 > "$O/ab_launch_form.txt" 2>&1 ;;
     tct) for f in after before reference; do
              (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/tct_$f" -o run \

@@ -498,6 +498,9 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
             const float rq = 2.f * sq + __builtin_amdgcn_sqrtf(db);
             const float e2 = 2.f * kFiltU16 * __builtin_fminf(rr * rr, rq * rq) * 1.001f;
             proven = (fs - fb) > e2;  // false for NaN
+#ifdef PCM_PROBE_NO_TIES
+            proven = true;  // timing probe only (make variant V=noties): no near-tie pass, results may differ
+#endif
             float hd = PCM_INF;
             int hk = 0x7fffffff;
             if (qbase + s < nq) {

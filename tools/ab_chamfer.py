@@ -49,7 +49,7 @@ def main():
     for _ in range(rounds):
         for v in vs:
             res[v].append(time_graph_us(graphs[v], reps))
-    lib = os.path.basename(os.environ.get("PCM_HIP_LIB", "libpcm_hip.so"))
+    lib = os.path.basename(os.environ.get("PCM_HIP_TUNE_LIB", "libpcm_hip_tune.so"))
     print(lib + ": " + ", ".join(f"v{v} {statistics.median(res[v]):.2f} us (min {min(res[v]):.2f}, same={same[v]})"
                                  for v in vs), flush=True)
 

@@ -1,8 +1,8 @@
 # same-box A/B of the one-launch Chamfer step across builds (tools/ab_chamfer.py)
 L=$PWD/3d-pointcloudreconstruction_amd/lib
 for r in 1 2; do
-  for lib in $L/libpcm_hip_base.so $L/libpcm_hip_v*.so $L/libpcm_hip.so; do
+  for lib in $L/libpcm_hip_base.so $L/libpcm_hip_v*.so $L/libpcm_hip_tune.so; do
     [ -f "$lib" ] || continue
-    PCM_HIP_LIB=$lib timeout -k 10 120 python -u tools/ab_chamfer.py || exit 1
+    PCM_HIP_LIB=$lib PCM_HIP_TUNE_LIB=$lib timeout -k 10 120 python -u tools/ab_chamfer.py || exit 1
   done
 done

@@ -62,8 +62,9 @@ for S in "$@"; do
     gridkt) timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/gridkt" -o grid --output-format csv \
                -- python3 tools/grid_diag.py > "$O/gridkt.log" 2>&1 ;;
     pmc) timeout -k 10 900 bash tools/pmc_passes.sh "$O/pmc" > "$O/pmc_passes.log" 2>&1 ;;
-    stamps) PCM_HIP_LIB=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_stamps.so timeout -k 10 300 \
-               python -u tools/stamp_filt.py fused 15 11 > "$O/stamps_fused.txt" 2>&1 ;;
+    stamps) PCM_HIP_LIB=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_stamps.so \
+            PCM_HIP_TUNE_LIB=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_stamps.so timeout -k 10 300 \
+               python -u tools/stamp_filt.py fused 15 > "$O/stamps_fused.txt" 2>&1 ;;
     stampslg) timeout -k 10 300 python -u tools/stamp_lgrid.py 13 > "$O/stamps_lgrid.txt" 2>&1 &&
               timeout -k 10 300 python -u tools/stamp_lgrid.py 11 >> "$O/stamps_lgrid.txt" 2>&1 ;;
     probe) timeout -k 10 300 python -u tools/probe_replay.py > "$O/probe_replay.txt" 2>&1 &&

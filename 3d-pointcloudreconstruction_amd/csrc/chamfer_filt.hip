@@ -201,11 +201,7 @@ __device__ __forceinline__ void filt_group4(float (&mn)[4], const pcm_f2 (&px)[4
 // first part overlaps the rest of the prologue's load burst.  Chunks are
 // visited in the same order (c = wave, wave + W, ...), so results are
 // identical.
-// kTieSplit: with at most kTB near-tie queries in a resident cloud, every
-// wave takes a share of each query's named chunks (a quarter-wave step of
-// 64 candidates each, round-robin), then one merge -- instead of one wave per
-// query while the others wait at the output barrier
-template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1, bool kSplit = false, bool kTieSplit = false>
+template <typename TIn, int W, int QPT, int C, int TILE, bool kSc1, bool kSplit = false>
 __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const TIn *__restrict__ T, int nq, int nt, int qbase,
                               float *__restrict__ D, int32_t *__restrict__ I, unsigned char *arena,
                               unsigned long long *__restrict__ Gr = nullptr, unsigned long long tag = 0,
@@ -572,8 +568,7 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
 #pragma unroll
             for (int i = 0; i < 64; i += W) wpat |= 1ull << i;
             const int nch = (nt + C - 1) / C;
-            const bool split = kTieSplit && nl <= kTB && nch <= 64;  // workgroup-uniform
-            for (int e = split ? nl : wave; e < nl; e += W) {
+            for (int e = wave; e < nl; e += W) {
                 const int s = __builtin_amdgcn_readfirstlane(sList[e]);
                 const unsigned plan = __builtin_amdgcn_readfirstlane(sPlan[s]);
                 int one[W];  // best chunk of each wave
@@ -619,65 +614,6 @@ __device__ __forceinline__ float filt_forward(const TIn *__restrict__ Q, const T
                 if (lane == 0) {
                     sD[s] = bd;
                     sK[s] = bk;
-                }
-            }
-            if constexpr (kTieSplit) {
-                if (split && nl > 0) {
-                    for (int e = 0; e < nl; ++e) {
-                        const int s = __builtin_amdgcn_readfirstlane(sList[e]);
-                        const unsigned plan = __builtin_amdgcn_readfirstlane(sPlan[s]);
-                        unsigned long long M = 0;
-#pragma unroll
-                        for (int w = 0; w < W; ++w) {
-                            if ((plan >> (W + w)) & 1u) M |= wpat << w;
-                            else if ((plan >> w) & 1u) M |= 1ull << __builtin_amdgcn_readfirstlane(sChunk[w][s]);
-                        }
-                        if (nch < 64) M &= (1ull << nch) - 1ull;
-                        float x = rx[0], y = ry[0], z = rz[0];
-#pragma unroll
-                        for (int qq = 1; qq < QPT; ++qq)
-                            if ((s >> 6) == qq) { x = rx[qq]; y = ry[qq]; z = rz[qq]; }
-                        x = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), s & 63));
-                        y = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y), s & 63));
-                        z = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(z), s & 63));
-                        float bd = PCM_INF;
-                        int bk = 0x7fffffff;
-                        // this wave's steps: t = wave, wave + W, ...; step t holds the
-                        // named chunks kCps t .. kCps t + kCps - 1 (in bit order)
-                        for (int i = 0; i < kCps * wave && M; ++i) M &= M - 1ull;
-                        while (M) {
-                            int ch[kCps];
-#pragma unroll
-                            for (int j = 0; j < kCps; ++j) {
-                                ch[j] = M ? __builtin_ctzll(M) : -1;
-                                M &= M - 1ull;
-                            }
-                            int c = ch[0];
-#pragma unroll
-                            for (int j = 1; j < kCps; ++j)
-                                if (lane / C == j) c = ch[j];
-                            const int k = c * C + (lane & (C - 1));
-                            const pcm_f4 t4 = sT[slot(min(max(k, 0), nt - 1))];
-                            const float d = pcm_sqd(t4.x - x, t4.y - y, t4.z - z);
-                            if (c >= 0 && k < nt) pcm_lexmin(bd, bk, d, k);
-                            for (int i = 0; i < kCps * (W - 1) && M; ++i) M &= M - 1ull;
-                        }
-                        pcm_wave_lexmin(bd, bk);
-                        if (lane == 0) {
-                            sTD[e * W + wave] = bd;
-                            sTK[e * W + wave] = bk;
-                        }
-                    }
-                    __syncthreads();
-                    if (tid < nl) {
-                        float d = sTD[tid * W];
-                        int k = sTK[tid * W];
-#pragma unroll
-                        for (int w = 1; w < W; ++w) pcm_lexmin(d, k, sTD[tid * W + w], sTK[tid * W + w]);
-                        const int s = sList[tid];
-                        sD[s] = d;
-                        sK[s] = k;
-                    }
                 }
             }
             if (nl > 0) __syncthreads();
@@ -2058,7 +1994,7 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
 // (pcm_chamfer_loss_grad_rescale checks it against the real one).
 template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false,
           bool kLocal = false, bool kSplit = false, bool kG4 = false, bool kG4x = false, int LAY1 = 0, int LAY2 = 0,
-          bool kLayOne = false, bool kTieSplit = false>
+          bool kLayOne = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -2138,7 +2074,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         float my_d;
         if constexpr (LAY1 == LAY2) {
             const PcmLay LQ = LAY1 ? PcmLay{1, first ? n : m} : PcmLay{3, 1};
-            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit, kTieSplit>(
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
                 first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
                 first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, kG4 ? nullptr : (first ? G1 : G2),
@@ -2146,17 +2082,17 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
                 LAY1 ? PcmLay{1, first ? m : n} : PcmLay{3, 1}, kG4 ? (first ? H1 : H2) : nullptr, tag4,
                 kG4 ? &myk : nullptr, g4x);
         } else if (kLayOne) {  // mixed layouts, one inlined forward with the strides in registers (tuning A/B)
-            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit, kTieSplit>(
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
                 first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
                 first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, nullptr, tag, nullptr, sQown,
                 first ? L1 : L2, first ? L2 : L1, first ? H1 : H2, tag4, &myk, g4x);
         } else if (first) {  // mixed layouts: each direction's strides known at compile time
-            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit, kTieSplit>(
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 X1, X2, n, m, q0, dist1 + (size_t)batch * n, idx1 + (size_t)batch * n, arena, nullptr, tag, nullptr,
                 sQown, L1, L2, H1, tag4, &myk, g4x);
         } else {
-            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit, kTieSplit>(
+            my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 X2, X1, m, n, q0, dist2 + (size_t)batch * m, idx2 + (size_t)batch * m, arena, nullptr, tag, nullptr,
                 sQown, L2, L1, H2, tag4, &myk, g4x);
         }
@@ -2434,10 +2370,6 @@ const GradVariant kGradVariants[] = {
 #endif
     // 15: 14 with four granules per 16-byte write-through store (a quarter of the fabric writes)
     {kDefaultGradVariant, PCM_GRAD_DEFAULT(0, 0), 8, 4},
-#ifdef PCM_TUNE
-    // 16: 15 with a workgroup's (<= 4) near-tie queries rescanned by all its waves
-    {16, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true, 0, 0, false, true>, 8, 4},
-#endif
 };
 // the default variant with cloud 1 / cloud 2 in channel planes (index 2 lay1 + lay2)
 const grad_kernel_t kGradDefaultLay[4] = {PCM_GRAD_DEFAULT(0, 0), PCM_GRAD_DEFAULT(0, 1), PCM_GRAD_DEFAULT(1, 0),
@@ -2504,7 +2436,7 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
     if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
     if ((unsigned)lay1 > 1u || (unsigned)lay2 > 1u) return PCM_ERR_INVALID_ARG;
     const GradVariant *v = find_grad_variant(variant);
-    if (!v) return variant >= 0 && variant <= 16 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // tuning build
+    if (!v) return variant >= 0 && variant <= 15 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // 0-14: tuning build
     if ((lay1 | lay2) && variant != kDefaultGradVariant) return PCM_ERR_UNSUPPORTED;
     if (!xyz1 || !xyz2 || !dist1 || !dist2 || !idx1 || !idx2 || !mean_out || !grad1 || !grad2 || !workspace)
         return PCM_ERR_INVALID_ARG;

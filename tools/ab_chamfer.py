@@ -32,19 +32,22 @@ def main():
     w1, w2 = 1.0 / (b * n), 1.0 / (b * m)
     vs = list(range(7, pcm_hip.tune_num_chamfer_loss_grad_variants()))  # (loads the tuning build first)
     ws = pcm_hip.chamfer_workspace(dev, b, n, m)  # sized for every variant of the tuning build
-    if os.environ.get("AB_VARIANTS"):  # e.g. AB_VARIANTS=11,15
-        vs = [int(v) for v in os.environ["AB_VARIANTS"].split(",")]
+    if os.environ.get("AB_VARIANTS"):  # e.g. AB_VARIANTS=11,15; P = the product library's default entry
+        vs = [v if v == "P" else int(v) for v in os.environ["AB_VARIANTS"].split(",")]
     out = {}
+
+    def pv(v):
+        return None if v == "P" else v
     # a zero-filled workspace per variant: variants of different granule formats
     # sharing one would make each switch's first call recompute every argmin
     wss = {v: torch.zeros_like(ws) for v in vs}
     for v in vs:
-        pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, wss[v], variant=v)
+        pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, wss[v], variant=pv(v))
         torch.cuda.synchronize()
         out[v] = [t.clone() for t in (d1, d2, i1, i2, gx1, gx2, mo)]
     same = {v: all(torch.equal(a, r) for a, r in zip(out[v], out[vs[0]])) for v in vs}
     graphs = {v: graph_of(lambda v=v: pcm_hip.chamfer_loss_grad(x1, x2, w1, w2, d1, d2, i1, i2, mo, gx1, gx2, wss[v],
-                                                                variant=v), reps) for v in vs}
+                                                                variant=pv(v)), reps) for v in vs}
     res = {v: [] for v in vs}
     for _ in range(rounds):
         for v in vs:

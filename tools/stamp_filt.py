@@ -138,7 +138,7 @@ def run_fused(v, b, n, m, dev):
               f"max {max(dur):7.2f}  (>1 us: {sum(d > 1.0 for d in dur)} workgroups)")
 
 
-FUSED_QPT = [2, 4, 2, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4]         # csrc/chamfer_filt.hip kGradVariants
+FUSED_QPT = [2, 4, 2, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4, 4]          # csrc/chamfer_filt.hip kGradVariants
 
 
 def main():

@@ -44,7 +44,27 @@ __global__ void pcm_clock_stamp_kernel(unsigned long long *out) {
     if (threadIdx.x == 0)
         __hip_atomic_store(out, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// one wave: a dependent FMA chain between two (s_memrealtime, s_memtime)
+// pairs -- the shader clock the chain ran at is the s_memtime ticks over the
+// 100 MHz real-time ticks
+__global__ void pcm_clock_rate_kernel(unsigned long long *out, int iters) {
+    const unsigned long long r0 = __builtin_amdgcn_s_memrealtime(), c0 = __builtin_amdgcn_s_memtime();
+    float a = (float)threadIdx.x;
+    for (int i = 0; i < iters; ++i) a = __builtin_fmaf(a, 0.999f, 0.5f);
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+        out[0] = r1 - r0;
+        out[1] = c1 - c0;
+        out[2] = (unsigned long long)__float_as_uint(a);
+    }
+}
 }  // namespace
+
+extern "C" int pcm_tune_clock_rate(unsigned long long *out, int iters, void *stream) {
+    if (!out || iters <= 0) return PCM_ERR_INVALID_ARG;
+    hipLaunchKernelGGL(pcm_clock_rate_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, out, iters);
+    return pcm_launch_status();
+}
 
 extern "C" int pcm_tune_occupy_flagged(int blocks, int threads, int lds_bytes, unsigned usec,
                                        unsigned long long *stamps, unsigned *host_flag, void *stream) {

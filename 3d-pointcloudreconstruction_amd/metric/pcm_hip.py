@@ -177,6 +177,9 @@ def _open(path):
         L.pcm_tune_occupy_stamped.argtypes = [ci, ci, ci, ctypes.c_uint, vp, vp]
         L.pcm_tune_clock_stamp.restype = ci
         L.pcm_tune_clock_stamp.argtypes = [vp, vp]
+    if hasattr(L, "pcm_tune_clock_rate"):
+        L.pcm_tune_clock_rate.restype = ci
+        L.pcm_tune_clock_rate.argtypes = [vp, ci, vp]
     if hasattr(L, "pcm_tune_occupy_flagged"):
         L.pcm_tune_occupy_flagged.restype = ci
         L.pcm_tune_occupy_flagged.argtypes = [ci, ci, ci, ctypes.c_uint, vp, vp, vp]
@@ -653,6 +656,15 @@ def tune_clock_stamp(out) -> None:
     dev = out.device if out.is_cuda else torch.device("cuda", torch.cuda.current_device())
     with torch.cuda.device(dev):
         _check(load_library().pcm_tune_clock_stamp(_ptr(out), _stream(dev)), "pcm_tune_clock_stamp")
+
+
+def tune_clock_rate(out, iters: int = 20000) -> None:
+    """Internal (tools/clock_state.py): one wave runs `iters` dependent FMAs on
+    the current stream and writes (s_memrealtime ticks, s_memtime ticks) over
+    them to out[0:2] (int64, device); the ratio x 0.1 is the shader clock in
+    GHz while it ran."""
+    with torch.cuda.device(out.device):
+        _check(load_library().pcm_tune_clock_rate(_ptr(out), int(iters), _stream(out.device)), "pcm_tune_clock_rate")
 
 
 def tune_num_chamfer_loss_grad_variants() -> int:

@@ -102,6 +102,14 @@ for S in "$@"; do
     benchab) for i in 1 2; do for o in first last; do
                timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 --side-legs $o \
                    > "$O/bench_${o}_$i.json" 2> "$O/bench_${o}_$i.err" || exit 1; done; done ;;
+    gap) timeout -k 10 300 python -u tools/ab_bench_gap.py > "$O/ab_bench_gap.txt" 2>&1 &&
+         timeout -k 10 300 python -u tools/ab_bench_gap.py >> "$O/ab_bench_gap.txt" 2>&1 ;;
+    clock) timeout -k 10 300 python -u tools/clock_state.py 24 > "$O/clock_state.txt" 2>&1 ;;
+    stampsw) for w in 0 20 0 20; do
+               PCM_HIP_LIB=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_stamps.so \
+               PCM_HIP_TUNE_LIB=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_stamps.so STAMP_WARM=$w \
+                   timeout -k 10 300 python -u tools/stamp_filt.py fused 15 >> "$O/stamps_warm_cold.txt" 2>&1 || exit 1
+             done ;;
     probeev) timeout -k 10 300 python -u tools/probe_events.py > "$O/probe_events.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac

@@ -810,6 +810,39 @@ def warm_graphs(g_many, g_one, per, warmup, steps, run_steps, dev, world):
     return info
 
 
+def sustained_kernel_us(launch, dev, busy_ms=45.0, reps=200):
+    """Per-launch device time once the GPU has run the step back to back for
+    `busy_ms` (profiles/r06/clock_state_r06k.txt: after an idle second the
+    step takes 15.1-15.3 us per launch and settles at 13.5 us after ~30 ms of
+    load; the in-kernel stamps put the whole difference in the VALU-bound scan,
+    profiles/r06/stamps_warm_cold_r06k.txt).  Reported beside the headline,
+    never as it: the driver's 25-step command always runs in the first state."""
+    s = torch.cuda.current_stream(dev)
+    g = torch.cuda.CUDAGraph()
+    cs = torch.cuda.Stream(dev)
+    cs.wait_stream(s)
+    with torch.cuda.stream(cs):
+        launch()
+    s.wait_stream(cs)
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            launch()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    g.replay()
+    e1.record(s)
+    e1.synchronize()
+    per_replay_ms = max(e0.elapsed_time(e1), 1e-3)
+    for _ in range(int(busy_ms / per_replay_ms) + 1):  # queued back to back, no host gap
+        g.replay()
+    e0.record(s)
+    for _ in range(5):
+        g.replay()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) * 1000.0 / (5 * reps)
+
+
 def side_legs(args, dev, rank, world):
     """The legs reported beside the headline (ICP, the unchanged caller's call
     sequence, config 5, EMD), after the headline (default) or, with
@@ -985,10 +1018,12 @@ def main(argv=None):
     if step.fused:
         dom_kernel, dom_bytes = FUSED_KERNEL, FUSED_BYTES
         graph_kernel_us = kernel_avg_us(lambda: step(0), 200, dev)
+        sustained_us = sustained_kernel_us(lambda: step(0), dev)
         dom_us = region_us if not (args.eager or multi) else graph_kernel_us
     else:
         dom_kernel, dom_bytes, dom_us = FWD_KERNEL, FWD_BYTES, fwd_us
         graph_kernel_us = fwd_us
+        sustained_us = None
     dom_tflops = pairs_per_step * FLOP_PER_PAIR / (dom_us * 1e-6) / 1e12
     traffic = pmc_bytes(dom_kernel)
     out = {
@@ -1017,6 +1052,12 @@ def main(argv=None):
                          "HIP events on the kernel's stream around the timed region, per step"
                          if dom_us == region_us else "HIP events around a 200-launch hipGraph replay, per launch"),
                      "kernel_us_graph200": graph_kernel_us, "timed_region_gpu_us_per_step": region_us,
+                     "kernel_us_sustained": sustained_us,
+                     "frac_sustained": None if sustained_us is None else
+                     pairs_per_step * FLOP_PER_PAIR / (sustained_us * 1e-6) / 1e12 / FP32_VALU_PEAK_TFLOPS,
+                     "sustained_note": "kernel_us_sustained: per launch after ~45 ms of back-to-back steps (a GPU "
+                                       "busy as in a training loop); the headline's short region runs on a GPU "
+                                       "that was idle, whose VALU-bound scan is ~25% slower (DESIGN.md section 5)",
                      "note": "FLOPs = 8 per point pair (algorithmic); VALU-bound, see DESIGN.md"},
         "roofline_hbm": {"bound": "hbm", "kernel": dom_kernel, "rank": rank,
                          "achieved": dom_bytes / (dom_us * 1e-6) / 1e9, "peak": HBM_PEAK_GBS,

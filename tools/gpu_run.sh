@@ -54,6 +54,10 @@ for S in "$@"; do
                2> "$GRAFT_REPO_ROOT/$O/rocprof.err") ;;
     abc) AB_VARIANTS=${AB_VARIANTS:-11,15} timeout -k 10 600 python -u tools/ab_chamfer.py > "$O/ab_chamfer.txt" 2>&1 &&
          AB_VARIANTS=${AB_VARIANTS:-11,15} timeout -k 10 600 python -u tools/ab_chamfer.py >> "$O/ab_chamfer.txt" 2>&1 ;;
+    abcc) AB_COLD=${AB_COLD:-0.3} AB_VARIANTS=${AB_VARIANTS:-11,15} timeout -k 10 600 python -u tools/ab_chamfer.py \
+               > "$O/ab_chamfer_cold.txt" 2>&1 &&
+          AB_COLD=${AB_COLD:-0.3} AB_VARIANTS=${AB_VARIANTS:-11,15} timeout -k 10 600 python -u tools/ab_chamfer.py \
+               >> "$O/ab_chamfer_cold.txt" 2>&1 ;;
     abe) timeout -k 10 600 python -u tools/ab_emd.py > "$O/ab_emd.txt" 2>&1 ;;
     grid) timeout -k 10 600 python -u -m pytest tests/test_chamfer_grid_gpu.py -m gpu -x -q --timeout 120 \
                --timeout-method thread > "$O/pytest_grid.txt" 2>&1 &&

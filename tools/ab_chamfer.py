@@ -20,7 +20,8 @@ from tune_chamfer import graph_of, time_graph_us  # noqa: E402
 
 def main():
     dev = torch.device("cuda:0")
-    b, n, m, reps, rounds = 32, 1024, 1024, 50, 7
+    b, n, m, reps = 32, 1024, 1024, 50
+    rounds = int(os.environ.get("AB_ROUNDS", "7"))
     # the bench's own clouds (bench.py ChamferStep, rank 0: seed BENCH_SEED = 1234)
     g = torch.Generator(device="cpu").manual_seed(1234)
     x1 = torch.rand(b, n, 3, generator=g).to(dev)
@@ -78,6 +79,9 @@ def main():
         lib += f" (cold: one 20-launch graph after {cold} s idle)"
     print(lib + ": " + ", ".join(f"v{v} {statistics.median(res[v]):.2f} us (min {min(res[v]):.2f}, same={same[v]})"
                                  for v in vs), flush=True)
+    if cold:  # the quartiles too: the driver's state spreads widely
+        print("  quartiles: " + ", ".join(
+            f"v{v} " + "/".join(f"{q:.2f}" for q in statistics.quantiles(res[v], n=4)) for v in vs), flush=True)
 
 
 if __name__ == "__main__":

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
     constexpr int kW = kSlabT / 64;
     __shared__ int hT[kSlabCells], hQ[kSlabCells];  // own slab: row-major / query-order histograms -> cursors
     __shared__ float red[7][kW];
-    __shared__ int sSlab[kSlabMax];
+    __shared__ int sBelow;  // points of the cloud in lower slabs
     __shared__ int sw[2][kW];
     // a cloud's slab workgroups share one XCD (pcm_xcd_remap): the cloud they
     // all read twice is fetched into that L2 only, not into all eight
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
         hT[i] = 0;
         hQ[i] = 0;
     }
-    if (tid < kSlabMax) sSlab[tid] = 0;
+    if (tid == 0) sBelow = 0;
     __syncthreads();
     float lo[3], ext = 0.f;
 #pragma unroll
@@ -212,10 +212,9 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
     }
     const int z0 = 4 * slab, kbase = slab * (G / 4) * (G / 4) * 64;  // first cell layer / query key of the slab
 
-    // 2. slab counts (ballots) and the own slab's histograms
-    int scnt[kSlabMax];
-#pragma unroll
-    for (int k = 0; k < kSlabMax; ++k) scnt[k] = 0;
+    // 2. the count of points in lower slabs (one ballot per point: only the
+    // own slab's offset is needed) and the own slab's histograms
+    int below = 0;
     for (int c0 = 0; c0 < np; c0 += kSlabK * kSlabT) {
         load(c0);
 #pragma unroll
@@ -225,8 +224,7 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
             const int ix = cell_axis(px[k], lo[0], inv, G), iy = cell_axis(py[k], lo[1], inv, G),
                       iz = cell_axis(pz[k], lo[2], inv, G);
             const int sl = iz >> 2;
-#pragma unroll
-            for (int q = 0; q < kSlabMax; ++q) scnt[q] += __popcll(__ballot(v && sl == q));
+            below += __popcll(__ballot(v && sl < slab));
             if (v && sl == slab) {
                 atomicAdd(&hT[((iz - z0) * G + iy) * G + ix], 1);
                 atomicAdd(&hQ[cell_query_key(ix, iy, iz, G) - kbase], 1);
@@ -235,14 +233,11 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
     }
     bad = wave_maxf(bad);
     if (lane == 0) {
-#pragma unroll
-        for (int q = 0; q < kSlabMax; ++q)
-            if (scnt[q]) atomicAdd(&sSlab[q], scnt[q]);
+        if (below) atomicAdd(&sBelow, below);
         red[6][w] = bad;  // read after the next barrier only
     }
     __syncthreads();
-    int soff = 0;
-    for (int q = 0; q < slab; ++q) soff += sSlab[q];
+    const int soff = sBelow;
     for (int i = 0; i < kW; ++i) bad = fmaxf(bad, red[6][i]);
 
     // 3. exclusive scans of both histograms (wave w: rows [w R, w R + R) of

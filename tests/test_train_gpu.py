@@ -86,6 +86,58 @@ def test_train_step_config4_workload_matches_oracle(cuda, oracle, epoch):
     assert logged[0] == pytest.approx(w[0] * cd + w[1] * emd, rel=1e-5)
 
 
+@pytest.mark.parametrize("epoch", [1, 31])
+def test_train_step_output_gradient_matches_oracle(cuda, oracle, epoch):
+    # the gradient the config-4 step hands the generator, d total / d fake
+    # (train.py:163-176), bit for bit: its Chamfer part from the oracle's
+    # restatement of the reference backward (chamfer3D.cu:155-195) fed
+    # graddist = fl(lambda_cd * fl(1/(B N))) -- torch's mean backward, pinned in
+    # test_chamfer_gpu.py::test_training_call_matches_oracle -- and its EMD
+    # part from the oracle's emd backward (emd_cuda.cu:284-316) fed the
+    # graddist torch's sqrt/mean backward handed emdFunction (captured); the
+    # two summed once, as autograd sums them.  Epoch 31 trains on EMD alone.
+    import emd_module
+    import loss as loss_mod
+    import pcm_hip
+    import train_step as T
+    cap = {}
+
+    class ProbeLoss(loss_mod.Loss):  # loss/loss.py's get_emd_loss, with its assignment and graddist kept
+        def get_emd_loss(self, pred, gt, radius=1.0, eps=0.05, iters=3000):
+            d, a = emd_module.emdModule()(pred, gt, eps=eps, iters=iters)
+            cap["assign"] = a.detach().clone()
+            d.register_hook(lambda g: cap.__setitem__("emd_gd", g.detach().clone()))
+            return torch.sqrt(d).mean(1).mean()
+
+    def keep_output(m, i, o):
+        cap["fake"] = o[2].detach().clone()
+        o[2].register_hook(lambda g: cap.__setitem__("grad", g.detach().clone()))
+
+    step = T.TrainStep(device=cuda, seed=3, loss_fn=ProbeLoss())
+    step.set_epoch(epoch)
+    images, points = T.synthetic_batch(16, 1024, cuda, seed=6)
+    hook = step.gen.register_forward_hook(keep_output)
+    step(images, points, epoch)
+    hook.remove()
+    torch.cuda.synchronize()
+    p, q = cap["fake"].transpose(2, 1).contiguous().cpu().numpy(), points.cpu().numpy()
+    b, n, m = p.shape[0], p.shape[1], q.shape[1]
+    _, ra = oracle.emd_forward(p, q, 0.05, 3000)
+    assign = cap["assign"].cpu().numpy()
+    assert np.array_equal(assign, ra)
+    expected = oracle.emd_backward(p, q, np.ascontiguousarray(cap["emd_gd"].cpu().numpy()), assign)
+    w_cd, _ = T.loss_weights(epoch, 100.0, 100.0)
+    if w_cd:
+        _, _, i1, i2 = oracle.chamfer_forward(p, q)
+        gd1 = np.float32(np.float32(w_cd) * np.float32(pcm_hip.mean_weight(b * n)))
+        gd2 = np.float32(np.float32(w_cd) * np.float32(pcm_hip.mean_weight(b * m)))
+        g1, _ = oracle.chamfer_backward(p, q, np.full((b, n), gd1, np.float32), np.full((b, m), gd2, np.float32),
+                                        i1, i2)
+        expected = (g1 + expected).astype(np.float32)  # one float32 rounding per element, order-free
+    got = cap["grad"].transpose(2, 1).contiguous().cpu().numpy()
+    np.testing.assert_array_equal(got.view(np.int32), expected.view(np.int32))
+
+
 @pytest.mark.parametrize("iters", [50, 400])
 def test_emd_training_setting_wide_clouds(cuda, oracle, iters):
     """EMD at the training call's eps (loss/loss.py:23) on predictions spread

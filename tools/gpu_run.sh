@@ -58,6 +58,10 @@ for S in "$@"; do
                > "$O/ab_chamfer_cold.txt" 2>&1 &&
           AB_COLD=${AB_COLD:-0.3} AB_VARIANTS=${AB_VARIANTS:-11,15} timeout -k 10 600 python -u tools/ab_chamfer.py \
                >> "$O/ab_chamfer_cold.txt" 2>&1 ;;
+    abgl) for r in 1 2 3; do for lib in base default; do
+              if [ $lib = base ]; then L=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_base.so; else L=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip.so; fi
+              PCM_HIP_LIB=$L timeout -k 10 120 python -u tools/ab_grid_libs.py >> "$O/ab_grid_libs.txt" 2>&1 || exit 1
+          done; done ;;
     abe) timeout -k 10 600 python -u tools/ab_emd.py > "$O/ab_emd.txt" 2>&1 ;;
     grid) timeout -k 10 600 python -u -m pytest tests/test_chamfer_grid_gpu.py -m gpu -x -q --timeout 120 \
                --timeout-method thread > "$O/pytest_grid.txt" 2>&1 &&

@@ -215,6 +215,10 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
     // 2. the count of points in lower slabs (one ballot per point: only the
     // own slab's offset is needed) and the own slab's histograms
     int below = 0;
+    // a cloud of one chunk stays in this thread's registers for pass 4, with
+    // its own-slab points' cells (packed x | y << 5 | z << 10; -1: not own)
+    const bool one = np <= kSlabK * kSlabT;
+    int ck[kSlabK];
     for (int c0 = 0; c0 < np; c0 += kSlabK * kSlabT) {
         load(c0);
 #pragma unroll
@@ -225,6 +229,7 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
                       iz = cell_axis(pz[k], lo[2], inv, G);
             const int sl = iz >> 2;
             below += __popcll(__ballot(v && sl < slab));
+            ck[k] = (v && sl == slab) ? (ix | (iy << 5) | (iz << 10)) : -1;
             if (v && sl == slab) {
                 atomicAdd(&hT[((iz - z0) * G + iy) * G + ix], 1);
                 atomicAdd(&hQ[cell_query_key(ix, iy, iz, G) - kbase], 1);
@@ -280,7 +285,18 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
     __syncthreads();
 
     // 4. the own slab's points into both copies
-    for (int c0 = 0; c0 < np; c0 += kSlabK * kSlabT) {
+    if (one) {
+#pragma unroll
+        for (int k = 0; k < kSlabK; ++k) {
+            if (ck[k] >= 0) {
+                const int ix = ck[k] & 31, iy = (ck[k] >> 5) & 31, iz = ck[k] >> 10;
+                const pcm_f4 v = pcm_f4{px[k], py[k], pz[k], __int_as_float(k * kSlabT + tid)};
+                tpts[off + atomicAdd(&hT[((iz - z0) * G + iy) * G + ix], 1)] = v;
+                qpts[off + atomicAdd(&hQ[cell_query_key(ix, iy, iz, G) - kbase], 1)] = v;
+            }
+        }
+    }
+    for (int c0 = 0; c0 < (one ? 0 : np); c0 += kSlabK * kSlabT) {
         load(c0);
 #pragma unroll
         for (int k = 0; k < kSlabK; ++k) {

@@ -162,15 +162,28 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
         }
     };
 
-    // 1. the grid's box from a strided sample of kSlabT points (every
-    // workgroup of the cloud computes the same bits).  Any box is exact: a
-    // point outside it is clamped into a boundary cell, which only moves it
-    // farther inside the cell range than it is, and the region proof holds
-    // for it as for every other point of that cell (search kernel).  The
-    // non-finite flag needs every point: pass 2.
+    // 1. the grid's box (every workgroup of the cloud computes the same
+    // bits): over the whole cloud when it is one chunk -- loaded here, once,
+    // for the box and passes 2 and 4 -- else over a strided sample of kSlabT
+    // points.  Any box is exact: a point outside it is clamped into a boundary
+    // cell, which only moves it farther inside the cell range than it is, and
+    // the region proof holds for it as for every other point of that cell
+    // (search kernel).  The non-finite flag needs every point: pass 2.
+    const bool one = np <= kSlabK * kSlabT;
     float mn[3] = {PCM_INF, PCM_INF, PCM_INF}, mx[3] = {-PCM_INF, -PCM_INF, -PCM_INF}, bad = 0.f;
-    {
-        const int i = np >= kSlabT ? (int)(((long long)tid * np) / kSlabT) : min(tid, np - 1);
+    if (one) {
+        load(0);  // (clamped: padding repeats the last point, which the box holds anyway)
+#pragma unroll
+        for (int k = 0; k < kSlabK; ++k) {
+            mn[0] = fminf(mn[0], px[k]);
+            mn[1] = fminf(mn[1], py[k]);
+            mn[2] = fminf(mn[2], pz[k]);
+            mx[0] = fmaxf(mx[0], px[k]);
+            mx[1] = fmaxf(mx[1], py[k]);
+            mx[2] = fmaxf(mx[2], pz[k]);
+        }
+    } else {
+        const int i = (int)(((long long)tid * np) / kSlabT);
         const float x = pcm_ld(src + 3 * i), y = pcm_ld(src + 3 * i + 1), z = pcm_ld(src + 3 * i + 2);
         mn[0] = mx[0] = x;
         mn[1] = mx[1] = y;
@@ -217,10 +230,9 @@ __global__ __launch_bounds__(kSlabT) void grid_build_kernel(const TIn *__restric
     int below = 0;
     // a cloud of one chunk stays in this thread's registers for pass 4, with
     // its own-slab points' cells (packed x | y << 5 | z << 10; -1: not own)
-    const bool one = np <= kSlabK * kSlabT;
     int ck[kSlabK];
     for (int c0 = 0; c0 < np; c0 += kSlabK * kSlabT) {
-        load(c0);
+        if (!one) load(c0);
 #pragma unroll
         for (int k = 0; k < kSlabK; ++k) {
             const bool v = c0 + k * kSlabT + tid < np;

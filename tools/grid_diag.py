@@ -68,6 +68,28 @@ def main():
         print(f"  placement: {int((ucnt > 0).sum().item())} distinct (xcc, se, sh, cu) units, waves per unit "
               f"min {int(ucnt[ucnt > 0].min().item())} max {int(ucnt.max().item())}; xcc counts "
               f"{torch.bincount(xcc, minlength=8).tolist()}", flush=True)
+        # where the late starts are: by XCD, and by the wave's slot inside its
+        # workgroup (stamps are indexed by workgroup * waves + slot)
+        full = 16 * 256  # launch_grid's rule (csrc/chamfer_grid.hip): 16-wave workgroups iff 3/4 full <= waves <= full
+        kw = 16 if full * 3 // 4 <= len(st0) <= full else 4
+        slot = torch.arange(len(st0), device=st0.device) % kw
+        print("  start median/max by xcc (us): " + " ".join(
+            f"{torch.quantile(st0[xcc == x], 0.5).item():.2f}/{st0[xcc == x].max().item():.2f}"
+            for x in range(8) if bool((xcc == x).any())), flush=True)
+        print(f"  start median by wave slot (of {kw}): " + " ".join(
+            f"{torch.quantile(st0[slot == j], 0.5).item():.2f}" for j in range(kw)), flush=True)
+        # the search alone (after a synchronize): its XCDs' start skew without the build before it
+        st_s = torch.zeros_like(st_all)
+        torch.cuda.synchronize()
+        pcm_hip.tune_chamfer_forward_grid(x1, x2, d1, d2, i1, i2, only="search", stats=st_s, workspace=ws)
+        torch.cuda.synchronize()
+        s2 = st_s[waves * 4:].view(waves, 8).cpu().long() & 0xffffffff
+        a0 = (s2[:, 0] - s2[:, 0].min()).float() * 0.01
+        x2c = s2[:, 7] & 0xf
+        print("  search alone: start median/max by xcc (us): " + " ".join(
+            f"{torch.quantile(a0[x2c == x], 0.5).item():.2f}/{a0[x2c == x].max().item():.2f}"
+            for x in range(8) if bool((x2c == x).any())) +
+            f"; last end {((s2[:, 5] - s2[:, 0].min()).float() * 0.01).max().item():.2f}", flush=True)
         print(f"  candidates round 0 p50/p90/p99/max {[round(v) for v in torch.quantile(c0, q).tolist()]}, "
               f"all rounds {[round(v) for v in torch.quantile(ca, q).tolist()]}, mean {ca.mean().item():.0f}",
               flush=True)

@@ -436,7 +436,16 @@ def grad_scale_hint(dev: torch.device) -> torch.Tensor:
     key = (dev, _stream_id(dev))
     t = _scale_hints.get(key)
     if t is None:
-        t = _scale_hints[key] = torch.ones(1, dtype=torch.float32, device=dev)
+        last = _scale_hints.get(("last", dev))
+        if last is not None and torch.cuda.is_current_stream_capturing():
+            # a capture stream takes the device's last-used hint (the scale the
+            # eager warm-up learned): a new tensor's fill would be captured and
+            # reset the scale at every replay
+            t = last
+        else:
+            t = torch.ones(1, dtype=torch.float32, device=dev)
+        _scale_hints[key] = t
+    _scale_hints[("last", dev)] = t
     return t
 
 

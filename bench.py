@@ -480,7 +480,17 @@ def _time_call(call, dev, reps):
     graph.replay()
     graph.replay()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    k = max(1, reps // GRAPH_STEPS)
+    # warm replays for ~5 ms first: the eager loop above leaves the GPU mostly
+    # idle, and the first few ms of load run its VALU-bound kernels slower
+    # (DESIGN.md section 5); without them the leg's figure depended on which
+    # legs ran before it (profiles/r06/tc_order_r06ze.txt)
+    e0.record(s)
+    graph.replay()
+    e1.record(s)
+    e1.synchronize()
+    for _ in range(int(5.0 / max(e0.elapsed_time(e1), 1e-3)) + 1):
+        graph.replay()
+    k = max(5, reps // GRAPH_STEPS)
     e0.record(s)
     for _ in range(k):
         graph.replay()

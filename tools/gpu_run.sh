@@ -118,6 +118,11 @@ for S in "$@"; do
                PCM_HIP_TUNE_LIB=$PWD/3d-pointcloudreconstruction_amd/lib/libpcm_hip_stamps.so STAMP_WARM=$w \
                    timeout -k 10 300 python -u tools/stamp_filt.py fused 15 >> "$O/stamps_warm_cold.txt" 2>&1 || exit 1
              done ;;
+    tctg) for f in after before; do
+             (cd /tmp && TCT_GRAPH=5 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/tctg_$f" -o run \
+                 --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/training_call_trace.py" $f 20 \
+                 > "$GRAFT_REPO_ROOT/$O/tctg_$f.log" 2>&1) || exit 1
+         done ;;
     probeev) timeout -k 10 300 python -u tools/probe_events.py > "$O/probe_events.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac

@@ -56,6 +56,19 @@ def main():
         call()
     torch.cuda.synchronize(dev)
     print(f"{form}: {k} calls", flush=True)
+    if os.environ.get("TCT_GRAPH"):
+        # bench.py _time_call's captured form: a graph of bench.GRAPH_STEPS calls,
+        # two warm replays, then TCT_GRAPH timed replays (the trace separates
+        # the replays' kernels from the eager calls by time)
+        out = bench._time_call(call, dev, 20)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(bench.GRAPH_STEPS):
+                call()
+        for _ in range(int(os.environ["TCT_GRAPH"])):
+            g.replay()
+        torch.cuda.synchronize(dev)
+        print(f"{form}: _time_call {out}", flush=True)
 
 
 if __name__ == "__main__":

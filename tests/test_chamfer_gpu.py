@@ -928,6 +928,24 @@ def test_training_call_graph_capture(cuda, oracle):
     np.testing.assert_array_equal(got.view(np.int32), rg1.view(np.int32))
 
 
+def test_capture_stream_takes_the_learned_scale(cuda):
+    # a graph captured on a stream with no scale of its own aliases the
+    # device's last-used one (the eager warm-up's learned lambda) instead of
+    # allocating a new one, whose fill the graph would capture and replay
+    import pcm_hip
+    hint = pcm_hip.grad_scale_hint(cuda)
+    hint.fill_(100.0)
+    torch.cuda.synchronize()
+    seen = []
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=torch.cuda.Stream(cuda)):  # a stream no hint is keyed by yet
+        seen.append(pcm_hip.grad_scale_hint(cuda))
+        scratch = torch.zeros(1, device=cuda)  # (something to capture)
+    graph.replay()
+    torch.cuda.synchronize()
+    assert seen[0].data_ptr() == hint.data_ptr() and hint.item() == 100.0 and scratch.item() == 0.0
+
+
 @pytest.mark.parametrize("b,n,m,lays", [
     (32, 1024, 1024, (1, 0)),   # train.py:163: fake.transpose(2, 1) against the GT rows
     (32, 1024, 1024, (1, 1)),

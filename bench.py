@@ -111,6 +111,9 @@ def parse(argv=None):
                         "replays of the captured 20-step hipGraph (matched A/B: profiles/r06/ab_launch_form_r06c.txt)")
     p.add_argument("--two-launch", action="store_true",
                    help="step = fused-loss forward + backward kernel (not the one-launch loss+gradient)")
+    p.add_argument("--tune-variant", type=int, default=None,
+                   help="A/B only: the headline step runs this fused variant of the tuning build "
+                        "(libpcm_hip_tune.so) instead of the product entry; marked in config")
     p.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     p.add_argument("--side-legs", choices=("first", "last"), default="last",
                    help="run the legs reported beside the headline after its timed region (default) or before "
@@ -179,7 +182,7 @@ class ChamferStep:
     cross-rank all-reduce can take the losses of a whole graph of steps at once
     (one bucketed collective instead of one 8-byte collective per step)."""
 
-    def __init__(self, dev, world, seed, slots, fused=True):
+    def __init__(self, dev, world, seed, slots, fused=True, variant=None):
         g = torch.Generator(device="cpu").manual_seed(seed)
         self.xyz1 = torch.rand(B, N, 3, generator=g).to(dev)
         self.xyz2 = torch.rand(B, M, 3, generator=g).to(dev)
@@ -194,6 +197,9 @@ class ChamferStep:
         self.gx2 = torch.empty(B, M, 3, device=dev)
         self.w1, self.w2 = 1.0 / (world * B * N), 1.0 / (world * B * M)
         self.loss = torch.zeros(slots, 3, device=dev)
+        self.variant = variant
+        if variant is not None:
+            pcm_hip.load_tune_library()  # (workspace sized for the tuning build's variants too)
         self.ws = pcm_hip.chamfer_workspace(dev, B, N, M)
         self.world = world
         self.collective = dist.is_available() and dist.is_initialized()
@@ -203,7 +209,7 @@ class ChamferStep:
         if self.fused:
             # one launch: forward, deterministic mean(dist1), mean(dist2), and both gradients
             pcm_hip.chamfer_loss_grad(self.xyz1, self.xyz2, self.w1, self.w2, self.d1, self.d2, self.i1,
-                                      self.i2, self.loss[slot], self.gx1, self.gx2, self.ws)
+                                      self.i2, self.loss[slot], self.gx1, self.gx2, self.ws, variant=self.variant)
             return
         # forward + deterministic in-kernel mean(dist1), mean(dist2); then the backward
         pcm_hip.chamfer_forward_loss(self.xyz1, self.xyz2, self.d1, self.d2, self.i1, self.i2,
@@ -901,7 +907,8 @@ def main(argv=None):
             dist.init_process_group(args.dist_backend)
 
     per = 1 if args.eager else max(1, min(GRAPH_STEPS, args.steps))
-    step = ChamferStep(dev, world, seed=BENCH_SEED + rank, slots=per, fused=not args.two_launch)
+    step = ChamferStep(dev, world, seed=BENCH_SEED + rank, slots=per, fused=not args.two_launch,
+                       variant=args.tune_variant)
 
     def run_eager(k):
         for _ in range(k):
@@ -1052,7 +1059,8 @@ def main(argv=None):
         "config": {"workload": "Chamfer3D fwd+bwd (+loss sums, +RCCL all-reduce of every step's loss when N>1)",
                    "batch_per_gpu": B, "n_points": N, "m_points": M,
                    "global_batch": world * B, "parallelism": f"dp{world} (batch-sharded)",
-                   "launch": mode, "dist_backend": args.dist_backend if multi else None},
+                   "launch": mode, "dist_backend": args.dist_backend if multi else None,
+                   **({"tune_variant": args.tune_variant} if args.tune_variant is not None else {})},
         "roofline": {"bound": "valu", "kernel": dom_kernel,
                      "achieved": dom_tflops, "peak": FP32_VALU_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": dom_tflops / FP32_VALU_PEAK_TFLOPS, "traffic": traffic,

@@ -123,6 +123,10 @@ for S in "$@"; do
                  --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/training_call_trace.py" $f 20 \
                  > "$GRAFT_REPO_ROOT/$O/tctg_$f.log" 2>&1) || exit 1
          done ;;
+    benchv) for r in 1 2 3; do for v in ${BENCH_VARIANTS:-15 14 7}; do
+               timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-emd --no-dense \
+                   --no-icp --no-ref-call --tune-variant $v >> "$O/bench_variants.jsonl" 2>> "$O/bench_variants.err" || exit 1
+           done; done ;;
     probeev) timeout -k 10 300 python -u tools/probe_events.py > "$O/probe_events.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac

@@ -2000,8 +2000,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
     float *__restrict__ mean_out, float *__restrict__ grad1, float *__restrict__ grad2, int nblk1, int nblk2,
     GradWs ws, unsigned max_spins, unsigned poll_spins, const float *__restrict__ gscale) {
-    static_assert((LAY1 == 0 && LAY2 == 0) || (kGran && kLocal && kG4 && !kEarly && !kMfma),
-                  "channel planes: the local-gradient 4-byte granule form");
+    static_assert((LAY1 == 0 && LAY2 == 0) || (kGran && !kMfma),
+                  "channel planes: the granule forms (the LDS copies keep each cloud's layout)");
     constexpr int QW = 64 * QPT;
     constexpr int NT = 64 * W;
     static_assert(!kMfma || (W == 8 && QPT == 4 && TILE == kMfmaTile), "the MFMA forward's fixed geometry");
@@ -2085,16 +2085,19 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
             my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
                 first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
-                first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, nullptr, tag, nullptr, sQown,
-                first ? L1 : L2, first ? L2 : L1, first ? H1 : H2, tag4, &myk, g4x);
+                first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, kG4 ? nullptr : (first ? G1 : G2),
+                tag, kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, first ? L1 : L2, first ? L2 : L1,
+                kG4 ? (first ? H1 : H2) : nullptr, tag4, kG4 ? &myk : nullptr, g4x);
         } else if (first) {  // mixed layouts: each direction's strides known at compile time
             my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
-                X1, X2, n, m, q0, dist1 + (size_t)batch * n, idx1 + (size_t)batch * n, arena, nullptr, tag, nullptr,
-                sQown, L1, L2, H1, tag4, &myk, g4x);
+                X1, X2, n, m, q0, dist1 + (size_t)batch * n, idx1 + (size_t)batch * n, arena, kG4 ? nullptr : G1, tag,
+                kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, L1, L2, kG4 ? H1 : nullptr, tag4,
+                kG4 ? &myk : nullptr, g4x);
         } else {
             my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
-                X2, X1, m, n, q0, dist2 + (size_t)batch * m, idx2 + (size_t)batch * m, arena, nullptr, tag, nullptr,
-                sQown, L2, L1, H2, tag4, &myk, g4x);
+                X2, X1, m, n, q0, dist2 + (size_t)batch * m, idx2 + (size_t)batch * m, arena, kG4 ? nullptr : G2, tag,
+                kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, L2, L1, kG4 ? H2 : nullptr, tag4,
+                kG4 ? &myk : nullptr, g4x);
         }
         PCM_STAMP2(1);
         const float s = wave_sum(my_d);
@@ -2136,12 +2139,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         } else {
             const float *P1 = reinterpret_cast<const float *>(garena);
             const float *P2 = P1 + 3 * kGradCap;
+            // (the clouds' LDS copies keep their own layouts: an element's
+            // channel planes are one contiguous 3n-float block, as rows are)
             ok = first ? range_grad<NT, QW, true>(true, q0, n, m, P1, P2, g1, g2, nullptr, nullptr, G,
                                                   garena + 24 * kGradCap, G1, G2, tag, max_spins,
-                                                  ws.epoch + kGradSlowWord)
+                                                  ws.epoch + kGradSlowWord, nullptr, nullptr, -1, L1, L2, L1)
                        : range_grad<NT, QW, true>(false, q0, m, n, P2, P1, g2, g1, nullptr, nullptr, G,
                                                   garena + 24 * kGradCap, G2, G1, tag, max_spins,
-                                                  ws.epoch + kGradSlowWord);
+                                                  ws.epoch + kGradSlowWord, nullptr, nullptr, -1, L2, L1, L2);
         }
         if (!ok) {  // a workgroup of this element never published: sticky error, NaN gradients
             if (tid == 0) __hip_atomic_store(ws.epoch + kGradErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2334,12 +2339,16 @@ struct GradVariant {
     grad_kernel_t k;
     int waves, qpt;
 };
-// round 5: variant 15 (4-byte argmin granules, four per 16-byte write-through
-// store, the range's own argmins from the forward): the same time as 11
-// (13.56 vs 13.56 us same-box, profiles/r05/) with 3.03 MB of HBM-side traffic
-// per launch against 3.65 MB
-constexpr int kDefaultGradVariant = 15;
-#define PCM_GRAD_DEFAULT(L1, L2) chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true, L1, L2>
+// round 6: variant 7 (8-byte {tag, idx} argmin granules, both clouds copied
+// into LDS for the gradient phase) again.  Round 5 had made 15 the default
+// (4-byte granules, four per 16-byte write-through store, the gradient phase
+// on the forward's own LDS: 3.09 MB of HBM-side traffic per launch against
+// 3.65 MB) at the same time as 11; re-measured on the round-6 code, 7 is the
+// fastest in every state: 13.09-13.12 vs 13.44-13.49 us in tools/ab_chamfer.py
+// and 15.48-15.72 vs 15.79-15.99 us per step in the bench's own command
+// (profiles/r06/bench_variants_r06zk_zl.txt)
+constexpr int kDefaultGradVariant = 7;
+#define PCM_GRAD_DEFAULT(L1, L2) chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false, false, false, L1, L2>
 // The product library holds the default only; the measured alternatives are
 // compiled into the tuning build (make tune: -DPCM_TUNE, libpcm_hip_tune.so),
 // which tools/ and the variant tests load.
@@ -2352,7 +2361,7 @@ const GradVariant kGradVariants[] = {
     {4, chamfer_loss_grad_kernel<8, 4, 32, 1024>, 8, 4},
     {5, chamfer_loss_grad_kernel<16, 4, 32, 1024>, 16, 4},
     {6, chamfer_loss_grad_kernel<8, 4, 16, 1024, true>, 8, 4},  // screen on the matrix cores
-    {7, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true>, 8, 4},  // granule hand-off
+    // 7: the granule hand-off (the default, below)
     {8, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, true>, 8, 4},  // 7 + the clouds copied during the scan
     {9, chamfer_loss_grad_kernel<8, 4, 8, 1024, false, true>, 8, 4},   // 7 with 8-candidate chunks
     {10, chamfer_loss_grad_kernel<8, 4, 32, 1024, false, true>, 8, 4},  // 7 with 32-candidate chunks
@@ -2367,8 +2376,10 @@ const GradVariant kGradVariants[] = {
     // 14: 11 with 4-byte argmin granules and the range's own argmins taken
     // from the forward (half the hand-off bytes, no own-range granule reads)
     {14, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true>, 8, 4},
+    // 15: 14 with four granules per 16-byte write-through store (a quarter of
+    // the fabric writes; the round-5 default)
+    {15, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true>, 8, 4},
 #endif
-    // 15: 14 with four granules per 16-byte write-through store (a quarter of the fabric writes)
     {kDefaultGradVariant, PCM_GRAD_DEFAULT(0, 0), 8, 4},
 };
 // the default variant with cloud 1 / cloud 2 in channel planes (index 2 lay1 + lay2)
@@ -2378,8 +2389,8 @@ const grad_kernel_t kGradDefaultLay[4] = {PCM_GRAD_DEFAULT(0, 0), PCM_GRAD_DEFAU
 // the mixed-layout instances with one inlined forward (strides in registers)
 const grad_kernel_t kGradLayOne[4] = {
     PCM_GRAD_DEFAULT(0, 0),
-    chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true, 0, 1, true>,
-    chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true, 1, 0, true>,
+    chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false, false, false, 0, 1, true>,
+    chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false, false, false, 1, 0, true>,
     PCM_GRAD_DEFAULT(1, 1)};
 #endif
 #undef PCM_GRAD_DEFAULT

@@ -683,7 +683,7 @@ def tune_num_chamfer_loss_grad_variants() -> int:
 
 
 # the product library's one-launch step (csrc/chamfer_filt.hip kDefaultGradVariant)
-DEFAULT_LOSS_GRAD_VARIANT = 15
+DEFAULT_LOSS_GRAD_VARIANT = 7
 
 
 def mean_weight(count: int) -> float:

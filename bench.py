@@ -71,7 +71,7 @@ BENCH_SEED = 1234                  # rank r's clouds: torch.Generator seed BENCH
 # up in for roofline.traffic (tools/pmc_passes.sh + tools/pmc_summarize.py)
 FWD_KERNEL = "chamfer_fwd_filt_kernel<float, 8, 4, 16, 1024, 3>"  # default fused-loss forward (clouds <= 1024)
 BWD_KERNEL = "chamfer_bwd_slots_kernel"
-FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true, 0, 0, false>"  # default variant 15 (4-byte granules in 16-byte stores, local gradient data)
+FUSED_KERNEL = "chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false, false, false, 0, 0, false>"  # default variant 7 (8-byte argmin granules, both clouds copied into LDS for the gradient phase)
 # the newest committed counter summary (profiles/rNN/pmc_summary.json)
 PMC_SUMMARY = next((p for p in (os.path.join(REPO, "profiles", r, "pmc_summary.json") for r in ("r06", "r05"))
                     if os.path.exists(p)), os.path.join(REPO, "profiles", "r05", "pmc_summary.json"))

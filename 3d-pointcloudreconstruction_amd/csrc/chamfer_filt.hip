@@ -2447,7 +2447,7 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
     if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
     if ((unsigned)lay1 > 1u || (unsigned)lay2 > 1u) return PCM_ERR_INVALID_ARG;
     const GradVariant *v = find_grad_variant(variant);
-    if (!v) return variant >= 0 && variant <= 15 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // 0-14: tuning build
+    if (!v) return variant >= 0 && variant <= 15 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // all but 7: tuning build
     if ((lay1 | lay2) && variant != kDefaultGradVariant) return PCM_ERR_UNSUPPORTED;
     if (!xyz1 || !xyz2 || !dist1 || !dist2 || !idx1 || !idx2 || !mean_out || !grad1 || !grad2 || !workspace)
         return PCM_ERR_INVALID_ARG;

@@ -127,6 +127,9 @@ for S in "$@"; do
                timeout -k 10 300 python -u bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --no-emd --no-dense \
                    --no-icp --no-ref-call --tune-variant $v >> "$O/bench_variants.jsonl" 2>> "$O/bench_variants.err" || exit 1
            done; done ;;
+    bench3) for r in 1 2 3; do
+              timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_$r.json" 2> "$O/bench_$r.err" || exit 1
+            done ;;
     probeev) timeout -k 10 300 python -u tools/probe_events.py > "$O/probe_events.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac

@@ -2141,6 +2141,16 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
             const float *P2 = P1 + 3 * kGradCap;
             // (the clouds' LDS copies keep their own layouts: an element's
             // channel planes are one contiguous 3n-float block, as rows are)
+            if constexpr (kG4)  // 4-byte granules; the range's own argmins from its forward
+                ok = first ? range_grad<NT, QW, true, 0, true>(true, q0, n, m, P1, P2, g1, g2, nullptr, nullptr, G,
+                                                               garena + 24 * kGradCap, H1, H2, tag4, max_spins,
+                                                               ws.epoch + kGradSlowWord, nullptr, nullptr, myk, L1,
+                                                               L2, L1)
+                           : range_grad<NT, QW, true, 0, true>(false, q0, m, n, P2, P1, g2, g1, nullptr, nullptr, G,
+                                                               garena + 24 * kGradCap, H2, H1, tag4, max_spins,
+                                                               ws.epoch + kGradSlowWord, nullptr, nullptr, myk, L2,
+                                                               L1, L2);
+            else
             ok = first ? range_grad<NT, QW, true>(true, q0, n, m, P1, P2, g1, g2, nullptr, nullptr, G,
                                                   garena + 24 * kGradCap, G1, G2, tag, max_spins,
                                                   ws.epoch + kGradSlowWord, nullptr, nullptr, -1, L1, L2, L1)
@@ -2379,6 +2389,10 @@ const GradVariant kGradVariants[] = {
     // 15: 14 with four granules per 16-byte write-through store (a quarter of
     // the fabric writes; the round-5 default)
     {15, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, true, false, true, true>, 8, 4},
+    // 16: 7 (both clouds copied into LDS for the gradient phase) with 15's
+    // granule hand-off: 4-byte granules, four per 16-byte store, the range's
+    // own argmins from its forward
+    {16, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false, true, true>, 8, 4},
 #endif
     {kDefaultGradVariant, PCM_GRAD_DEFAULT(0, 0), 8, 4},
 };
@@ -2447,7 +2461,7 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
     if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
     if ((unsigned)lay1 > 1u || (unsigned)lay2 > 1u) return PCM_ERR_INVALID_ARG;
     const GradVariant *v = find_grad_variant(variant);
-    if (!v) return variant >= 0 && variant <= 15 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // all but 7: tuning build
+    if (!v) return variant >= 0 && variant <= 16 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // all but 7: tuning build
     if ((lay1 | lay2) && variant != kDefaultGradVariant) return PCM_ERR_UNSUPPORTED;
     if (!xyz1 || !xyz2 || !dist1 || !dist2 || !idx1 || !idx2 || !mean_out || !grad1 || !grad2 || !workspace)
         return PCM_ERR_INVALID_ARG;

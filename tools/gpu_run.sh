@@ -130,6 +130,15 @@ for S in "$@"; do
     bench3) for r in 1 2 3; do
               timeout -k 10 600 python -u bench.py --gpus 1 --steps 20 --warmup 5 > "$O/bench_$r.json" 2> "$O/bench_$r.err" || exit 1
             done ;;
+    pmcf) (cd /tmp && timeout -s KILL 90 rocprofv3 --pmc FETCH_SIZE -d "$GRAFT_REPO_ROOT/$O/pmcf_fetch" -o fetch \
+               --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/profile_kernels.py" fused ${PMC_VARIANTS:-7,16} \
+               > "$GRAFT_REPO_ROOT/$O/pmcf_fetch.log" 2>&1 &&
+           timeout -s KILL 90 rocprofv3 --pmc WRITE_SIZE -d "$GRAFT_REPO_ROOT/$O/pmcf_write" -o write \
+               --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/profile_kernels.py" fused ${PMC_VARIANTS:-7,16} \
+               > "$GRAFT_REPO_ROOT/$O/pmcf_write.log" 2>&1 &&
+           timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/pmcf_kt" -o kt \
+               --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/profile_kernels.py" fused ${PMC_VARIANTS:-7,16} \
+               > "$GRAFT_REPO_ROOT/$O/pmcf_kt.log" 2>&1) ;;
     probeev) timeout -k 10 300 python -u tools/probe_events.py > "$O/probe_events.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac

@@ -35,9 +35,37 @@ def emd_training_call():
     print("done")
 
 
+def fused_variants(spec):
+    """`profile_kernels.py fused 7,16`: 20 one-launch steps per tuning-build
+    variant at config 2 (bench clouds, seed 1234), each variant on a zeroed
+    workspace of its own (a granule format switch recomputes every argmin)."""
+    dev = torch.device("cuda:0")
+    B, N = 32, 1024
+    g = torch.Generator(device="cpu").manual_seed(1234)
+    x1 = torch.rand(B, N, 3, generator=g).to(dev)
+    x2 = torch.rand(B, N, 3, generator=g).to(dev)
+    d1, d2 = torch.empty(B, N, device=dev), torch.empty(B, N, device=dev)
+    i1 = torch.empty(B, N, dtype=torch.int32, device=dev)
+    i2 = torch.empty(B, N, dtype=torch.int32, device=dev)
+    gx1, gx2 = torch.empty(B, N, 3, device=dev), torch.empty(B, N, 3, device=dev)
+    mo = torch.empty(3, device=dev)
+    vs = [int(v) for v in spec.split(",")]
+    pcm_hip.tune_num_chamfer_loss_grad_variants()  # loads the tuning build
+    ws0 = pcm_hip.chamfer_workspace(dev, B, N, N)
+    for v in vs:
+        ws = torch.zeros_like(ws0)
+        for _ in range(20):
+            pcm_hip.chamfer_loss_grad(x1, x2, 1.0 / (B * N), 1.0 / (B * N), d1, d2, i1, i2, mo, gx1, gx2, ws,
+                                      variant=v)
+        torch.cuda.synchronize()
+    print("done")
+
+
 def main():
     if len(sys.argv) > 1 and sys.argv[1] == "emdtrain":
         return emd_training_call()
+    if len(sys.argv) > 2 and sys.argv[1] == "fused":
+        return fused_variants(sys.argv[2])
     dev = torch.device("cuda:0")
     g = torch.Generator().manual_seed(0)
     B, N = 32, 1024

@@ -2393,6 +2393,8 @@ const GradVariant kGradVariants[] = {
     // granule hand-off: 4-byte granules, four per 16-byte store, the range's
     // own argmins from its forward
     {16, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false, true, true>, 8, 4},
+    // 17: 16 with one 4-byte granule store per query lane (no gathering shuffles)
+    {17, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false, true, false>, 8, 4},
 #endif
     {kDefaultGradVariant, PCM_GRAD_DEFAULT(0, 0), 8, 4},
 };
@@ -2461,7 +2463,7 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
     if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
     if ((unsigned)lay1 > 1u || (unsigned)lay2 > 1u) return PCM_ERR_INVALID_ARG;
     const GradVariant *v = find_grad_variant(variant);
-    if (!v) return variant >= 0 && variant <= 16 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // all but 7: tuning build
+    if (!v) return variant >= 0 && variant <= 17 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // all but 7: tuning build
     if ((lay1 | lay2) && variant != kDefaultGradVariant) return PCM_ERR_UNSUPPORTED;
     if (!xyz1 || !xyz2 || !dist1 || !dist2 || !idx1 || !idx2 || !mean_out || !grad1 || !grad2 || !workspace)
         return PCM_ERR_INVALID_ARG;

@@ -139,6 +139,8 @@ for S in "$@"; do
            timeout -k 10 120 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/pmcf_kt" -o kt \
                --output-format csv -- python3 "$GRAFT_REPO_ROOT/tools/profile_kernels.py" fused ${PMC_VARIANTS:-7,16} \
                > "$GRAFT_REPO_ROOT/$O/pmcf_kt.log" 2>&1) ;;
+    emdwarm) timeout -k 10 120 python -u tools/emd_warm_probe.py 6 50 > "$O/emd_warm.txt" 2>&1 &&
+             timeout -k 10 120 python -u tools/emd_warm_probe.py 6 200 >> "$O/emd_warm.txt" 2>&1 ;;
     probeev) timeout -k 10 300 python -u tools/probe_events.py > "$O/probe_events.txt" 2>&1 ;;
     *) echo "unknown step $S"; exit 2 ;;
     esac

@@ -43,6 +43,9 @@ def _verified_emd(a, c, ass):
     (3, 1024, 0.005, 1, 4),       # single (last) iteration: everyone takes its bid
     (2, 1024, 0.002, 10000, 5),   # metric/emd/README.md test-time setting (eps 0.002, 10000 iters)
     (20, 2048, 0.05, 3000, 6),    # metric/emd/test.py:7-11 (B=20, N=2048, eps 0.05, 3000 iters)
+    # the README setting at N=2048 does not converge: 4 bidders from iteration
+    # 8,113 to the end, whose last-iteration takes duplicate owned objects
+    (2, 2048, 0.002, 10000, 5),
 ])
 def test_emd_forward_matches_oracle(cuda, oracle, b, n, eps, iters, seed):
     a, c = _clouds(seed, b, n)

@@ -1994,7 +1994,7 @@ __device__ __forceinline__ void poll_grad_loss_wg(int b, int n, int m, int per, 
 // (pcm_chamfer_loss_grad_rescale checks it against the real one).
 template <int W, int QPT, int C, int TILE, bool kMfma = false, bool kGran = false, bool kEarly = false,
           bool kLocal = false, bool kSplit = false, bool kG4 = false, bool kG4x = false, int LAY1 = 0, int LAY2 = 0,
-          bool kLayOne = false>
+          bool kLayOne = false, bool kOwnK = false>
 __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void chamfer_loss_grad_kernel(
     const float *__restrict__ xyz1, const float *__restrict__ xyz2, int b, int n, int m, float w1, float w2,
     float *__restrict__ dist1, float *__restrict__ dist2, int32_t *__restrict__ idx1, int32_t *__restrict__ idx2,
@@ -2080,24 +2080,24 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
                 first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, kG4 ? nullptr : (first ? G1 : G2),
                 tag, kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, LQ,
                 LAY1 ? PcmLay{1, first ? m : n} : PcmLay{3, 1}, kG4 ? (first ? H1 : H2) : nullptr, tag4,
-                kG4 ? &myk : nullptr, g4x);
+                (kG4 || kOwnK) ? &myk : nullptr, g4x);
         } else if (kLayOne) {  // mixed layouts, one inlined forward with the strides in registers (tuning A/B)
             my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 first ? X1 : X2, first ? X2 : X1, first ? n : m, first ? m : n, q0,
                 first ? dist1 + (size_t)batch * n : dist2 + (size_t)batch * m,
                 first ? idx1 + (size_t)batch * n : idx2 + (size_t)batch * m, arena, kG4 ? nullptr : (first ? G1 : G2),
                 tag, kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, first ? L1 : L2, first ? L2 : L1,
-                kG4 ? (first ? H1 : H2) : nullptr, tag4, kG4 ? &myk : nullptr, g4x);
+                kG4 ? (first ? H1 : H2) : nullptr, tag4, (kG4 || kOwnK) ? &myk : nullptr, g4x);
         } else if (first) {  // mixed layouts: each direction's strides known at compile time
             my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 X1, X2, n, m, q0, dist1 + (size_t)batch * n, idx1 + (size_t)batch * n, arena, kG4 ? nullptr : G1, tag,
                 kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, L1, L2, kG4 ? H1 : nullptr, tag4,
-                kG4 ? &myk : nullptr, g4x);
+                (kG4 || kOwnK) ? &myk : nullptr, g4x);
         } else {
             my_d = filt_forward<float, W, QPT, C, TILE, false, kSplit>(
                 X2, X1, m, n, q0, dist2 + (size_t)batch * m, idx2 + (size_t)batch * m, arena, kG4 ? nullptr : G2, tag,
                 kEarly ? &pre : nullptr, kLocal ? sQown : nullptr, L2, L1, kG4 ? H2 : nullptr, tag4,
-                kG4 ? &myk : nullptr, g4x);
+                (kG4 || kOwnK) ? &myk : nullptr, g4x);
         }
         PCM_STAMP2(1);
         const float s = wave_sum(my_d);
@@ -2153,10 +2153,10 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
             else
             ok = first ? range_grad<NT, QW, true>(true, q0, n, m, P1, P2, g1, g2, nullptr, nullptr, G,
                                                   garena + 24 * kGradCap, G1, G2, tag, max_spins,
-                                                  ws.epoch + kGradSlowWord, nullptr, nullptr, -1, L1, L2, L1)
+                                                  ws.epoch + kGradSlowWord, nullptr, nullptr, kOwnK ? myk : -1, L1, L2, L1)
                        : range_grad<NT, QW, true>(false, q0, m, n, P2, P1, g2, g1, nullptr, nullptr, G,
                                                   garena + 24 * kGradCap, G2, G1, tag, max_spins,
-                                                  ws.epoch + kGradSlowWord, nullptr, nullptr, -1, L2, L1, L2);
+                                                  ws.epoch + kGradSlowWord, nullptr, nullptr, kOwnK ? myk : -1, L2, L1, L2);
         }
         if (!ok) {  // a workgroup of this element never published: sticky error, NaN gradients
             if (tid == 0) __hip_atomic_store(ws.epoch + kGradErrWord, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2395,6 +2395,9 @@ const GradVariant kGradVariants[] = {
     {16, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false, true, true>, 8, 4},
     // 17: 16 with one 4-byte granule store per query lane (no gathering shuffles)
     {17, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false, true, false>, 8, 4},
+    // 18: 7 with the range's own argmins from its forward (8-byte granules, no
+    // own-range granule reads)
+    {18, chamfer_loss_grad_kernel<8, 4, 16, 1024, false, true, false, false, false, false, false, 0, 0, false, true>, 8, 4},
 #endif
     {kDefaultGradVariant, PCM_GRAD_DEFAULT(0, 0), 8, 4},
 };
@@ -2463,7 +2466,7 @@ int launch_loss_grad(int variant, const float *xyz1, const float *xyz2, int b, i
     if (n > kGradCap || m > kGradCap) return PCM_ERR_UNSUPPORTED;
     if ((unsigned)lay1 > 1u || (unsigned)lay2 > 1u) return PCM_ERR_INVALID_ARG;
     const GradVariant *v = find_grad_variant(variant);
-    if (!v) return variant >= 0 && variant <= 17 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // all but 7: tuning build
+    if (!v) return variant >= 0 && variant <= 18 ? PCM_ERR_UNSUPPORTED : PCM_ERR_INVALID_ARG;  // all but 7: tuning build
     if ((lay1 | lay2) && variant != kDefaultGradVariant) return PCM_ERR_UNSUPPORTED;
     if (!xyz1 || !xyz2 || !dist1 || !dist2 || !idx1 || !idx2 || !mean_out || !grad1 || !grad2 || !workspace)
         return PCM_ERR_INVALID_ARG;

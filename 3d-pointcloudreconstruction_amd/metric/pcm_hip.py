@@ -18,7 +18,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get(
     "PCM_HIP_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libpcm_hip.so"))
 # the tuning build (make -C csrc tune): the product library plus the measured
-# alternatives of the one-launch Chamfer step (fused variants 0-17 beside the default 7), which
+# alternatives of the one-launch Chamfer step (fused variants 0-18 beside the default 7), which
 # tools/ and the variant tests select by number; never on the product path
 TUNE_LIB_PATH = os.environ.get(
     "PCM_HIP_TUNE_LIB", os.path.join(os.path.dirname(_HERE), "lib", "libpcm_hip_tune.so"))
@@ -63,7 +63,7 @@ def load_library():
 
 
 def load_tune_library():
-    """Load libpcm_hip_tune.so, the tuning build (fused variants 0-17 beside
+    """Load libpcm_hip_tune.so, the tuning build (fused variants 0-18 beside
     the default); raises OSError if it is missing."""
     global _tune_lib
     if _tune_lib is None:
